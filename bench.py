@@ -1,0 +1,184 @@
+"""Throughput benchmark: message-passing edges/s, RouteNet synth50 batched (BASELINE.json).
+
+One "step" = one full forward of the engine over one batch (hidden-state init, T=8
+iterations of link->path ordered GRU + path->link sum GRU, readout MLP) with every input
+already resident in HBM.  edges per step = B x T x sum_mp sum_src |adj|.
+
+Multi-GPU (torchrun): one process per GPU, each rank owns its own batch of 512 graphs
+(graph-sharded, weak scaling; the forward has no data-path collective).  Timing: barrier +
+device sync on both sides of exactly K steps; the max over ranks is reported.
+
+Extra objects on the JSON line:
+  roofline      dominant kernel (seq_gru), algorithmic FLOPs per launch / average launch
+                time from HIP events recorded on the engine stream over the timed region;
+                peak = fp32 MFMA 157.3 TFLOP/s (MI355X_MICROARCH.md); traffic = HBM bytes per
+                launch from the committed rocprofv3 PMC summary (profiles/), or null.
+  cpu_baseline  the dense-padded oracle (oracle/dense_forward.py, float32 numpy, the TF op
+                sequence incl. padded work) on a bounded sample of the same workload, rank 0, N=1.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "message-passing edges/sec, RouteNet synth50 batched, 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--graphs", type=int, default=512, help="graphs per GPU")
+    ap.add_argument("--topology", default="synth50")
+    ap.add_argument("--model", default="routenet", choices=["routenet", "qsize"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
+    return ap.parse_args()
+
+
+def load_traffic(kernel_kind, workload):
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(workload, {}).get(kernel_kind, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(desc, dims, prm, graphs, budget_s):
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+
+    from ignnition_amd import workloads
+    from ignnition_amd.json_operations import Model_information
+    from oracle.dense_forward import DenseOracle
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    ora = DenseOracle(desc, dims, prm, dtype=np.float32)
+    mi = Model_information(desc, dims)
+    done, edges = 0, 0
+    with threadpool_limits(limits=threads):
+        ora.forward(graphs[:1])  # warm-up
+        t0 = time.perf_counter()
+        while done < len(graphs):
+            ora.forward([graphs[done]])
+            edges += workloads.edges_per_forward(mi, [graphs[done]])
+            done += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": edges / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": "%d of the %d synth50 graphs, full T=8 forward each, dense-padded numpy float32 oracle "
+                      "(TF op sequence incl. padded rows), %.1f s" % (done, len(graphs), dt)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import numpy as np
+
+    from ignnition_amd import workloads
+    from ignnition_amd.engine import Batch, Engine, MPPlan
+
+    def barrier_sync(eng):
+        eng.synchronize()
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    # per-rank shard: graphs [rank*G, (rank+1)*G) -> weak scaling, no forward collective
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(args.model, args.topology, args.graphs,
+                                                            first_id=rank * args.graphs)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(seed=0, bias_scale=0.05)
+    eng = Engine(plan, local if world > 1 else 0)
+    eng.set_params(prm)
+    batch = Batch(eng, graphs)
+    edges = batch.edges_per_forward
+
+    for _ in range(args.warmup):
+        batch.forward(to_host=False)
+    barrier_sync(eng)
+    eng.set_timing(not args.no_timing)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.forward(to_host=False)
+    barrier_sync(eng)
+    dt = time.perf_counter() - t0
+    stats = eng.stats()
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    total_edges = edges * args.steps * world
+    value = total_edges / dt
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    workload = "%s_%s_x%d" % (args.model, args.topology, args.graphs)
+    roof = None
+    if not args.no_timing:
+        dom = max(("seq_gru", "sum_gru", "readout"), key=lambda k: stats[k]["ms"])
+        s = stats[dom]
+        launches = max(s["launches"], 1)
+        avg_s = s["ms"] / launches / 1e3
+        flops_launch = s["flops"] / launches
+        achieved = flops_launch / avg_s / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                "traffic": load_traffic(dom, workload),
+                "alg_bytes_per_launch": s["bytes"] / launches,
+                "avg_launch_ms": round(s["ms"] / launches, 4),
+                "hbm_frac_alg": round(s["bytes"] / launches / avg_s / 1e9 / PEAK_HBM_GBS, 4),
+                "kernels": {k: {"launches": v["launches"], "ms_total": round(v["ms"], 3),
+                                "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2),
+                                "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                            for k, v in stats.items() if v["launches"]}}
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
+    line = {
+        "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic: random %s-size topologies (networkx gnm, shortest-path routing, PCG64 seed "
+                "20261015+graph_id), migrate.py sample layout, random-init weights" % args.topology,
+        "config": {"workload": workload, "model": args.model, "graphs_per_gpu": args.graphs,
+                   "global_batch": args.graphs * world, "hidden": plan.hidden[0], "iterations": plan.iterations,
+                   "edges_per_step_per_gpu": edges, "gru_steps_per_forward": batch.gru_steps_per_forward,
+                   "parallelism": "graph-sharded (%d ranks), no collective in the forward" % world},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

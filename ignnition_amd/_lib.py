@@ -1,0 +1,122 @@
+"""ctypes binding of libignmp.so (include/ignmp.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` / ``python -m ignnition_amd.build``.
+There is no fallback: if the shared object is missing or fails to load, importing this
+module raises, and every compute call goes through the HIP kernels or fails loudly.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libignmp.so")
+
+i32, i64, f32 = C.c_int32, C.c_int64, C.c_float
+
+
+class EntityDesc(C.Structure):
+    _fields_ = [("hidden_dim", i32), ("feature_total", i32)]
+
+
+class SourceDesc(C.Structure):
+    _fields_ = [("entity", i32), ("adjacency", i32), ("interleave", i32)]
+
+
+class MPDesc(C.Structure):
+    _fields_ = [("dst_entity", i32), ("aggregation", i32), ("concat_axis", i32), ("cell", i32),
+                ("num_sources", i32), ("sources", C.POINTER(SourceDesc))]
+
+
+class CellDesc(C.Structure):
+    _fields_ = [("input_dim", i32), ("units", i32)]
+
+
+class DenseDesc(C.Structure):
+    _fields_ = [("units", i32), ("activation", i32), ("use_bias", i32)]
+
+
+class PlanDesc(C.Structure):
+    _fields_ = [("num_iterations", i32), ("num_entities", i32), ("entities", C.POINTER(EntityDesc)),
+                ("num_adjacencies", i32), ("num_interleave", i32), ("num_mps", i32),
+                ("mps", C.POINTER(MPDesc)), ("num_cells", i32), ("cells", C.POINTER(CellDesc)),
+                ("num_readout_inputs", i32), ("readout_inputs", C.POINTER(i32)),
+                ("num_dense", i32), ("dense", C.POINTER(DenseDesc))]
+
+
+class BatchDesc(C.Structure):
+    _fields_ = [("num_graphs", i32), ("num_nodes", C.POINTER(i64)), ("features", C.POINTER(C.POINTER(f32))),
+                ("adj_edges", C.POINTER(i64)), ("adj_src", C.POINTER(C.POINTER(i64))),
+                ("adj_dst", C.POINTER(C.POINTER(i64))), ("adj_seq", C.POINTER(C.POINTER(i64))),
+                ("interleave_len", C.POINTER(i64)), ("interleave_idx", C.POINTER(C.POINTER(i64)))]
+
+
+class BatchInfo(C.Structure):
+    _fields_ = [("num_graphs", i64), ("predictions", i64), ("output_units", i64), ("edges_per_forward", i64),
+                ("gru_steps_per_forward", i64), ("rows", i64 * 8)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("kinds", i32), ("launches", i64 * 8), ("ms", C.c_double * 8), ("flops", C.c_double * 8),
+                ("bytes", C.c_double * 8)]
+
+
+KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "other"]
+
+AGGR = {"sum": 0, "ordered": 1, "interleave": 2, "concat": 3, "attention": 4, "convolution": 5}
+ACT = {None: 0, "None": 0, "linear": 0, "relu": 1, "selu": 2, "sigmoid": 3, "tanh": 4}
+
+# every symbol declared in include/ignmp.h
+SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_create", "ign_plan_destroy",
+           "ign_plan_num_params", "ign_plan_num_param_tensors", "ign_plan_param_tensor", "ign_plan_set_params",
+           "ign_plan_set_timing", "ign_plan_set_stream", "ign_batch_create", "ign_batch_destroy", "ign_batch_info",
+           "ign_forward", "ign_synchronize", "ign_batch_predictions", "ign_batch_state", "ign_stats"]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libignmp.so not built: run `python -m ignnition_amd.build` (or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    P, VP = C.POINTER, C.c_void_p
+    sig = {
+        "ign_abi_version": (C.c_int, []),
+        "ign_last_error": (C.c_char_p, []),
+        "ign_device_count": (C.c_int, [P(i32)]),
+        "ign_plan_create": (C.c_int, [P(PlanDesc), i32, P(VP)]),
+        "ign_plan_destroy": (None, [VP]),
+        "ign_plan_num_params": (C.c_int, [VP, P(i64)]),
+        "ign_plan_num_param_tensors": (C.c_int, [VP, P(i32)]),
+        "ign_plan_param_tensor": (C.c_int, [VP, i32, P(i32), P(i32), P(i64), P(i32), P(i32)]),
+        "ign_plan_set_params": (C.c_int, [VP, VP, i32]),
+        "ign_plan_set_timing": (C.c_int, [VP, i32]),
+        "ign_plan_set_stream": (C.c_int, [VP, VP]),
+        "ign_batch_create": (C.c_int, [VP, P(BatchDesc), P(VP)]),
+        "ign_batch_destroy": (None, [VP]),
+        "ign_batch_info": (C.c_int, [VP, P(BatchInfo)]),
+        "ign_forward": (C.c_int, [VP, VP, VP]),
+        "ign_synchronize": (C.c_int, [VP]),
+        "ign_batch_predictions": (C.c_int, [VP, P(VP)]),
+        "ign_batch_state": (C.c_int, [VP, VP, i32, VP]),
+        "ign_stats": (C.c_int, [VP, P(Stats)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libignmp error %d: %s" % (code, msg))
+        self.code = code
+
+
+def check(rc):
+    if rc != 0:
+        raise EngineError(rc, lib.ign_last_error().decode(errors="replace"))
+    return rc

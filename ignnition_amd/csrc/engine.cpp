@@ -1,0 +1,858 @@
+// engine.cpp — C ABI (include/ignmp.h), plan lowering, native batch builder, forward driver.
+//
+// Reference behaviour restated here (generate_model.py = GM, auxilary_classes.py = AUX):
+//  * hidden-state init per entity                                  GM:396-400, AUX:128-160
+//  * T iterations x stages x MPs, destination state overwritten
+//    after each MP (later MPs of a stage see it)                   GM:406-603
+//  * per-graph dense padding semantics of the combine step:
+//      lens = in-degree, Lmax = max(seq)+1 per graph and source,
+//      source k's slots start after sources 0..k-1's Lmax           GM:477-543
+//      interleave permutes slots through indices_<src>_to_<dst>    AUX:421-440, GM:507-519
+//      sorted update consumes positions 0..final_len-1 (holes are
+//      zero inputs, later positions dropped)                       AUX:767-796
+//    These become per-destination step tables (CSR) built here on the host, once per batch.
+//  * readout predict op (Dense stack)                              GM:611-629
+// Errors the reference raises at run time (e.g. gather_nd(-1) when final_len = 0, scatter_nd
+// with an out-of-range interleave index, an adjacency with no edges) are returned as
+// IGN_ERR_INVALID with a message.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/ignmp.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return fail(IGN_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e));    \
+  } while (0)
+
+enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_OTHER = 4, K_KINDS = 5 };
+
+struct Tensor {
+  int kind, owner;
+  int64_t offset;
+  int rows, cols;
+};
+
+struct CellP {
+  int din, H;
+  int64_t off_k, off_rk, off_b;   // raw Keras-layout params
+  int64_t pk_w, pk_u, pk_b;       // packed fragments (in d_packed)
+  bool used = false;
+};
+
+struct DenseP {
+  int in, out, act, use_bias;
+  int64_t off_w, off_b, pk_w;
+};
+
+struct MPP {
+  int dst, aggr, concat_axis, cell;
+  std::vector<ign_source_desc> src;
+  bool sorted;                    // sorted (sequence) update vs single-step update
+  int din;
+};
+
+}  // namespace
+
+struct ign_plan {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int T = 0;
+  std::vector<ign_entity_desc> ents;
+  int n_adj = 0, n_il = 0;
+  std::vector<MPP> mps;
+  std::vector<CellP> cells;
+  std::vector<int> ro_in;
+  std::vector<DenseP> dense;
+  std::vector<Tensor> tensors;
+  int64_t n_params = 0, n_packed = 0;
+  float* d_params = nullptr;
+  float* d_packed = nullptr;
+  bool params_set = false;
+  bool fused_readout = false;
+  int ro_width = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev;     // pairs
+  std::vector<int> ev_kind;
+  std::vector<double> ev_flops, ev_bytes;
+  ign_stats_t stats{};
+};
+
+namespace {
+
+struct MPB {
+  bool sorted = false;
+  int64_t n_dst = 0, n_steps = 0, n_msgs = 0, edges = 0;
+  int32_t* d_order = nullptr;
+  int32_t* d_len = nullptr;
+  int32_t* d_step_ptr = nullptr;
+  int32_t* d_msg_ptr = nullptr;
+  uint32_t* d_msg_src = nullptr;
+  double flops = 0, bytes = 0;    // algorithmic, per launch
+};
+
+}  // namespace
+
+struct ign_batch {
+  ign_plan* plan = nullptr;
+  int G = 0;
+  std::vector<int64_t> rows;                    // per entity
+  std::vector<std::vector<int64_t>> row_off;    // [entity][graph]
+  std::vector<float*> d_feat;                   // per entity [rows][F] or null
+  std::vector<float*> d_state[2];               // per entity ping-pong
+  std::vector<int> cur;
+  std::vector<MPB> mp;
+  float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
+  std::vector<float*> d_ro_tmp;                 // generic readout intermediates
+  float* d_pred = nullptr;
+  int64_t n_pred = 0, out_units = 1;
+  int64_t edges_per_forward = 0, gru_steps = 0;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+int set_device(int dev) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(IGN_ERR_DEVICE, "no HIP device available (%s)", e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+  if (dev < 0 || dev >= n) return fail(IGN_ERR_DEVICE, "device %d out of range (%d devices)", dev, n);
+  HIP_TRY(hipSetDevice(dev));
+  return IGN_OK;
+}
+
+int ensure_device(ign_plan* p) {
+  int rc = set_device(p->device);
+  if (rc) return rc;
+  if (!p->d_params) {
+    HIP_TRY(hipMalloc(&p->d_params, std::max<int64_t>(p->n_params, 1) * sizeof(float)));
+    HIP_TRY(hipMemset(p->d_params, 0, std::max<int64_t>(p->n_params, 1) * sizeof(float)));
+    HIP_TRY(hipMalloc(&p->d_packed, std::max<int64_t>(p->n_packed, 1) * sizeof(float)));
+  }
+  if (!p->stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    p->own_stream = true;
+  }
+  return IGN_OK;
+}
+
+template <typename T>
+int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
+  size_t n = std::max<size_t>(host.size(), 1);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+  b->allocs.push_back(p);
+  if (!host.empty()) HIP_TRY(hipMemcpy(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+  else HIP_TRY(hipMemset(p, 0, sizeof(T)));
+  *out = static_cast<T*>(p);
+  return IGN_OK;
+}
+
+int dev_alloc(ign_batch* b, float** out, int64_t n) {
+  void* p = nullptr;
+  // +64 floats of slack: kernels may read a whole (masked-off) row at index 0 of an empty table
+  hipError_t e = hipMalloc(&p, (std::max<int64_t>(n, 0) + 64) * sizeof(float));
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%lld floats): %s", (long long)n, hipGetErrorString(e));
+  b->allocs.push_back(p);
+  *out = static_cast<float*>(p);
+  return IGN_OK;
+}
+
+int act_ok(int a) { return a >= IGN_ACT_LINEAR && a <= IGN_ACT_TANH; }
+
+// Per-launch algorithmic cost: one GRU application = 2*3H*(DIN+H) + 14H flops.
+double gru_flops(int din, int H) { return 2.0 * 3 * H * (din + H) + 14.0 * H; }
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+int ign_abi_version(void) { return IGN_ABI_VERSION; }
+
+const char* ign_last_error(void) { return g_err.c_str(); }
+
+int ign_device_count(int32_t* n) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (n) *n = (e == hipSuccess) ? c : 0;
+  return IGN_OK;
+}
+
+int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
+  if (!d || !out) return fail(IGN_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (d->num_iterations <= 0) return fail(IGN_ERR_INVALID, "num_iterations must be > 0");
+  if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
+  std::unique_ptr<ign_plan> p(new ign_plan());
+  p->device = device;
+  p->T = d->num_iterations;
+  p->ents.assign(d->entities, d->entities + d->num_entities);
+  for (size_t e = 0; e < p->ents.size(); ++e) {
+    const auto& en = p->ents[e];
+    if (en.hidden_dim <= 0) return fail(IGN_ERR_INVALID, "entity %zu: hidden_state_dimension must be > 0", e);
+    if (en.feature_total > en.hidden_dim)   // AUX:155-159: zeros(H - total) needs total <= H
+      return fail(IGN_ERR_INVALID, "entity %zu: total feature size %d exceeds hidden_state_dimension %d", e,
+                  en.feature_total, en.hidden_dim);
+  }
+  p->n_adj = d->num_adjacencies;
+  p->n_il = d->num_interleave;
+  for (int c = 0; c < d->num_cells; ++c) {
+    CellP cp;
+    cp.din = d->cells[c].input_dim;
+    cp.H = d->cells[c].units;
+    p->cells.push_back(cp);
+  }
+  for (int m = 0; m < d->num_mps; ++m) {
+    const ign_mp_desc& md = d->mps[m];
+    MPP mp;
+    mp.dst = md.dst_entity;
+    mp.aggr = md.aggregation;
+    mp.concat_axis = md.concat_axis;
+    mp.cell = md.cell;
+    if (mp.dst < 0 || mp.dst >= d->num_entities) return fail(IGN_ERR_INVALID, "mp %d: bad destination", m);
+    if (md.num_sources <= 0) return fail(IGN_ERR_INVALID, "mp %d: no source entities", m);
+    if (md.num_sources > IGN_MAX_SLOTS)
+      return fail(IGN_ERR_UNSUPPORTED, "mp %d: more than %d source entities", m, IGN_MAX_SLOTS);
+    mp.src.assign(md.sources, md.sources + md.num_sources);
+    switch (mp.aggr) {
+      case IGN_AGGR_SUM: mp.sorted = false; break;
+      case IGN_AGGR_ORDERED: mp.sorted = true; break;
+      case IGN_AGGR_INTERLEAVE:
+        mp.sorted = true;
+        if (md.num_sources != 2)  // tf.stack of the index lists (GM:518) needs exactly two sources
+          return fail(IGN_ERR_UNSUPPORTED, "mp %d: interleave aggregation supports exactly 2 sources (GM:518)", m);
+        break;
+      case IGN_AGGR_CONCAT:
+        if (mp.concat_axis != 1)
+          return fail(IGN_ERR_UNSUPPORTED, "mp %d: concat aggregation on axis %d is not lowered yet", m, mp.concat_axis);
+        mp.sorted = true;
+        break;
+      default:
+        return fail(IGN_ERR_UNSUPPORTED, "mp %d: aggregation %d (attention/convolution) is not lowered yet", m, mp.aggr);
+    }
+    int din = -1;
+    for (auto& s : mp.src) {
+      if (s.entity < 0 || s.entity >= d->num_entities) return fail(IGN_ERR_INVALID, "mp %d: bad source entity", m);
+      if (s.adjacency < 0 || s.adjacency >= p->n_adj) return fail(IGN_ERR_INVALID, "mp %d: bad adjacency slot", m);
+      if (mp.aggr == IGN_AGGR_INTERLEAVE && (s.interleave < 0 || s.interleave >= p->n_il))
+        return fail(IGN_ERR_INVALID, "mp %d: interleave slot missing", m);
+      int dm = p->ents[s.entity].hidden_dim;   // direct_assignation: message = source state
+      if (din >= 0 && dm != din)
+        return fail(IGN_ERR_INVALID, "mp %d: sources have different message dimensions (%d vs %d)", m, din, dm);
+      din = dm;
+    }
+    mp.din = din;
+    if (mp.cell < 0 || mp.cell >= (int)p->cells.size()) return fail(IGN_ERR_INVALID, "mp %d: bad cell index", m);
+    CellP& cp = p->cells[mp.cell];
+    if (cp.H != p->ents[mp.dst].hidden_dim)
+      return fail(IGN_ERR_INVALID, "mp %d: cell units %d != destination hidden dim %d", m, cp.H, p->ents[mp.dst].hidden_dim);
+    if (cp.din != din)
+      return fail(IGN_ERR_INVALID, "mp %d: cell input_dim %d != message dim %d", m, cp.din, din);
+    if (!gru_shape_supported(din, cp.H))
+      return fail(IGN_ERR_UNSUPPORTED, "mp %d: GRU shape (input %d, units %d) not instantiated (16/32)", m, din, cp.H);
+    cp.used = true;
+    p->mps.push_back(mp);
+  }
+  // readout
+  p->ro_in.assign(d->readout_inputs, d->readout_inputs + d->num_readout_inputs);
+  if (p->ro_in.empty()) return fail(IGN_ERR_INVALID, "readout has no input");
+  int width = 0;
+  for (int e : p->ro_in) {
+    if (e < 0 || e >= d->num_entities) return fail(IGN_ERR_INVALID, "readout input entity %d", e);
+    width += p->ents[e].hidden_dim;
+  }
+  p->ro_width = width;
+  int in = width;
+  for (int l = 0; l < d->num_dense; ++l) {
+    DenseP dp;
+    dp.in = in;
+    dp.out = d->dense[l].units;
+    dp.act = d->dense[l].activation;
+    dp.use_bias = d->dense[l].use_bias;
+    if (dp.out <= 0) return fail(IGN_ERR_INVALID, "dense layer %d: units must be > 0", l);
+    if (!act_ok(dp.act)) return fail(IGN_ERR_UNSUPPORTED, "dense layer %d: activation %d", l, dp.act);
+    p->dense.push_back(dp);
+    in = dp.out;
+  }
+  if (p->dense.empty()) return fail(IGN_ERR_INVALID, "readout has no Dense layer");
+  p->fused_readout = p->dense.size() == 3 && readout3_supported(width, p->dense[0].out, p->dense[1].out) &&
+                     p->dense[2].out == 1;
+
+  // parameter layout (256-B aligned tensors)
+  auto align = [](int64_t x) { return (x + 63) & ~int64_t(63); };
+  int64_t off = 0;
+  for (size_t c = 0; c < p->cells.size(); ++c) {
+    CellP& cp = p->cells[c];
+    int g3 = 3 * cp.H;
+    cp.off_k = off; p->tensors.push_back({0, (int)c, off, cp.din, g3}); off = align(off + (int64_t)cp.din * g3);
+    cp.off_rk = off; p->tensors.push_back({1, (int)c, off, cp.H, g3}); off = align(off + (int64_t)cp.H * g3);
+    cp.off_b = off; p->tensors.push_back({2, (int)c, off, 2, g3}); off = align(off + 2LL * g3);
+  }
+  for (size_t l = 0; l < p->dense.size(); ++l) {
+    DenseP& dp = p->dense[l];
+    dp.off_w = off; p->tensors.push_back({3, (int)l, off, dp.in, dp.out}); off = align(off + (int64_t)dp.in * dp.out);
+    dp.off_b = off; p->tensors.push_back({4, (int)l, off, 1, dp.out}); off = align(off + dp.out);
+  }
+  p->n_params = off;
+  int64_t pk = 0;
+  for (auto& cp : p->cells) {
+    if (!cp.used) continue;
+    cp.pk_w = pk; pk = align(pk + 3LL * cp.din * cp.H);
+    cp.pk_u = pk; pk = align(pk + 3LL * cp.H * cp.H);
+    cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
+  }
+  if (p->fused_readout) {
+    p->dense[0].pk_w = pk; pk = align(pk + (int64_t)p->dense[0].in * p->dense[0].out);
+    p->dense[1].pk_w = pk; pk = align(pk + (int64_t)p->dense[1].in * p->dense[1].out);
+  }
+  p->n_packed = pk;
+
+  // Device resources are allocated on first use (ensure_device), so plan validation and the
+  // parameter layout are available without a GPU.
+  *out = p.release();
+  return IGN_OK;
+}
+
+void ign_plan_destroy(ign_plan* p) {
+  if (!p) return;
+  if (!p->d_params && !p->stream) {
+    delete p;
+    return;
+  }
+  hipSetDevice(p->device);
+  if (p->stream) hipStreamSynchronize(p->stream);
+  for (auto e : p->ev) hipEventDestroy(e);
+  if (p->d_params) hipFree(p->d_params);
+  if (p->d_packed) hipFree(p->d_packed);
+  if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
+  delete p;
+}
+
+int ign_plan_num_params(const ign_plan* p, int64_t* n) {
+  if (!p || !n) return fail(IGN_ERR_INVALID, "null argument");
+  *n = p->n_params;
+  return IGN_OK;
+}
+
+int ign_plan_num_param_tensors(const ign_plan* p, int32_t* n) {
+  if (!p || !n) return fail(IGN_ERR_INVALID, "null argument");
+  *n = (int32_t)p->tensors.size();
+  return IGN_OK;
+}
+
+int ign_plan_param_tensor(const ign_plan* p, int32_t i, int32_t* kind, int32_t* owner, int64_t* offset,
+                          int32_t* rows, int32_t* cols) {
+  if (!p || i < 0 || i >= (int)p->tensors.size()) return fail(IGN_ERR_INVALID, "tensor index out of range");
+  const Tensor& t = p->tensors[i];
+  if (kind) *kind = t.kind;
+  if (owner) *owner = t.owner;
+  if (offset) *offset = t.offset;
+  if (rows) *rows = t.rows;
+  if (cols) *cols = t.cols;
+  return IGN_OK;
+}
+
+int ign_plan_set_params(ign_plan* p, const float* params, int32_t on_device) {
+  if (!p || !params) return fail(IGN_ERR_INVALID, "null argument");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(p->d_params, params, p->n_params * sizeof(float),
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, p->stream));
+  for (auto& cp : p->cells) {
+    if (!cp.used) continue;
+    HIP_TRY(launch_pack_gru(p->d_params + cp.off_k, p->d_params + cp.off_rk, p->d_params + cp.off_b,
+                            p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
+                            p->stream));
+  }
+  if (p->fused_readout) {
+    for (int l = 0; l < 2; ++l)
+      HIP_TRY(launch_pack_dense(p->d_params + p->dense[l].off_w, p->d_packed + p->dense[l].pk_w, p->dense[l].in,
+                                p->dense[l].out, p->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  p->params_set = true;
+  return IGN_OK;
+}
+
+int ign_plan_set_timing(ign_plan* p, int32_t enabled) {
+  if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  p->timing = enabled != 0;
+  p->stats = ign_stats_t{};
+  return IGN_OK;
+}
+
+int ign_plan_set_stream(ign_plan* p, void* s) {
+  if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  if (p->own_stream && p->stream) {
+    hipStreamSynchronize(p->stream);
+    hipStreamDestroy(p->stream);
+  }
+  p->own_stream = false;
+  p->stream = static_cast<hipStream_t>(s);
+  return IGN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
+  if (!p || !d || !out) return fail(IGN_ERR_INVALID, "null argument");
+  *out = nullptr;
+  const int G = d->num_graphs;
+  const int E = (int)p->ents.size();
+  if (G <= 0) return fail(IGN_ERR_INVALID, "num_graphs must be > 0");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  std::unique_ptr<ign_batch, void (*)(ign_batch*)> b(new ign_batch(), ign_batch_destroy);
+  b->plan = p;
+  b->G = G;
+  b->rows.assign(E, 0);
+  b->row_off.assign(E, std::vector<int64_t>(G + 1, 0));
+  for (int e = 0; e < E; ++e) {
+    for (int g = 0; g < G; ++g) {
+      int64_t n = d->num_nodes[(int64_t)g * E + e];
+      if (n < 0) return fail(IGN_ERR_INVALID, "graph %d: negative num_ for entity %d", g, e);
+      b->row_off[e][g + 1] = b->row_off[e][g] + n;
+    }
+    b->rows[e] = b->row_off[e][G];
+    if (b->rows[e] >= (int64_t)IGN_ROW_MASK) return fail(IGN_ERR_UNSUPPORTED, "entity %d: too many rows", e);
+  }
+  // edge offsets per adjacency
+  std::vector<std::vector<int64_t>> eoff(p->n_adj, std::vector<int64_t>(G + 1, 0));
+  for (int a = 0; a < p->n_adj; ++a)
+    for (int g = 0; g < G; ++g) {
+      int64_t n = d->adj_edges[(int64_t)g * p->n_adj + a];
+      if (n < 0) return fail(IGN_ERR_INVALID, "negative edge count");
+      eoff[a][g + 1] = eoff[a][g] + n;
+    }
+  std::vector<std::vector<int64_t>> ioff(p->n_il, std::vector<int64_t>(G + 1, 0));
+  for (int i = 0; i < p->n_il; ++i)
+    for (int g = 0; g < G; ++g) ioff[i][g + 1] = ioff[i][g] + d->interleave_len[(int64_t)g * p->n_il + i];
+
+  // features + state buffers
+  b->d_feat.assign(E, nullptr);
+  b->d_state[0].assign(E, nullptr);
+  b->d_state[1].assign(E, nullptr);
+  b->cur.assign(E, 0);
+  for (int e = 0; e < E; ++e) {
+    const int H = p->ents[e].hidden_dim, F = p->ents[e].feature_total;
+    if (F > 0) {
+      if (!d->features || !d->features[e]) return fail(IGN_ERR_INVALID, "entity %d: features missing", e);
+      std::vector<float> f(d->features[e], d->features[e] + b->rows[e] * F);
+      if ((rc = dev_upload(b.get(), &b->d_feat[e], f))) return rc;
+    }
+    if ((rc = dev_alloc(b.get(), &b->d_state[0][e], b->rows[e] * H))) return rc;
+    if ((rc = dev_alloc(b.get(), &b->d_state[1][e], b->rows[e] * H))) return rc;
+  }
+
+  // per-MP CSR / step tables
+  for (size_t mi = 0; mi < p->mps.size(); ++mi) {
+    const MPP& mp = p->mps[mi];
+    const int S = (int)mp.src.size();
+    const int dst = mp.dst;
+    const int64_t ND = b->rows[dst];
+    MPB mb;
+    mb.sorted = mp.sorted;
+    mb.n_dst = ND;
+    // messages: (dst row, position, code), in source order then edge order
+    std::vector<int64_t> mdst;
+    std::vector<int64_t> mpos;
+    std::vector<uint32_t> mcode;
+    int64_t tot = 0;
+    for (int s = 0; s < S; ++s) tot += eoff[mp.src[s].adjacency][G];
+    mdst.reserve(tot);
+    mpos.reserve(tot);
+    mcode.reserve(tot);
+    std::vector<int64_t> flen(ND, 0);
+    for (int g = 0; g < G; ++g) {
+      int64_t slot_off = 0;  // sum of Lmax of previous sources in this graph (GM:533)
+      std::vector<int64_t> ilflat;
+      if (mp.aggr == IGN_AGGR_INTERLEAVE) {
+        // tf.stack([indices_a, indices_b]) then reshape [-1,1] (GM:518, AUX:433)
+        int64_t len0 = -1;
+        for (int s = 0; s < S; ++s) {
+          int il = mp.src[s].interleave;
+          int64_t n = ioff[il][g + 1] - ioff[il][g];
+          if (len0 >= 0 && n != len0)
+            return fail(IGN_ERR_INVALID, "graph %d: interleave index lists have different lengths (%lld vs %lld;"
+                        " tf.stack fails, GM:518)", g, (long long)len0, (long long)n);
+          len0 = n;
+          for (int64_t k = ioff[il][g]; k < ioff[il][g + 1]; ++k) ilflat.push_back(d->interleave_idx[il][k]);
+        }
+      }
+      int64_t total_slots = 0;
+      std::vector<int64_t> lmax(S, 0);
+      for (int s = 0; s < S; ++s) {
+        const int a = mp.src[s].adjacency;
+        const int64_t e0 = eoff[a][g], e1 = eoff[a][g + 1];
+        if (e1 == e0)
+          return fail(IGN_ERR_INVALID, "graph %d: adjacency slot %d has no edges (the reference's scatter_nd shape"
+                      " max(seq)+1 is undefined, GM:484-490)", g, a);
+        int64_t mx = -1;
+        for (int64_t k = e0; k < e1; ++k) {
+          int64_t sq = d->adj_seq[a][k];
+          if (sq < 0) return fail(IGN_ERR_INVALID, "graph %d: negative seq value", g);
+          mx = std::max(mx, sq);
+        }
+        lmax[s] = mx + 1;
+        total_slots += lmax[s];
+      }
+      if (mp.aggr == IGN_AGGR_INTERLEAVE && (int64_t)ilflat.size() != total_slots)
+        return fail(IGN_ERR_INVALID, "graph %d: interleave indices cover %lld slots but the messages need %lld"
+                    " (scatter_nd shape mismatch, AUX:435)", g, (long long)ilflat.size(), (long long)total_slots);
+      for (int s = 0; s < S; ++s) {
+        const int a = mp.src[s].adjacency;
+        const int se = mp.src[s].entity;
+        const int64_t e0 = eoff[a][g], e1 = eoff[a][g + 1];
+        const int64_t nsrc = b->row_off[se][g + 1] - b->row_off[se][g];
+        const int64_t ndst = b->row_off[dst][g + 1] - b->row_off[dst][g];
+        for (int64_t k = e0; k < e1; ++k) {
+          int64_t si = d->adj_src[a][k], di = d->adj_dst[a][k], sq = d->adj_seq[a][k];
+          if (si < 0 || si >= nsrc) return fail(IGN_ERR_INVALID, "graph %d: src index %lld out of range [0,%lld)", g, (long long)si, (long long)nsrc);
+          if (di < 0 || di >= ndst) return fail(IGN_ERR_INVALID, "graph %d: dst index %lld out of range [0,%lld)", g, (long long)di, (long long)ndst);
+          int64_t pos = slot_off + sq;
+          if (mp.aggr == IGN_AGGR_INTERLEAVE) {
+            pos = ilflat[pos];
+            if (pos < 0 || pos >= total_slots)
+              return fail(IGN_ERR_INVALID, "graph %d: interleave index %lld outside [0,%lld) (scatter_nd, AUX:435)",
+                          g, (long long)pos, (long long)total_slots);
+          }
+          int64_t drow = b->row_off[dst][g] + di;
+          mdst.push_back(drow);
+          mpos.push_back(pos);
+          mcode.push_back(((uint32_t)s << IGN_SLOT_SHIFT) | (uint32_t)(b->row_off[se][g] + si));
+          flen[drow] += 1;   // final_len = sum of lens over sources (GM:505/519/543)
+        }
+        slot_off += lmax[s];
+      }
+      if (mp.sorted) {
+        // gather_nd(outputs, [d, final_len-1]) needs final_len <= sum of Lmax (AUX:793-795)
+        for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r)
+          if (flen[r] > total_slots)
+            return fail(IGN_ERR_INVALID, "graph %d: destination row %lld has final_len %lld > %lld padded slots"
+                        " (gather_nd out of range, AUX:793-795)", g, (long long)(r - b->row_off[dst][g]),
+                        (long long)flen[r], (long long)total_slots);
+      }
+    }
+    mb.edges = tot;
+    b->edges_per_forward += tot * p->T;
+    const CellP& cp = p->cells[mp.cell];
+    const int H = cp.H, DIN = mp.din;
+
+    std::vector<int32_t> order(ND);
+    std::iota(order.begin(), order.end(), 0);
+    if (mp.sorted) {
+      for (int64_t r = 0; r < ND; ++r)
+        if (flen[r] == 0)   // AUX:793-795: gather_nd(outputs, [d, final_len-1]) with -1
+          return fail(IGN_ERR_INVALID, "destination row %lld receives no message: the reference's sorted update"
+                      " gathers position -1 (AUX:793-795)", (long long)r);
+      std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
+      // bucket messages by destination (stable), keep those with pos < final_len, sort by pos
+      std::vector<int64_t> dcnt(ND + 1, 0);
+      for (size_t k = 0; k < mdst.size(); ++k) dcnt[mdst[k] + 1]++;
+      for (int64_t r = 0; r < ND; ++r) dcnt[r + 1] += dcnt[r];
+      std::vector<int64_t> byd(mdst.size());
+      {
+        std::vector<int64_t> fill(dcnt.begin(), dcnt.end() - 1);
+        for (size_t k = 0; k < mdst.size(); ++k) byd[fill[mdst[k]]++] = (int64_t)k;
+      }
+      std::vector<int32_t> len(ND), step_ptr(ND), msg_ptr;
+      std::vector<uint32_t> msrc;
+      msg_ptr.reserve(mdst.size() + 1);
+      msrc.reserve(mdst.size());
+      int64_t steps = 0;
+      std::vector<int64_t> tmp;
+      for (int64_t i = 0; i < ND; ++i) {
+        const int64_t r = order[i];
+        const int64_t L = flen[r];
+        len[i] = (int32_t)L;
+        step_ptr[i] = (int32_t)steps;
+        tmp.assign(byd.begin() + dcnt[r], byd.begin() + dcnt[r + 1]);
+        std::stable_sort(tmp.begin(), tmp.end(), [&](int64_t x, int64_t y) { return mpos[x] < mpos[y]; });
+        size_t q = 0;
+        for (int64_t t = 0; t < L; ++t) {
+          msg_ptr.push_back((int32_t)msrc.size());
+          while (q < tmp.size() && mpos[tmp[q]] < t) ++q;
+          while (q < tmp.size() && mpos[tmp[q]] == t) msrc.push_back(mcode[tmp[q++]]);
+        }
+        steps += L;
+      }
+      msg_ptr.push_back((int32_t)msrc.size());
+      if (steps >= INT32_MAX || (int64_t)msrc.size() >= INT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
+      mb.n_steps = steps;
+      mb.n_msgs = (int64_t)msrc.size();
+      if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_len, len))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_step_ptr, step_ptr))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_msg_ptr, msg_ptr))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_msg_src, msrc))) return rc;
+      mb.flops = (double)steps * gru_flops(DIN, H) + (double)mb.n_msgs * DIN;
+      mb.bytes = (double)mb.n_msgs * (4.0 * DIN + 4) + (double)steps * 4 + (double)ND * (8.0 * H + 12);
+      b->gru_steps += steps * p->T;
+    } else {
+      std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
+      std::vector<int32_t> where(ND);
+      for (int64_t i = 0; i < ND; ++i) where[order[i]] = (int32_t)i;
+      std::vector<int32_t> ptr(ND + 1, 0);
+      for (size_t k = 0; k < mdst.size(); ++k) ptr[where[mdst[k]] + 1]++;
+      for (int64_t i = 0; i < ND; ++i) ptr[i + 1] += ptr[i];
+      std::vector<uint32_t> msrc(mdst.size());
+      {
+        std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
+        for (size_t k = 0; k < mdst.size(); ++k) msrc[fill[where[mdst[k]]]++] = mcode[k];
+      }
+      mb.n_msgs = (int64_t)msrc.size();
+      if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_msg_ptr, ptr))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_msg_src, msrc))) return rc;
+      mb.flops = (double)ND * gru_flops(DIN, H) + (double)mb.n_msgs * DIN;
+      mb.bytes = (double)mb.n_msgs * (4.0 * DIN + 4) + (double)ND * (8.0 * H + 8);
+      b->gru_steps += ND * p->T;
+    }
+    b->mp.push_back(mb);
+  }
+
+  // readout buffers
+  const int64_t P = b->rows[p->ro_in[0]];
+  for (int e : p->ro_in)
+    if (b->rows[e] != P) return fail(IGN_ERR_INVALID, "readout inputs have different row counts (concat axis 1)");
+  b->n_pred = P;
+  b->out_units = p->dense.back().out;
+  if (p->ro_in.size() > 1 && (rc = dev_alloc(b.get(), &b->d_ro_in, P * p->ro_width))) return rc;
+  if (!p->fused_readout) {
+    for (size_t l = 0; l + 1 < p->dense.size(); ++l) {
+      float* t = nullptr;
+      if ((rc = dev_alloc(b.get(), &t, P * p->dense[l].out))) return rc;
+      b->d_ro_tmp.push_back(t);
+    }
+  }
+  if ((rc = dev_alloc(b.get(), &b->d_pred, P * b->out_units))) return rc;
+  *out = b.release();
+  return IGN_OK;
+}
+
+void ign_batch_destroy(ign_batch* b) {
+  if (!b) return;
+  if (b->plan) {
+    hipSetDevice(b->plan->device);
+    if (b->plan->stream) hipStreamSynchronize(b->plan->stream);
+  }
+  for (void* a : b->allocs) hipFree(a);
+  delete b;
+}
+
+int ign_batch_info(const ign_batch* b, ign_batch_info_t* o) {
+  if (!b || !o) return fail(IGN_ERR_INVALID, "null argument");
+  std::memset(o, 0, sizeof(*o));
+  o->num_graphs = b->G;
+  o->predictions = b->n_pred;
+  o->output_units = b->out_units;
+  o->edges_per_forward = b->edges_per_forward;
+  o->gru_steps_per_forward = b->gru_steps;
+  for (size_t e = 0; e < b->rows.size() && e < 8; ++e) o->rows[e] = b->rows[e];
+  return IGN_OK;
+}
+
+int ign_batch_predictions(ign_batch* b, const float** ptr) {
+  if (!b || !ptr) return fail(IGN_ERR_INVALID, "null argument");
+  *ptr = b->d_pred;
+  return IGN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct Timer {
+  ign_plan* p;
+  int slot = 0;
+  void begin(int kind, double flops, double bytes) {
+    if (!p->timing) return;
+    size_t need = 2 * (slot + 1);
+    while (p->ev.size() < need) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      p->ev.push_back(e);
+    }
+    if ((int)p->ev_kind.size() <= slot) {
+      p->ev_kind.resize(slot + 1);
+      p->ev_flops.resize(slot + 1);
+      p->ev_bytes.resize(slot + 1);
+    }
+    p->ev_kind[slot] = kind;
+    p->ev_flops[slot] = flops;
+    p->ev_bytes[slot] = bytes;
+    hipEventRecord(p->ev[2 * slot], p->stream);
+  }
+  void end() {
+    if (!p->timing) return;
+    hipEventRecord(p->ev[2 * slot + 1], p->stream);
+    ++slot;
+  }
+};
+
+}  // namespace
+
+int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
+  if (!p || !b) return fail(IGN_ERR_INVALID, "null argument");
+  if (b->plan != p) return fail(IGN_ERR_INVALID, "batch was created for another plan");
+  if (!p->params_set) return fail(IGN_ERR_INVALID, "parameters not set (ign_plan_set_params)");
+  int rc = set_device(p->device);
+  if (rc) return rc;
+  hipStream_t st = p->stream;
+  Timer tm{p};
+  const int E = (int)p->ents.size();
+
+  for (int e = 0; e < E; ++e) {   // GM:396-400
+    const int H = p->ents[e].hidden_dim, F = p->ents[e].feature_total;
+    tm.begin(K_INIT, 0, (double)b->rows[e] * (4.0 * F + 4.0 * H));
+    HIP_TRY(launch_init_state(b->d_state[0][e], b->d_feat[e], b->rows[e], H, F, st));
+    tm.end();
+    b->cur[e] = 0;
+  }
+  for (int it = 0; it < p->T; ++it) {              // GM:406
+    for (size_t mi = 0; mi < p->mps.size(); ++mi) { // GM:410-414 (stages flattened in order)
+      const MPP& mp = p->mps[mi];
+      const MPB& mb = b->mp[mi];
+      const CellP& cp = p->cells[mp.cell];
+      SrcBases sbases{};
+      for (size_t s = 0; s < mp.src.size(); ++s) {
+        int se = mp.src[s].entity;
+        sbases.base[s] = b->d_state[b->cur[se]][se];
+      }
+      const int dst = mp.dst;
+      const float* hin = b->d_state[b->cur[dst]][dst];
+      float* hout = b->d_state[1 - b->cur[dst]][dst];
+      if (mp.sorted) {
+        SeqGruArgs a{hin, hout, sbases, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_msg_ptr, mb.d_msg_src,
+                     p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst};
+        tm.begin(K_SEQ, mb.flops, mb.bytes);
+        HIP_TRY(launch_seq_gru(a, mp.din, cp.H, st));
+        tm.end();
+      } else {
+        SumGruArgs a{hin, hout, sbases, mb.d_order, mb.d_msg_ptr, mb.d_msg_src,
+                     p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst};
+        tm.begin(K_SUM, mb.flops, mb.bytes);
+        HIP_TRY(launch_sum_gru(a, mp.din, cp.H, st));
+        tm.end();
+      }
+      b->cur[dst] ^= 1;   // GM:602: the destination state is overwritten
+    }
+  }
+  // readout (GM:611-629)
+  const int64_t P = b->n_pred;
+  const float* x = b->d_state[b->cur[p->ro_in[0]]][p->ro_in[0]];
+  int xs = p->ro_width;
+  if (p->ro_in.size() > 1) {
+    int col = 0;
+    for (int e : p->ro_in) {
+      HIP_TRY(launch_concat_cols(b->d_ro_in, P, p->ro_width, col, b->d_state[b->cur[e]][e], p->ents[e].hidden_dim, st));
+      col += p->ents[e].hidden_dim;
+    }
+    x = b->d_ro_in;
+  }
+  const float* prm = p->d_params;
+  if (p->fused_readout) {
+    const DenseP &l1 = p->dense[0], &l2 = p->dense[1], &l3 = p->dense[2];
+    Readout3Args a{x, P, xs,
+                   p->d_packed + l1.pk_w, l1.use_bias ? prm + l1.off_b : nullptr,
+                   p->d_packed + l2.pk_w, l2.use_bias ? prm + l2.off_b : nullptr,
+                   prm + l3.off_w, l3.use_bias ? prm + l3.off_b : nullptr,
+                   l1.act, l2.act, l3.act, b->d_pred};
+    // a null bias pointer means "no bias": point at a zero region instead for the fused kernel
+    static_assert(sizeof(Readout3Args) > 0, "");
+    if (!a.b1 || !a.b2) return fail(IGN_ERR_UNSUPPORTED, "fused readout requires use_bias on hidden layers");
+    double flops = 2.0 * P * ((double)l1.in * l1.out + (double)l2.in * l2.out + l3.in);
+    tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0));
+    HIP_TRY(launch_readout3(a, l1.in, l1.out, l2.out, st));
+    tm.end();
+  } else {
+    const float* in = x;
+    int in_stride = xs;
+    for (size_t l = 0; l < p->dense.size(); ++l) {
+      const DenseP& dl = p->dense[l];
+      float* o = (l + 1 == p->dense.size()) ? b->d_pred : b->d_ro_tmp[l];
+      tm.begin(K_READOUT, 2.0 * P * dl.in * dl.out, (double)P * 4.0 * (dl.in + dl.out));
+      HIP_TRY(launch_dense_generic(in, P, dl.in, in_stride, prm + dl.off_w, dl.use_bias ? prm + dl.off_b : nullptr,
+                                   dl.out, dl.act, o, st));
+      tm.end();
+      in = o;
+      in_stride = dl.out;
+    }
+  }
+  if (pred_out) {
+    HIP_TRY(hipMemcpyAsync(pred_out, b->d_pred, P * b->out_units * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (p->timing) {
+    HIP_TRY(hipStreamSynchronize(st));
+    ign_stats_t& s = p->stats;
+    s.kinds = K_KINDS;
+    for (int i = 0; i < tm.slot; ++i) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]);
+      int k = p->ev_kind[i];
+      s.launches[k] += 1;
+      s.ms[k] += ms;
+      s.flops[k] += p->ev_flops[i];
+      s.bytes[k] += p->ev_bytes[i];
+    }
+  }
+  return IGN_OK;
+}
+
+int ign_synchronize(ign_plan* p) {
+  if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  return IGN_OK;
+}
+
+int ign_batch_state(ign_plan* p, ign_batch* b, int32_t e, float* host_out) {
+  if (!p || !b || !host_out) return fail(IGN_ERR_INVALID, "null argument");
+  if (e < 0 || e >= (int)p->ents.size()) return fail(IGN_ERR_INVALID, "entity index");
+  int rc = set_device(p->device);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(host_out, b->d_state[b->cur[e]][e], b->rows[e] * p->ents[e].hidden_dim * sizeof(float),
+                         hipMemcpyDeviceToHost, p->stream));
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  return IGN_OK;
+}
+
+int ign_stats(const ign_plan* p, ign_stats_t* out) {
+  if (!p || !out) return fail(IGN_ERR_INVALID, "null argument");
+  *out = p->stats;
+  return IGN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// kernels.h — kernel argument blocks and launchers shared by engine.cpp and kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define IGN_SLOT_SHIFT 29u
+#define IGN_ROW_MASK ((1u << IGN_SLOT_SHIFT) - 1u)
+#define IGN_MAX_SLOTS 4
+
+enum { IGN_K_ACT_LINEAR = 0, IGN_K_ACT_RELU = 1, IGN_K_ACT_SELU = 2, IGN_K_ACT_SIGMOID = 3, IGN_K_ACT_TANH = 4 };
+
+// Base pointer of each source slot's current hidden-state table (message code = slot<<29 | row).
+struct SrcBases {
+  const float* base[IGN_MAX_SLOTS];
+};
+
+struct SeqGruArgs {
+  const float* h_in;       // [rows][H] destination state before the update
+  float* h_out;            // [rows][H] destination state after the update
+  SrcBases src;
+  const int32_t* order;    // [n_dst] destination rows, sorted by final_len (descending)
+  const int32_t* len;      // [n_dst] final_len per order position
+  const int32_t* step_ptr; // [n_dst] first step of each order position
+  const int32_t* msg_ptr;  // [n_steps + 1] message range of every step
+  const uint32_t* msg_src; // [n_msgs] message source codes
+  const float* Wp;         // packed input-kernel fragments
+  const float* Up;         // packed recurrent-kernel fragments
+  const float* bias;       // [4][H] combined biases
+  int64_t n_dst;
+};
+
+struct SumGruArgs {
+  const float* h_in;
+  float* h_out;
+  SrcBases src;
+  const int32_t* order;    // [n_dst] destination rows, sorted by in-degree (descending)
+  const int32_t* msg_ptr;  // [n_dst + 1] message range per order position
+  const uint32_t* msg_src;
+  const float* Wp;
+  const float* Up;
+  const float* bias;
+  int64_t n_dst;
+};
+
+struct Readout3Args {
+  const float* x;          // [n_rows][x_stride]
+  int64_t n_rows;
+  int x_stride;
+  const float* W1p; const float* b1;
+  const float* W2p; const float* b2;
+  const float* w3;  const float* b3;  // [N2] (output units == 1), [1]
+  int act1, act2, act3;
+  float* y;                // [n_rows]
+};
+
+hipError_t launch_init_state(float* state, const float* feats, int64_t n, int H, int F, hipStream_t st);
+hipError_t launch_pack_gru(const float* W, const float* U, const float* bias, float* Wp, float* Up, float* bp,
+                           int DIN, int H, hipStream_t st);
+hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStream_t st);
+bool gru_shape_supported(int din, int h);
+hipError_t launch_seq_gru(const SeqGruArgs& args, int din, int h, hipStream_t st);
+hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st);
+bool readout3_supported(int din, int n1, int n2);
+hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
+hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
+                                int out, int act, float* y, hipStream_t st);
+hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,
+                              hipStream_t st);

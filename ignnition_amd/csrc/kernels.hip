@@ -1,0 +1,538 @@
+// kernels.hip — gfx950 (CDNA4) kernels of the message-passing engine.
+//
+// Every kernel works on the CSR tables built by engine.cpp; the layout in HBM is
+// documented in DESIGN.md.  The GRU and readout contractions run on fp32-input MFMA
+// (v_mfma_f32_16x16x4_f32: exact f32 fma chain, 64 FLOP/clk/SIMD = the chip's fp32 peak).
+//
+// Transposed formulation used everywhere: D[unit][row] = W^T[unit][k] * X^T[k][row], i.e.
+// the MFMA A operand is a weight fragment and the B operand holds 16 graph rows
+// (paths / links / nodes) on the lanes.  Lane l holds row j = l & 15 and, in the
+// accumulator, units 16t + 4g + r (g = l >> 4, r = register 0..3).  The k order of
+// every contraction is permuted as  k(s, g) = 16*(s>>2) + 4*g + (s&3)  so that
+//   * the per-row input x is read as float4 chunks [16c + 4g, +4) of the row (one 64-B
+//     segment per 4 lanes: a coalesced row gather), and
+//   * an accumulator tile is directly the B operand of the next contraction: register
+//     (s&3) of tile (s>>2) is exactly x[k(s,g)].  The GRU hidden state therefore never
+//     leaves registers across the steps of a sequence (no LDS round trip, no shuffles).
+// Weights are pre-packed (pack_* kernels) into that fragment order once per
+// ign_plan_set_params, so a wave loads each fragment with one coalesced 256-B read.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kernels.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float tanhf_(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for |x| large.
+  float e = __expf(2.0f * x);
+  return 1.0f - 2.0f / (e + 1.0f);
+}
+
+__device__ __forceinline__ float act_apply(float x, int act) {
+  switch (act) {
+    case IGN_K_ACT_RELU: return x > 0.f ? x : 0.f;
+    case IGN_K_ACT_SELU: {
+      const float lam = 1.0507009873554805f, alpha = 1.6732632423543772f;
+      return x > 0.f ? lam * x : lam * alpha * (__expf(x) - 1.0f);
+    }
+    case IGN_K_ACT_SIGMOID: return sigmoidf_(x);
+    case IGN_K_ACT_TANH: return tanhf_(x);
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// ---------------------------------------------------------------------------------------------
+// Hidden-state init (AUX:128-160): state[n] = [features[n] (F floats) | zeros(H - F)].
+__global__ void init_state_kernel(float* __restrict__ state, const float* __restrict__ feats,
+                                  int64_t n, int H, int F) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = n * (int64_t)H;
+  for (; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t row = i / H;
+    int c = (int)(i - row * H);
+    state[i] = (c < F && feats) ? feats[row * F + c] : 0.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// GRU weight packing.  Keras GRUCell v2 layout: kernel [DIN][3H], recurrent_kernel [H][3H],
+// bias [2][3H]; gate column order z, r, h (AUX:748-749).
+// Packed fragment f = ((gate * NT + t) * KS + s), 64 lanes each:
+//   lane l -> M[k(s, l>>4)][gate*H + 16t + (l&15)]
+__global__ void pack_gru_kernel(const float* __restrict__ W, const float* __restrict__ U,
+                                const float* __restrict__ bias, float* __restrict__ Wp,
+                                float* __restrict__ Up, float* __restrict__ bp, int DIN, int H) {
+  int NT = H / 16;
+  int64_t nW = 3LL * NT * (DIN / 4) * 64;
+  int64_t nU = 3LL * NT * (H / 4) * 64;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = i; e < nW + nU + 4LL * H; e += stride) {
+    if (e < nW + nU) {
+      bool isU = e >= nW;
+      int64_t idx = isU ? e - nW : e;
+      int KS = isU ? H / 4 : DIN / 4;
+      int lane = (int)(idx & 63);
+      int64_t f = idx >> 6;
+      int s = (int)(f % KS);
+      int64_t gt = f / KS;
+      int t = (int)(gt % NT);
+      int gate = (int)(gt / NT);
+      int k = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
+      int col = gate * H + 16 * t + (lane & 15);
+      if (isU) Up[idx] = U[(int64_t)k * 3 * H + col];
+      else     Wp[idx] = W[(int64_t)k * 3 * H + col];
+    } else {
+      // combined biases: [0] bz_in+bz_rec, [1] br_in+br_rec, [2] bh_in, [3] bh_rec
+      int b = (int)(e - nW - nU);
+      int which = b / H, u = b % H;
+      const float* bin = bias;            // bias[0][:]
+      const float* brec = bias + 3 * H;   // bias[1][:]
+      float v;
+      if (which == 0) v = bin[u] + brec[u];
+      else if (which == 1) v = bin[H + u] + brec[H + u];
+      else if (which == 2) v = bin[2 * H + u];
+      else v = brec[2 * H + u];
+      bp[b] = v;
+    }
+  }
+}
+
+// Dense kernel [IN][OUT] -> float4-grouped A fragments: ((u * (IN/16) + c) * 64 + lane) * 4 + q
+//   -> W[16c + 4*(lane>>4) + q][16u + (lane&15)]
+__global__ void pack_dense_kernel(const float* __restrict__ W, float* __restrict__ Wp, int IN, int OUT) {
+  int64_t total = (int64_t)IN * OUT;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int q = (int)(i & 3);
+    int lane = (int)((i >> 2) & 63);
+    int64_t f = i >> 8;
+    int C = IN / 16;
+    int c = (int)(f % C);
+    int u = (int)(f / C);
+    int k = 16 * c + 4 * (lane >> 4) + q;
+    int col = 16 * u + (lane & 15);
+    Wp[i] = W[(int64_t)k * OUT + col];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// One GRU step for the wave's 16 rows (reset_after=True, AUX:764 / Keras GRUCell v2):
+//   z = s(x Wz + h Uz + bz) ; r = s(x Wr + h Ur + br) ; c = tanh(x Wh + bhx + r (h Uh + bhh))
+//   h' = z h + (1 - z) c
+template <int DIN, int H>
+struct GruWeights {
+  static constexpr int NT = H / 16, KX = DIN / 4, KH = H / 4;
+  float w[3][NT][KX];
+  float u[3][NT][KH];
+};
+
+template <int DIN, int H>
+__device__ __forceinline__ void load_gru_weights(GruWeights<DIN, H>& W, const float* __restrict__ Wp,
+                                                 const float* __restrict__ Up, int lane) {
+  constexpr int NT = H / 16, KX = DIN / 4, KH = H / 4;
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int s = 0; s < KX; ++s) W.w[g][t][s] = Wp[(((g * NT + t) * KX + s) << 6) + lane];
+#pragma unroll
+      for (int s = 0; s < KH; ++s) W.u[g][t][s] = Up[(((g * NT + t) * KH + s) << 6) + lane];
+    }
+}
+
+template <int DIN, int H>
+__device__ __forceinline__ void gru_step(const GruWeights<DIN, H>& W, const float* __restrict__ sb,
+                                         const f4 (&x)[DIN / 16], f4 (&h)[H / 16], int g) {
+  constexpr int NT = H / 16, KX = DIN / 4, KH = H / 4;
+  f4 az[NT], ar[NT], ax[NT], ah[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int u0 = 16 * t + 4 * g;
+    az[t] = *reinterpret_cast<const f4*>(sb + 0 * H + u0);
+    ar[t] = *reinterpret_cast<const f4*>(sb + 1 * H + u0);
+    ax[t] = *reinterpret_cast<const f4*>(sb + 2 * H + u0);
+    ah[t] = *reinterpret_cast<const f4*>(sb + 3 * H + u0);
+  }
+#pragma unroll
+  for (int s = 0; s < KX; ++s) {
+    const float xb = x[s >> 2][s & 3];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      az[t] = MFMA(W.w[0][t][s], xb, az[t]);
+      ar[t] = MFMA(W.w[1][t][s], xb, ar[t]);
+      ax[t] = MFMA(W.w[2][t][s], xb, ax[t]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KH; ++s) {
+    const float hb = h[s >> 2][s & 3];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      az[t] = MFMA(W.u[0][t][s], hb, az[t]);
+      ar[t] = MFMA(W.u[1][t][s], hb, ar[t]);
+      ah[t] = MFMA(W.u[2][t][s], hb, ah[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float z = sigmoidf_(az[t][r]);
+      float rr = sigmoidf_(ar[t][r]);
+      float c = tanhf_(ax[t][r] + rr * ah[t][r]);
+      h[t][r] = z * h[t][r] + (1.0f - z) * c;
+    }
+  }
+}
+
+__device__ __forceinline__ const float* src_ptr(const SrcBases& sb, uint32_t code, int din) {
+  uint32_t slot = code >> IGN_SLOT_SHIFT;
+  uint32_t row = code & IGN_ROW_MASK;
+  const float* b = sb.base[0];
+  if (slot == 1) b = sb.base[1];
+  if (slot == 2) b = sb.base[2];
+  if (slot == 3) b = sb.base[3];
+  return b + (int64_t)row * din;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ordered / interleave / concat(axis 1) update: masked GRU over each destination's message
+// sequence (AUX:767-796 with the dense-padding semantics of GM:477-543).  One wave = 16
+// destinations of similar length (rows sorted by length, descending).  Step t of destination
+// d sums the messages whose position is t (scatter_nd accumulates duplicates; holes are zero
+// inputs); steps t >= final_len[d] leave the state unchanged (sequence_mask).
+template <int DIN, int H>
+__global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16;
+  __shared__ float sbias[4 * H];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = pos < a.n_dst;
+
+  GruWeights<DIN, H> W;
+  load_gru_weights<DIN, H>(W, a.Wp, a.Up, lane);
+
+  const int row = valid ? a.order[pos] : 0;
+  const int L = valid ? a.len[pos] : 0;
+  const int64_t sbase = valid ? a.step_ptr[pos] : 0;
+
+  f4 h[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+
+  // tile length = max over the wave (rows are sorted, but take the max to be safe)
+  int Lmax = L;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  __syncthreads();
+
+  // gather of step t for this lane: sum of the rows whose position is t
+  auto gather = [&](int t, f4 (&x)[NC]) {
+    const bool act = t < L;
+    const int64_t s = act ? sbase + t : 0;
+    int m0 = a.msg_ptr[s], m1 = a.msg_ptr[s + 1];
+    if (!act) m1 = m0;
+    const int mi = (m1 > m0) ? m0 : 0;
+    const float* p = src_ptr(a.src, a.msg_src[mi], DIN);
+    const bool any = m1 > m0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      f4 v = ld4(p + 16 * c + 4 * g);
+      x[c] = any ? v : f4{0, 0, 0, 0};
+    }
+    for (int m = m0 + 1; m < m1; ++m) {  // rare: several messages at one position
+      const float* q = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += ld4(q + 16 * c + 4 * g);
+    }
+  };
+
+  f4 x[NC], xn[NC];
+  gather(0, x);
+  for (int t = 0; t < Lmax; ++t) {
+    if (t + 1 < Lmax) gather(t + 1, xn);
+    f4 hn[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) hn[i] = h[i];
+    gru_step<DIN, H>(W, sbias, x, hn, g);
+    const bool act = t < L;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) h[i] = act ? hn[i] : h[i];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = xn[c];
+  }
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
+// updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
+// in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
+template <int DIN, int H>
+__global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16;
+  __shared__ float sbias[4 * H];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = pos < a.n_dst;
+
+  const int row = valid ? a.order[pos] : 0;
+  const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+  const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+
+  f4 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+  int64_t m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    uint32_t c0 = a.msg_src[m], c1 = a.msg_src[m + 1], c2 = a.msg_src[m + 2], c3 = a.msg_src[m + 3];
+    const float* p0 = src_ptr(a.src, c0, DIN);
+    const float* p1 = src_ptr(a.src, c1, DIN);
+    const float* p2 = src_ptr(a.src, c2, DIN);
+    const float* p3 = src_ptr(a.src, c3, DIN);
+    f4 v0[NC], v1[NC], v2[NC], v3[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      v0[c] = ld4(p0 + 16 * c + 4 * g);
+      v1[c] = ld4(p1 + 16 * c + 4 * g);
+      v2[c] = ld4(p2 + 16 * c + 4 * g);
+      v3[c] = ld4(p3 + 16 * c + 4 * g);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = (((x[c] + v0[c]) + v1[c]) + v2[c]) + v3[c];
+  }
+  for (; m < m1; ++m) {
+    const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+  }
+
+  GruWeights<DIN, H> W;
+  load_gru_weights<DIN, H>(W, a.Wp, a.Up, lane);
+  f4 h[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  __syncthreads();
+  gru_step<DIN, H>(W, sbias, x, h, g);
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused readout MLP (GM:611-629, RNJ:113-142): y = act2(act1(X W1 + b1) W2 + b2) . w3 + b3.
+// One wave = 32 rows (two 16-row B tiles).  Layer-1 activations stay in registers in the
+// accumulator layout (N1/16 tiles x 2) and feed layer 2 as B operands; layer 2 is produced
+// 16 units at a time and immediately contracted with the 1-unit output layer, so the second
+// hidden layer is never materialised.  W1/W2 fragments stream from L2 as float4 per lane.
+template <int DIN, int N1, int N2>
+__global__ __launch_bounds__(256) void readout3_kernel(Readout3Args a) {
+  constexpr int C0 = DIN / 16, U1 = N1 / 16, U2 = N2 / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + wave) * 32;
+
+  // x B fragments for the two row tiles
+  f4 xb[2][C0];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    int64_t r = base + 16 * p + j;
+    bool ok = r < a.n_rows;
+    const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
+#pragma unroll
+    for (int c = 0; c < C0; ++c) xb[p][c] = ok ? ld4(xr + 16 * c + 4 * g) : f4{0, 0, 0, 0};
+  }
+
+  f4 h1[U1][2];
+#pragma unroll
+  for (int u = 0; u < U1; ++u) {
+    f4 b = ld4(a.b1 + 16 * u + 4 * g);
+    f4 acc0 = b, acc1 = b;
+#pragma unroll
+    for (int c = 0; c < C0; ++c) {
+      f4 w = ld4(a.W1p + ((((int64_t)u * C0 + c) << 6) + lane) * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc0 = MFMA(w[q], xb[0][c][q], acc0);
+        acc1 = MFMA(w[q], xb[1][c][q], acc1);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc0[r] = act_apply(acc0[r], a.act1);
+      acc1[r] = act_apply(acc1[r], a.act1);
+    }
+    h1[u][0] = acc0;
+    h1[u][1] = acc1;
+  }
+
+  float y0 = 0.f, y1 = 0.f;
+#pragma unroll 1
+  for (int v = 0; v < U2; ++v) {
+    f4 b = ld4(a.b2 + 16 * v + 4 * g);
+    f4 acc0 = b, acc1 = b;
+    const float* wv = a.W2p + (((int64_t)v * U1) << 8) + lane * 4;
+#pragma unroll
+    for (int c = 0; c < U1; ++c) {
+      f4 w = ld4(wv + (c << 8));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc0 = MFMA(w[q], h1[c][0][q], acc0);
+        acc1 = MFMA(w[q], h1[c][1][q], acc1);
+      }
+    }
+    f4 w3 = ld4(a.w3 + 16 * v + 4 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      y0 += w3[r] * act_apply(acc0[r], a.act2);
+      y1 += w3[r] * act_apply(acc1[r], a.act2);
+    }
+  }
+  // reduce the four unit groups (lanes j, j+16, j+32, j+48)
+  y0 += __shfl_xor(y0, 16);
+  y1 += __shfl_xor(y1, 16);
+  y0 += __shfl_xor(y0, 32);
+  y1 += __shfl_xor(y1, 32);
+  if (g == 0) {
+    const float b3 = a.b3 ? a.b3[0] : 0.f;
+    int64_t r0 = base + j, r1 = base + 16 + j;
+    if (r0 < a.n_rows) a.y[r0] = act_apply(y0 + b3, a.act3);
+    if (r1 < a.n_rows) a.y[r1] = act_apply(y1 + b3, a.act3);
+  }
+}
+
+// Generic Dense layer (any shape): y[n][o] = act(sum_k x[n][k] W[k][o] + b[o]).  Used for
+// readout stacks that do not match the fused 3-layer kernel.
+__global__ void dense_generic_kernel(const float* __restrict__ x, int64_t n, int in, int x_stride,
+                                     const float* __restrict__ W, const float* __restrict__ b, int out,
+                                     int act, float* __restrict__ y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = n * (int64_t)out;
+  for (; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i / out;
+    int o = (int)(i - r * out);
+    float acc = b ? b[o] : 0.f;
+    const float* xr = x + r * x_stride;
+    for (int k = 0; k < in; ++k) acc = fmaf(xr[k], W[(int64_t)k * out + o], acc);
+    y[i] = act_apply(acc, act);
+  }
+}
+
+// Column copy used to concatenate several readout inputs (GM:615-621).
+__global__ void concat_cols_kernel(float* __restrict__ dst, int64_t n, int dst_stride, int col0,
+                                   const float* __restrict__ src, int width) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = n * (int64_t)width;
+  for (; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i / width;
+    int c = (int)(i - r * width);
+    dst[r * dst_stride + col0 + c] = src[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host-side launchers
+static inline int grid_for(int64_t n, int per_block) { return (int)((n + per_block - 1) / per_block); }
+
+hipError_t launch_init_state(float* state, const float* feats, int64_t n, int H, int F, hipStream_t st) {
+  int64_t total = n * (int64_t)H;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(init_state_kernel, dim3(blocks), dim3(256), 0, st, state, feats, n, H, F);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_gru(const float* W, const float* U, const float* bias, float* Wp, float* Up, float* bp,
+                           int DIN, int H, hipStream_t st) {
+  hipLaunchKernelGGL(pack_gru_kernel, dim3(64), dim3(256), 0, st, W, U, bias, Wp, Up, bp, DIN, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStream_t st) {
+  hipLaunchKernelGGL(pack_dense_kernel, dim3(256), dim3(256), 0, st, W, Wp, IN, OUT);
+  return hipGetLastError();
+}
+
+#define GRU_DISPATCH(KERNEL, DIN_, H_, ARGS, N)                                                      \
+  if (din == DIN_ && h == H_) {                                                                   \
+    hipLaunchKernelGGL((KERNEL<DIN_, H_>), dim3(grid_for(N, 64)), dim3(256), 0, st, ARGS);         \
+    return hipGetLastError();                                                                     \
+  }
+
+bool gru_shape_supported(int din, int h) {
+  return (din == 16 || din == 32) && (h == 16 || h == 32);
+}
+
+hipError_t launch_seq_gru(const SeqGruArgs& args, int din, int h, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  GRU_DISPATCH(seq_gru_kernel, 32, 32, args, args.n_dst)
+  GRU_DISPATCH(seq_gru_kernel, 16, 16, args, args.n_dst)
+  GRU_DISPATCH(seq_gru_kernel, 16, 32, args, args.n_dst)
+  GRU_DISPATCH(seq_gru_kernel, 32, 16, args, args.n_dst)
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  GRU_DISPATCH(sum_gru_kernel, 32, 32, args, args.n_dst)
+  GRU_DISPATCH(sum_gru_kernel, 16, 16, args, args.n_dst)
+  GRU_DISPATCH(sum_gru_kernel, 16, 32, args, args.n_dst)
+  GRU_DISPATCH(sum_gru_kernel, 32, 16, args, args.n_dst)
+  return hipErrorInvalidValue;
+}
+
+bool readout3_supported(int din, int n1, int n2) {
+  return (din == 16 || din == 32 || din == 64) && n1 == 256 && n2 == 256;
+}
+
+hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st) {
+  if (args.n_rows == 0) return hipSuccess;
+  int blocks = grid_for(args.n_rows, 128);
+  if (n1 == 256 && n2 == 256) {
+    if (din == 32) { hipLaunchKernelGGL((readout3_kernel<32, 256, 256>), dim3(blocks), dim3(256), 0, st, args); return hipGetLastError(); }
+    if (din == 16) { hipLaunchKernelGGL((readout3_kernel<16, 256, 256>), dim3(blocks), dim3(256), 0, st, args); return hipGetLastError(); }
+    if (din == 64) { hipLaunchKernelGGL((readout3_kernel<64, 256, 256>), dim3(blocks), dim3(256), 0, st, args); return hipGetLastError(); }
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
+                                int out, int act, float* y, hipStream_t st) {
+  int64_t total = n * (int64_t)out;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dense_generic_kernel, dim3(blocks), dim3(256), 0, st, x, n, in, x_stride, W, b, out, act, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,
+                              hipStream_t st) {
+  int64_t total = n * (int64_t)width;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(concat_cols_kernel, dim3(blocks), dim3(256), 0, st, dst, n, dst_stride, col0, src, width);
+  return hipGetLastError();
+}

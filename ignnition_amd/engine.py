@@ -1,0 +1,368 @@
+"""Lowering of a ``Model_information`` plan to the C ABI, parameters and batches.
+
+``MPPlan`` is the counterpart of ``ComnetModel.__init__`` (GM:235-382): it walks the MP
+stages in order and decides, per message passing, the aggregation, the GRU cell of the
+destination (one per destination entity name, GM:309-313) and the adjacency arrays each
+source reads (``src_/dst_<adj>``, ``seq_<src>_<dst>``, ``indices_<src>_to_<dst>``, exactly
+the keys of input_fn, GM:127-158).  ``Batch`` turns a list of per-graph feature dicts
+into one disjoint-union batch on the device.
+
+Parameters use Keras-style names so checkpoints read like the reference's variables:
+``<dst>_update/kernel`` [in, 3H], ``<dst>_update/recurrent_kernel`` [H, 3H],
+``<dst>_update/bias`` [2, 3H], ``readout_model_0/<layer>/kernel`` / ``bias``.
+"""
+
+from __future__ import annotations
+
+import atexit
+import ctypes as C
+import weakref
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+SUPPORTED_GRU_KEYS = {"units", "name"}
+
+# Live handles, released explicitly at interpreter exit (batches before plans) while the HIP
+# runtime is still up; relying on __del__ during module teardown can run after it is gone.
+_LIVE_BATCHES: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE_ENGINES: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _release_all():
+    for b in list(_LIVE_BATCHES):
+        b.close()
+    for e in list(_LIVE_ENGINES):
+        e.close()
+
+
+class UnsupportedModel(ValueError):
+    pass
+
+
+@dataclass
+class AdjSlot:
+    adj: str
+    src: str
+    dst: str
+
+    @property
+    def keys(self):
+        return "src_" + self.adj, "dst_" + self.adj, "seq_" + self.src + "_" + self.dst
+
+
+@dataclass
+class MPPlan:
+    """The lowered plan (entities, adjacency slots, MPs, cells, readout)."""
+    model_info: object
+    entities: list = field(default_factory=list)       # names
+    hidden: list = field(default_factory=list)
+    features: list = field(default_factory=list)       # [(name, size)] per entity
+    adj_slots: list = field(default_factory=list)
+    il_slots: list = field(default_factory=list)       # indices_<src>_to_<dst> keys
+    mps: list = field(default_factory=list)            # dicts
+    cells: list = field(default_factory=list)          # [(dst_name, din, H)]
+    readout_inputs: list = field(default_factory=list)
+    dense: list = field(default_factory=list)          # [(name, units, act, use_bias, l2)]
+    iterations: int = 0
+    readout_label: str = ""
+
+    @classmethod
+    def from_model_info(cls, mi) -> "MPPlan":
+        p = cls(model_info=mi)
+        p.iterations = mi.get_mp_iterations()
+        for e in mi.get_entities():
+            p.entities.append(e.name)
+            h = int(e.hidden_state_dimension)
+            if h != e.hidden_state_dimension:
+                raise UnsupportedModel("non-integer hidden_state_dimension")
+            p.hidden.append(h)
+            p.features.append([(f.name, int(f.size)) for f in e.features])
+        eidx = {n: i for i, n in enumerate(p.entities)}
+        cell_of = {}
+        for stage_name, mps in mi.get_mp_instances():
+            for mp in mps:
+                dst = mp.destination_entity
+                upd = mp.update
+                if upd.type != "recurrent_nn":
+                    # GM:324-346 references an undefined `mp` (NameError): the reference cannot build it.
+                    raise UnsupportedModel("feed-forward update is not executable in the reference (GM:338)")
+                cell = upd.model
+                if cell.type != "GRU":
+                    raise UnsupportedModel("recurrent_type %s is not lowered (only GRU; LSTM passes one state, "
+                                           "AUX:764)" % cell.type)
+                extra = set(cell.parameters) - SUPPORTED_GRU_KEYS
+                if extra:
+                    raise UnsupportedModel("GRU options %s are not lowered (Keras defaults only)" % sorted(extra))
+                aggr = mp.aggregation.type
+                if aggr not in ("sum", "ordered", "interleave", "concat"):
+                    raise UnsupportedModel("aggregation %r is not lowered yet" % aggr)
+                if aggr == "concat" and mp.aggregation.concat_axis != 1:
+                    raise UnsupportedModel("concat aggregation on axis 2 is not lowered yet")
+                srcs = []
+                din = None
+                for s in mp.source_entities:
+                    for op in s.message_formation:
+                        if op.type != "direct_assignation":
+                            raise UnsupportedModel("message-creation neural networks are not lowered yet")
+                    slot = AdjSlot(s.adj_vector, s.name, dst)
+                    if slot not in p.adj_slots:
+                        p.adj_slots.append(slot)
+                    il = -1
+                    if aggr == "interleave":
+                        key = "indices_" + s.name + "_to_" + dst
+                        if key not in p.il_slots:
+                            p.il_slots.append(key)
+                        il = p.il_slots.index(key)
+                    srcs.append((eidx[s.name], p.adj_slots.index(slot), il))
+                    din = p.hidden[eidx[s.name]]
+                if dst not in cell_of:
+                    cell_of[dst] = len(p.cells)
+                    p.cells.append((dst, din, p.hidden[eidx[dst]]))
+                p.mps.append({"dst": eidx[dst], "aggr": aggr, "axis": getattr(mp.aggregation, "concat_axis", 0),
+                              "cell": cell_of[dst], "sources": srcs, "stage": stage_name})
+        preds = [op for op in mi.get_readout_operations() if op.type == "predict"]
+        others = [op for op in mi.get_readout_operations() if op.type != "predict"]
+        if others:
+            raise UnsupportedModel("readout operations %s are not lowered yet" % [o.type for o in others])
+        if len(preds) != 1:
+            raise UnsupportedModel("exactly one predict operation is required")
+        op = preds[0]
+        p.readout_label = op.label
+        for name in op.input:
+            if name not in eidx:
+                raise UnsupportedModel("readout input %r is not an entity state" % name)
+            p.readout_inputs.append(eidx[name])
+        for l in op.architecture.layers:
+            if l.type != "Dense":
+                raise UnsupportedModel("readout layer type %s is not lowered (Dense only)" % l.type)
+            prm = dict(l.parameters)
+            act = prm.get("activation", None)
+            if act not in _lib.ACT:
+                raise UnsupportedModel("activation %r not supported" % act)
+            known = {"units", "activation", "kernel_regularizer", "name", "use_bias"}
+            if set(prm) - known:
+                raise UnsupportedModel("Dense options %s are not lowered" % sorted(set(prm) - known))
+            p.dense.append((prm.get("name"), int(prm["units"]), _lib.ACT[act], int(bool(prm.get("use_bias", True))),
+                            float(prm.get("kernel_regularizer", 0.0) or 0.0)))
+        return p
+
+    # ------------------------------------------------------------------ C structures
+    def to_desc(self):
+        keep = []
+        ents = (_lib.EntityDesc * len(self.entities))(
+            *[_lib.EntityDesc(h, sum(s for _, s in f)) for h, f in zip(self.hidden, self.features)])
+        mps = (_lib.MPDesc * len(self.mps))()
+        for i, m in enumerate(self.mps):
+            srcs = (_lib.SourceDesc * len(m["sources"]))(*[_lib.SourceDesc(*s) for s in m["sources"]])
+            keep.append(srcs)
+            mps[i] = _lib.MPDesc(m["dst"], _lib.AGGR[m["aggr"]], int(m["axis"] or 0), m["cell"], len(m["sources"]),
+                                 C.cast(srcs, C.POINTER(_lib.SourceDesc)))
+        cells = (_lib.CellDesc * len(self.cells))(*[_lib.CellDesc(din, h) for _, din, h in self.cells])
+        ro = (C.c_int32 * len(self.readout_inputs))(*self.readout_inputs)
+        dense = (_lib.DenseDesc * len(self.dense))(*[_lib.DenseDesc(u, a, b) for _, u, a, b, _ in self.dense])
+        keep += [ents, mps, cells, ro, dense]
+        d = _lib.PlanDesc(self.iterations, len(self.entities), ents, len(self.adj_slots), len(self.il_slots),
+                          len(self.mps), mps, len(self.cells), cells, len(self.readout_inputs), ro,
+                          len(self.dense), dense)
+        return d, keep
+
+    # ------------------------------------------------------------------ parameters
+    def param_specs(self):
+        """[(name, shape)] in the engine's tensor order (ign_plan_param_tensor)."""
+        specs = []
+        for dst, din, h in self.cells:
+            specs += [(dst + "_update/kernel", (din, 3 * h)), (dst + "_update/recurrent_kernel", (h, 3 * h)),
+                      (dst + "_update/bias", (2, 3 * h))]
+        width = sum(self.hidden[e] for e in self.readout_inputs)
+        fan_in = width
+        for li, (name, units, _, use_bias, _) in enumerate(self.dense):
+            lname = name or ("layer_%d" % li)
+            specs += [("readout_model_0/" + lname + "/kernel", (fan_in, units)),
+                      ("readout_model_0/" + lname + "/bias", (units,))]
+            fan_in = units
+        return specs
+
+    def init_params(self, seed: int = 0, bias_scale: float = 0.0) -> dict:
+        """Keras default initialisers: glorot_uniform kernels, orthogonal recurrent kernels, zero
+        biases (``bias_scale`` > 0 draws biases uniformly instead, for tests)."""
+        rng = np.random.default_rng(seed)
+        out = {}
+        for name, shape in self.param_specs():
+            if name.endswith("recurrent_kernel"):
+                a = rng.standard_normal((shape[1], shape[0]))
+                q, r = np.linalg.qr(a)
+                q = q * np.sign(np.diag(r))
+                out[name] = q.T.astype(np.float32)
+            elif name.endswith("kernel"):
+                lim = np.sqrt(6.0 / (shape[0] + shape[1]))
+                out[name] = rng.uniform(-lim, lim, shape).astype(np.float32)
+            else:
+                out[name] = (rng.uniform(-bias_scale, bias_scale, shape).astype(np.float32) if bias_scale
+                             else np.zeros(shape, np.float32))
+        return out
+
+
+class Engine:
+    """A plan on one device (``ign_plan``)."""
+
+    def __init__(self, plan: MPPlan, device: int = 0):
+        self.plan = plan
+        self.device = device
+        desc, self._keep = plan.to_desc()
+        h = C.c_void_p()
+        check(lib.ign_plan_create(C.byref(desc), device, C.byref(h)))
+        self.handle = h
+        _LIVE_ENGINES.add(self)
+        n = C.c_int64()
+        check(lib.ign_plan_num_params(h, C.byref(n)))
+        self.n_params = n.value
+        nt = C.c_int32()
+        check(lib.ign_plan_num_param_tensors(h, C.byref(nt)))
+        self.layout = []
+        specs = plan.param_specs()
+        if nt.value != len(specs):
+            raise RuntimeError("parameter layout mismatch between host and engine")
+        for i in range(nt.value):
+            kind, owner, off, rows, cols = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32(), C.c_int32()
+            check(lib.ign_plan_param_tensor(h, i, C.byref(kind), C.byref(owner), C.byref(off), C.byref(rows),
+                                            C.byref(cols)))
+            name, shape = specs[i]
+            if int(np.prod(shape)) != rows.value * cols.value:
+                raise RuntimeError("parameter %s: engine shape %dx%d vs host %s" % (name, rows.value, cols.value, shape))
+            self.layout.append((name, shape, off.value))
+
+    def set_params(self, params: dict):
+        flat = np.zeros(self.n_params, np.float32)
+        for name, shape, off in self.layout:
+            v = np.ascontiguousarray(params[name], dtype=np.float32).reshape(-1)
+            flat[off:off + v.size] = v
+        check(lib.ign_plan_set_params(self.handle, flat.ctypes.data_as(C.c_void_p), 0))
+
+    def set_timing(self, on: bool):
+        check(lib.ign_plan_set_timing(self.handle, int(on)))
+
+    def stats(self) -> dict:
+        s = _lib.Stats()
+        check(lib.ign_stats(self.handle, C.byref(s)))
+        return {k: {"launches": s.launches[i], "ms": s.ms[i], "flops": s.flops[i], "bytes": s.bytes[i]}
+                for i, k in enumerate(_lib.KERNEL_KINDS)}
+
+    def synchronize(self):
+        check(lib.ign_synchronize(self.handle))
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h:
+            lib.ign_plan_destroy(h)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+def _i64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int64).reshape(-1))
+
+
+class Batch:
+    """A disjoint-union batch of graphs on the device (``ign_batch``).
+
+    ``graphs``: list of feature dicts with the input_fn keys (GM:127-158), features already
+    normalised.  Graph-local indices are kept; the engine offsets them per graph."""
+
+    def __init__(self, engine: Engine, graphs: list):
+        p = engine.plan
+        self.engine = engine
+        G = len(graphs)
+        E = len(p.entities)
+        num = np.zeros((G, E), np.int64)
+        for g, x in enumerate(graphs):
+            for e, name in enumerate(p.entities):
+                num[g, e] = int(np.asarray(x["num_" + name]).reshape(()))
+        feats = []
+        for e, name in enumerate(p.entities):
+            cols = []
+            for fname, size in p.features[e]:
+                parts = [np.asarray(x[fname], np.float32).reshape(int(num[g, e]), size) for g, x in enumerate(graphs)]
+                cols.append(np.concatenate(parts, 0) if parts else np.zeros((0, size), np.float32))
+            feats.append(np.ascontiguousarray(np.concatenate(cols, 1)) if cols else None)
+        A = len(p.adj_slots)
+        cnt = np.zeros((G, A), np.int64)
+        srcs, dsts, seqs = [], [], []
+        for a, slot in enumerate(p.adj_slots):
+            ks, kd, kq = slot.keys
+            s_parts, d_parts, q_parts = [], [], []
+            for g, x in enumerate(graphs):
+                s, d, q = _i64(x[ks]), _i64(x[kd]), _i64(x[kq])
+                if not (len(s) == len(d) == len(q)):
+                    raise ValueError("graph %d: %s/%s/%s have different lengths" % (g, ks, kd, kq))
+                cnt[g, a] = len(s)
+                s_parts.append(s), d_parts.append(d), q_parts.append(q)
+            srcs.append(np.concatenate(s_parts)), dsts.append(np.concatenate(d_parts)), seqs.append(np.concatenate(q_parts))
+        I = len(p.il_slots)
+        il_len = np.zeros((G, max(I, 1)), np.int64)
+        ils = []
+        for i, key in enumerate(p.il_slots):
+            parts = []
+            for g, x in enumerate(graphs):
+                v = _i64(x[key])
+                il_len[g, i] = len(v)
+                parts.append(v)
+            ils.append(np.concatenate(parts))
+        self._arrays = (num, feats, cnt, srcs, dsts, seqs, il_len, ils)
+        fp = C.POINTER(C.c_float)
+        lp = C.POINTER(C.c_int64)
+        feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
+        mk = lambda arrs: (lp * max(len(arrs), 1))(*[a.ctypes.data_as(lp) for a in arrs])
+        desc = _lib.BatchDesc(G, num.ctypes.data_as(lp), feat_ptrs, cnt.ctypes.data_as(lp), mk(srcs), mk(dsts),
+                              mk(seqs), il_len.ctypes.data_as(lp), mk(ils))
+        h = C.c_void_p()
+        check(lib.ign_batch_create(engine.handle, C.byref(desc), C.byref(h)))
+        self.handle = h
+        _LIVE_BATCHES.add(self)
+        info = _lib.BatchInfo()
+        check(lib.ign_batch_info(h, C.byref(info)))
+        self.num_graphs = info.num_graphs
+        self.predictions = info.predictions
+        self.output_units = info.output_units
+        self.edges_per_forward = info.edges_per_forward
+        self.gru_steps_per_forward = info.gru_steps_per_forward
+        self.rows = list(info.rows)[:E]
+        self.graph_rows = num
+        self._arrays = None  # the engine copied what it needs
+
+    def forward(self, to_host: bool = True):
+        eng = self.engine
+        if to_host:
+            out = np.empty((self.predictions, self.output_units), np.float32)
+            check(lib.ign_forward(eng.handle, self.handle, out.ctypes.data_as(C.c_void_p)))
+            return out
+        check(lib.ign_forward(eng.handle, self.handle, None))
+        return None
+
+    def state(self, entity: str) -> np.ndarray:
+        p = self.engine.plan
+        e = p.entities.index(entity)
+        out = np.empty((self.rows[e], p.hidden[e]), np.float32)
+        check(lib.ign_batch_state(self.engine.handle, self.handle, e, out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h:
+            lib.ign_batch_destroy(h)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+def device_count() -> int:
+    n = C.c_int32()
+    lib.ign_device_count(C.byref(n))
+    return n.value

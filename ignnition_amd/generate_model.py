@@ -1,0 +1,163 @@
+"""Host half of ``code/utils/generate_model.py`` (GM) on top of the HIP engine.
+
+* ``set_model_info``      GM:34-43
+* ``normalization``       GM:46-86  user functions resolved *by name* from the user's
+                                    namespace (the reference uses ``eval`` on ``from main import *``)
+* ``batching_func`` / ``input_fn``  GM:89-198 (a host iterator instead of tf.data)
+* ``r_squared``           GM:201-216 (numpy)
+* ``ComnetModel``         GM:219-694: construction lowers the plan to ``libignmp.so``;
+                          ``__call__`` runs one graph, ``predict_batch`` a disjoint-union
+                          batch of graphs (what ``model_fn`` does graph by graph, GM:712-724).
+"""
+
+from __future__ import annotations
+
+import logging
+import sys
+
+import numpy as np
+
+from .engine import Batch, Engine, MPPlan
+from .generator import generator
+
+log = logging.getLogger("ignnition_amd")
+
+model_info = None
+user_namespace: dict = {}
+
+
+def set_model_info(model_description):
+    """GM:34-43."""
+    global model_info
+    model_info = model_description
+
+
+def register_user_functions(namespace: dict):
+    """The reference reaches the user's normalization functions through ``from main import *``
+    (GM:24) and ``eval(name)``; here the caller hands its namespace over explicitly."""
+    user_namespace.update(namespace)
+
+
+def _resolve(name):
+    if name in user_namespace:
+        return user_namespace[name]
+    main = sys.modules.get("__main__")
+    if main is not None and hasattr(main, name):
+        return getattr(main, name)
+    raise KeyError(name)
+
+
+def normalization(x, feature_list, output_name, output_normalization, y=None):
+    """GM:46-86."""
+    for f in feature_list:
+        norm_type = f.normalization
+        if str(norm_type) != "None":
+            try:
+                x[f.name] = _resolve(norm_type)(np.asarray(x[f.name], np.float32), f.name)
+            except KeyError:
+                log.error("IGNNITION: The normalization function " + str(norm_type) + " is not defined in the main file.")
+                sys.exit(1)
+    if str(output_normalization) != "None" and y is not None:
+        try:
+            y = _resolve(output_normalization)(np.asarray(y, np.float32), output_name)
+        except KeyError:
+            log.error("IGNNITION: The normalization function " + str(output_normalization) +
+                      " is not defined in the main file.")
+            sys.exit(1)
+        return x, y
+    return x
+
+
+def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True):
+    """GM:102-198: generator -> normalization -> repeat -> batches of ``batch_size`` graphs."""
+    mi = model_info
+    feature_list = mi.get_all_features()
+    adjacency_info = mi.get_adjecency_info()
+    interleave_list = mi.get_interleave_tensors()
+    output_name, output_normalization, _ = mi.get_output_info()
+    additional_input = mi.get_additional_input_names()
+    unique_additional_input = [a for a in additional_input if a not in [f.name for f in feature_list]]
+    feature_names = [f.name for f in feature_list]
+
+    def stream():
+        while True:
+            n = 0
+            for item in generator(data_dir, feature_names, output_name, adjacency_info, interleave_list,
+                                  unique_additional_input, training, shuffle):
+                n += 1
+                if training:
+                    xs, ys = item
+                    yield normalization(xs, feature_list, output_name, output_normalization, ys)
+                else:
+                    yield normalization(item, feature_list, output_name, output_normalization)
+            if not repeat or n == 0:
+                return
+
+    it = stream()
+    while True:
+        batch = []
+        for _ in range(batch_size):
+            try:
+                batch.append(next(it))
+            except StopIteration:
+                break
+        if not batch:
+            return
+        if training:
+            yield [b[0] for b in batch], [b[1] for b in batch]
+        else:
+            yield batch
+
+
+def r_squared(labels, predictions):
+    """GM:201-216 (value of the streaming mean for one batch)."""
+    labels = np.asarray(labels, np.float64)
+    predictions = np.asarray(predictions, np.float64)
+    total_error = np.sum(np.square(labels - labels.mean()))
+    unexplained_error = np.sum(np.square(labels - predictions))
+    return 1.0 - unexplained_error / total_error
+
+
+class ComnetModel:
+    """GM:219-694, executed by the HIP engine."""
+
+    def __init__(self, model_description=None, device: int = 0, params: dict | None = None, seed: int = 0):
+        mi = model_description if model_description is not None else model_info
+        if mi is None:
+            raise RuntimeError("set_model_info() first (GM:34)")
+        self.model_info = mi
+        self.plan = MPPlan.from_model_info(mi)
+        self.engine = Engine(self.plan, device)
+        self.params = params if params is not None else self.plan.init_params(seed)
+        self.engine.set_params(self.params)
+
+    def set_params(self, params: dict):
+        self.params = params
+        self.engine.set_params(params)
+
+    @property
+    def trainable_variables(self):
+        return self.params
+
+    @property
+    def losses(self):
+        """Keras ``model.losses``: l2 terms of the readout kernel_regularizers (AUX:833-834)."""
+        out = []
+        for (name, _, _, _, l2), (pname, _) in zip(self.plan.dense, [s for s in self.plan.param_specs()
+                                                                      if s[0].startswith("readout_model_0/")
+                                                                      and s[0].endswith("/kernel")]):
+            if l2:
+                w = np.asarray(self.params[pname], np.float64)
+                out.append(l2 * float((w * w).sum()))
+        return out
+
+    def batch(self, graphs: list) -> Batch:
+        return Batch(self.engine, graphs)
+
+    def predict_batch(self, graphs: list) -> np.ndarray:
+        """Flattened predictions of every graph, concatenated in batch order (GM:716-724)."""
+        return self.batch(graphs).forward().reshape(-1)
+
+    def __call__(self, input: dict, training: bool = False) -> np.ndarray:
+        """``ComnetModel.call`` (GM:384) for one graph: [P, units] predictions."""
+        return self.batch([input]).forward()

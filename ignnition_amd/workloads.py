@@ -1,0 +1,95 @@
+"""Synthetic workloads for tests and bench: samples -> GEN index dicts -> normalised inputs.
+
+The normalisation functions restate the examples' ``main.py`` (RNM:26-38, QSM:27-39) on
+numpy (the reference's use ``tf.math.log``).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import model_examples, synthetic
+from .framework_operations import dimensions_of_sample
+from .generator import sample_to_data
+from .json_operations import Model_information
+
+
+def normalization_routenet(feature, feature_name):
+    """RNM:26-31."""
+    if feature_name == "traffic":
+        feature = (feature - 170) / 130
+    if feature_name == "link_capacity":
+        feature = (feature - 25000) / 40000
+    return feature
+
+
+def normalization_queue_size(feature, feature_name):
+    """QSM:27-39 / MAIN:26-38."""
+    if feature_name == "delay":
+        feature = (np.log(feature) + 1.78) / 0.93
+    if feature_name == "traffic":
+        feature = (feature - 0.28) / 0.15
+    if feature_name == "jitter":
+        feature = (feature - 1.5) / 1.5
+    if feature_name == "link_capacity":
+        feature = (feature - 27.0) / 14.86
+    if feature_name == "queue_sizes":
+        feature = (feature - 16.5) / 15.5
+    return feature
+
+
+def log(feature, feature_name):
+    return np.log(feature)
+
+
+def exp(feature, feature_name):
+    return np.exp(feature)
+
+
+USER_FUNCTIONS = {"normalization_routenet": normalization_routenet,
+                  "normalization_queue_size": normalization_queue_size, "log": log, "exp": exp}
+
+
+def model(kind: str):
+    """(description dict, Model_information) for 'routenet' or 'qsize'."""
+    desc = model_examples.routenet() if kind == "routenet" else model_examples.qsize()
+    sample = synthetic.routenet_sample("nsfnet", 0, qsize=(kind == "qsize"))
+    dims = dimensions_of_sample(sample)
+    return desc, dims, Model_information(desc, dims)
+
+
+def graph_inputs(mi, samples, normalize: bool = True):
+    """GEN + normalisation (GM:46-86) for a list of samples -> (inputs, labels)."""
+    feature_list = mi.get_all_features()
+    names = [f.name for f in feature_list]
+    out_name, out_norm, _ = mi.get_output_info()
+    graphs, labels = [], []
+    for s in samples:
+        data, y = sample_to_data(s, names, out_name, mi.get_adjecency_info(), mi.get_interleave_tensors(), [], True)
+        if normalize:
+            for f in feature_list:
+                if str(f.normalization) != "None":
+                    data[f.name] = USER_FUNCTIONS[f.normalization](np.asarray(data[f.name], np.float32), f.name)
+            if out_norm is not None and str(out_norm) != "None":
+                y = USER_FUNCTIONS[out_norm](np.asarray(y, np.float32), out_name)
+        graphs.append(data)
+        labels.append(np.asarray(y, np.float32))
+    return graphs, labels
+
+
+def make_batch_inputs(kind: str, topology: str, n_graphs: int, first_id: int = 0):
+    desc, dims, mi = model(kind)
+    samples = [synthetic.routenet_sample(topology, first_id + g, qsize=(kind == "qsize")) for g in range(n_graphs)]
+    graphs, labels = graph_inputs(mi, samples)
+    return desc, dims, mi, graphs, labels
+
+
+def edges_per_forward(mi, graphs) -> int:
+    """B x T x sum over MPs and sources of |adj|."""
+    T = mi.get_mp_iterations()
+    tot = 0
+    for _, mps in mi.get_mp_instances():
+        for mp in mps:
+            for s in mp.source_entities:
+                tot += sum(len(g["src_" + s.adj_vector]) for g in graphs)
+    return T * tot

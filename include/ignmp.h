@@ -1,0 +1,186 @@
+/*
+ * ignmp.h — C ABI of the MI355X message-passing engine (libignmp.so).
+ *
+ * This is the drop-in boundary for IGNNITION's hot path: the multi-stage
+ * message-passing loop + readout that the reference lowers to TensorFlow ops in
+ * ComnetModel.call (code/utils/generate_model.py:384-658).  The reference's own
+ * boundary is a Python/Keras operator:
+ *
+ *   ComnetModel()                       generate_model.py:235-382  (plan from Model_information)
+ *   ComnetModel.call(input, training)   generate_model.py:384      (feature dict -> [P,1] predictions)
+ *
+ * whose input dict is fixed by input_fn (generate_model.py:127-158): per feature a
+ * float vector, per adjacency src_<adj>/dst_<adj> int64 [E], seq_<srcEnt>_<dstEnt>
+ * int64 [E], num_<entity> int64 scalar, indices_<src>_to_<dst> int64 [L].
+ *
+ *   ign_plan_create     <-> ComnetModel.__init__  (GM:235-382): entities, MP stages,
+ *                           GRU cells (one per destination entity, GM:309-313),
+ *                           readout Dense stack (GM:350-358, AUX:918-975).
+ *   ign_plan_set_params <-> the Keras variables (kernel / recurrent_kernel / bias,
+ *                           Dense kernel / bias) — layout from ign_plan_param_tensor.
+ *   ign_batch_create    <-> the feature dict of input_fn (GM:127-158) for a batch of
+ *                           graphs (model_fn's per-graph loop, GM:712-724, becomes
+ *                           one disjoint-union batch; exact for sum/ordered/interleave
+ *                           + predict).
+ *   ign_forward         <-> model(f) for every graph + concat of the flattened
+ *                           predictions in batch order (GM:716-724).
+ *
+ * Conventions: plain C types only.  Status 0 = OK, negative = error class; the
+ * message of the last error on the calling thread is ign_last_error().  The caller
+ * owns every host array passed in (borrowed for the call); plans and batches own
+ * their device memory.  Calls on one plan are not reentrant; one plan per thread.
+ * There is no CPU execution path: every compute entry point runs HIP kernels on
+ * the plan's device and fails with IGN_ERR_DEVICE when no GPU is present.
+ */
+#ifndef IGNMP_H
+#define IGNMP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IGN_ABI_VERSION 1
+
+enum ign_status {
+  IGN_OK = 0,
+  IGN_ERR_INVALID = -1,      /* malformed plan/batch (reference: ValueError / InvalidArgument) */
+  IGN_ERR_UNSUPPORTED = -2,  /* schema-legal but not (yet) lowered: FF update, attention, ... */
+  IGN_ERR_DEVICE = -3,       /* no GPU / HIP runtime error */
+  IGN_ERR_OOM = -4,
+  IGN_ERR_RUNTIME = -5
+};
+
+enum ign_aggregation {        /* AUX:229-456, dispatch GM:547-569 */
+  IGN_AGGR_SUM = 0,
+  IGN_AGGR_ORDERED = 1,
+  IGN_AGGR_INTERLEAVE = 2,
+  IGN_AGGR_CONCAT = 3,
+  IGN_AGGR_ATTENTION = 4,
+  IGN_AGGR_CONVOLUTION = 5
+};
+
+enum ign_activation {         /* Dense activations accepted by the readout (AUX:836-837) */
+  IGN_ACT_LINEAR = 0,          /* "None" / "linear" */
+  IGN_ACT_RELU = 1,
+  IGN_ACT_SELU = 2,
+  IGN_ACT_SIGMOID = 3,
+  IGN_ACT_TANH = 4
+};
+
+typedef struct ign_plan ign_plan;
+typedef struct ign_batch ign_batch;
+
+typedef struct {
+  int32_t hidden_dim;              /* hidden_state_dimension (AUX:101) */
+  int32_t feature_total;           /* sum of feature sizes, features concatenated in listed order (AUX:140-153) */
+} ign_entity_desc;
+
+typedef struct {
+  int32_t entity;                  /* source entity index */
+  int32_t adjacency;               /* adjacency slot: index into ign_batch_desc.adj_* */
+  int32_t interleave;              /* interleave slot (indices_<src>_to_<dst>) or -1 */
+} ign_source_desc;
+
+typedef struct {
+  int32_t dst_entity;              /* GM:415 */
+  int32_t aggregation;             /* enum ign_aggregation */
+  int32_t concat_axis;             /* for IGN_AGGR_CONCAT (AUX:456) */
+  int32_t cell;                    /* GRU cell index (one per destination entity name, GM:313) */
+  int32_t num_sources;
+  const ign_source_desc* sources;  /* in model_description order (GM:423) */
+} ign_mp_desc;
+
+typedef struct {
+  int32_t input_dim;               /* message dimension fed to the cell */
+  int32_t units;                   /* = hidden_dim of the destination (AUX:747) */
+} ign_cell_desc;
+
+typedef struct {
+  int32_t units;
+  int32_t activation;              /* enum ign_activation */
+  int32_t use_bias;
+} ign_dense_desc;
+
+typedef struct {
+  int32_t num_iterations;          /* GM:406 */
+  int32_t num_entities;
+  const ign_entity_desc* entities;
+  int32_t num_adjacencies;
+  int32_t num_interleave;
+  int32_t num_mps;                 /* stages flattened in execution order (GM:410-414) */
+  const ign_mp_desc* mps;
+  int32_t num_cells;
+  const ign_cell_desc* cells;
+  int32_t num_readout_inputs;      /* predict op inputs, concatenated on axis 1 (GM:615-621) */
+  const int32_t* readout_inputs;   /* entity indices */
+  int32_t num_dense;
+  const ign_dense_desc* dense;     /* readout Dense stack (RNJ:113-142) */
+} ign_plan_desc;
+
+typedef struct {
+  int32_t num_graphs;
+  const int64_t* num_nodes;        /* [num_graphs][num_entities]  num_<entity> per graph */
+  const float* const* features;    /* [num_entities] -> [sum_g N_e(g)][feature_total] (NULL if no features) */
+  const int64_t* adj_edges;        /* [num_graphs][num_adjacencies] edges per graph */
+  const int64_t* const* adj_src;   /* [num_adjacencies] -> graph-concatenated, graph-local src_<adj> */
+  const int64_t* const* adj_dst;   /* graph-local dst_<adj> */
+  const int64_t* const* adj_seq;   /* seq_<srcEnt>_<dstEnt> */
+  const int64_t* interleave_len;   /* [num_graphs][num_interleave] */
+  const int64_t* const* interleave_idx; /* [num_interleave] -> graph-concatenated indices_<src>_to_<dst> */
+} ign_batch_desc;
+
+typedef struct {
+  int64_t num_graphs;
+  int64_t predictions;             /* rows of the predict entity (outputs = predictions * last units) */
+  int64_t output_units;
+  int64_t edges_per_forward;       /* T * sum over MPs and sources of |adj| */
+  int64_t gru_steps_per_forward;   /* GRU cell applications (per destination row / sequence step) */
+  int64_t rows[8];                 /* total rows per entity (first 8 entities) */
+} ign_batch_info_t;
+
+/* Per-kernel timing of the last forward (HIP events on the plan stream, enabled by
+ * ign_plan_set_timing).  kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 other */
+typedef struct {
+  int32_t kinds;
+  int64_t launches[8];
+  double  ms[8];
+  double  flops[8];                /* algorithmic FLOPs of those launches */
+  double  bytes[8];                /* algorithmic HBM bytes of those launches */
+} ign_stats_t;
+
+int  ign_abi_version(void);
+const char* ign_last_error(void);
+int  ign_device_count(int32_t* n);
+
+int  ign_plan_create(const ign_plan_desc* desc, int32_t device, ign_plan** out);
+void ign_plan_destroy(ign_plan* plan);
+int  ign_plan_num_params(const ign_plan* plan, int64_t* n_floats);
+int  ign_plan_num_param_tensors(const ign_plan* plan, int32_t* n);
+/* tensor i: kind 0 gru kernel [in,3H], 1 gru recurrent_kernel [H,3H], 2 gru bias [2,3H],
+ *           3 dense kernel [in,out], 4 dense bias [1,out]; owner = cell or dense index */
+int  ign_plan_param_tensor(const ign_plan* plan, int32_t i, int32_t* kind, int32_t* owner,
+                           int64_t* offset, int32_t* rows, int32_t* cols);
+int  ign_plan_set_params(ign_plan* plan, const float* params, int32_t on_device);
+int  ign_plan_set_timing(ign_plan* plan, int32_t enabled);
+int  ign_plan_set_stream(ign_plan* plan, void* hip_stream);
+
+int  ign_batch_create(ign_plan* plan, const ign_batch_desc* desc, ign_batch** out);
+void ign_batch_destroy(ign_batch* batch);
+int  ign_batch_info(const ign_batch* batch, ign_batch_info_t* out);
+
+/* Full forward (hidden-state init, T x stages x MPs, readout) on the plan stream.
+ * pred_out: host pointer (copied + synchronised) or NULL (stays on device, async).  */
+int  ign_forward(ign_plan* plan, ign_batch* batch, float* pred_out);
+int  ign_synchronize(ign_plan* plan);
+/* Device pointer of the batch's prediction buffer (valid until ign_batch_destroy). */
+int  ign_batch_predictions(ign_batch* batch, const float** dev_ptr);
+/* Copy the current hidden state of an entity (after ign_forward) to host [rows][H]. */
+int  ign_batch_state(ign_plan* plan, ign_batch* batch, int32_t entity, float* host_out);
+int  ign_stats(const ign_plan* plan, ign_stats_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IGNMP_H */

@@ -1,0 +1,26 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+
+
+@pytest.fixture(scope="session")
+def gen_fixtures():
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "gen_fixtures.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="session")
+def plan_fixtures():
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "plan_fixtures.json")) as fh:
+        return json.load(fh)

@@ -1,0 +1,196 @@
+"""HIP engine vs the oracle, through the C ABI (MI355X only).
+
+Tolerance (fp32 engine vs float64 oracle, after T=8 iterations and the readout):
+  |engine - oracle| <= 1e-4 * max(1, |oracle|)         
+Hidden states are checked with the same bound.  Indices are integer and exact by
+construction (the engine consumes the generator's arrays unchanged).
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from ignnition_amd import _lib, model_examples, synthetic, workloads
+from ignnition_amd.engine import Batch, Engine, MPPlan, device_count
+from ignnition_amd.json_operations import Model_information
+from oracle.dense_forward import DenseOracle
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _close(got, exp, tol=TOL):
+    got = np.asarray(got, np.float64).reshape(-1)
+    exp = np.asarray(exp, np.float64).reshape(-1)
+    err = np.abs(got - exp) / np.maximum(1.0, np.abs(exp))
+    assert got.shape == exp.shape
+    assert np.all(np.isfinite(got))
+    assert err.max() <= tol, "max scaled error %.3g at %d" % (err.max(), int(err.argmax()))
+
+
+def _run(desc, dims, graphs, seed=0, bias=0.05):
+    mi = Model_information(copy.deepcopy(desc), dims)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(seed, bias_scale=bias)
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    b = Batch(eng, graphs)
+    out = b.forward()
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    return out, ref, b, prm
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+
+
+@pytest.mark.parametrize("kind,topo,n", [("routenet", "nsfnet", 1), ("routenet", "nsfnet", 3),
+                                         ("routenet", "geant2", 2), ("qsize", "nsfnet", 2)])
+def test_forward_matches_oracle(kind, topo, n):
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(kind, topo, n)
+    out, ref, b, _ = _run(desc, dims, graphs)
+    _close(out, ref)
+    assert b.edges_per_forward == workloads.edges_per_forward(mi, graphs)
+
+
+@pytest.mark.parametrize("hidden", [16, 32])
+def test_hidden_sizes(hidden):
+    desc = model_examples.routenet(hidden=hidden, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", 11)])
+    out, ref, _, _ = _run(desc, dims, graphs, seed=2, bias=0.3)
+    _close(out, ref)
+
+
+def test_zero_gru_known_answer_on_gpu():
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 1)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(0)
+    for k in prm:
+        if "_update/" in k:
+            prm[k] = np.zeros_like(prm[k])
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    b = Batch(eng, graphs)
+    b.forward()
+    g = graphs[0]
+    L = np.bincount(np.asarray(g["dst_adj_links_paths"]), minlength=g["num_path"])
+    path = b.state("path")
+    np.testing.assert_allclose(path[:, 0], np.asarray(g["traffic"]) * 0.5 ** (8 * L), rtol=1e-6, atol=1e-30)
+    assert np.all(path[:, 1:] == 0)
+
+
+def test_interleave_holes_and_dropped_positions():
+    from tests.test_oracle import QS_DIMS, holes_input
+    desc = model_examples.qsize(hidden=16, iterations=3)
+    out, ref, _, _ = _run(desc, QS_DIMS, [holes_input(), holes_input()], seed=7, bias=0.3)
+    _close(out, ref)
+
+
+def test_duplicate_positions_accumulate():
+    """scatter_nd adds messages that share (dst, seq) (GM:490): two links at position 0 of
+    path 0, a hole at position 1, one link at position 2 (final_len 3 = Lmax 3)."""
+    desc = model_examples.routenet(hidden=16, iterations=2)
+    dims = {"link_capacity": 1, "traffic": 1, "adj_links_paths": 0, "adj_paths_links": 0}
+    x = {"link_capacity": [0.5, -0.3, 0.8], "traffic": [0.2, -0.4],
+         "src_adj_links_paths": [0, 1, 2, 2], "dst_adj_links_paths": [0, 0, 0, 1], "seq_link_path": [0, 0, 2, 0],
+         "src_adj_paths_links": [0, 1, 0], "dst_adj_paths_links": [0, 1, 2], "seq_path_link": [0, 0, 0],
+         "num_link": 3, "num_path": 2}
+    out, ref, _, _ = _run(desc, dims, [x], seed=3, bias=0.2)
+    _close(out, ref)
+
+
+def test_multi_source_ordered_slots_after_global_lmax():
+    """Two sources with 'ordered': source 2's slots start after source 1's Lmax (GM:533),
+    leaving holes for destinations with fewer source-1 messages."""
+    desc = model_examples.qsize(hidden=16, iterations=2)
+    desc["message_passing"]["stages"][0]["stage_mp"][0]["aggregation"] = {"type": "ordered"}
+    from tests.test_oracle import QS_DIMS, holes_input
+    x = holes_input()
+    del x["indices_link_to_path"], x["indices_node_to_path"]
+    out, ref, _, _ = _run(desc, QS_DIMS, [x], seed=9, bias=0.3)
+    _close(out, ref)
+
+
+def test_final_len_beyond_padding_rejected():
+    """Duplicates that make final_len exceed max(seq)+1: TF's gather_nd fails (AUX:793-795)."""
+    desc = model_examples.routenet(hidden=16, iterations=2)
+    dims = {"link_capacity": 1, "traffic": 1, "adj_links_paths": 0, "adj_paths_links": 0}
+    x = {"link_capacity": [0.5, -0.3, 0.8], "traffic": [0.2, -0.4],
+         "src_adj_links_paths": [0, 1, 2, 2], "dst_adj_links_paths": [0, 0, 0, 1], "seq_link_path": [0, 0, 1, 0],
+         "src_adj_paths_links": [0, 1, 0], "dst_adj_paths_links": [0, 1, 2], "seq_path_link": [0, 0, 0],
+         "num_link": 3, "num_path": 2}
+    mi = Model_information(copy.deepcopy(desc), dims)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(0))
+    with pytest.raises(_lib.EngineError, match="gather_nd"):
+        Batch(eng, [x])
+
+
+def test_error_paths_match_reference():
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 1)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(0))
+    g = dict(graphs[0])
+    keep = np.asarray(g["dst_adj_links_paths"]) != 0
+    for k in ("src_adj_links_paths", "dst_adj_links_paths", "seq_link_path"):
+        g[k] = np.asarray(g[k])[keep]
+    with pytest.raises(_lib.EngineError) as ei:
+        Batch(eng, [g])
+    assert ei.value.code == -1 and "no message" in str(ei.value)
+    g = dict(graphs[0])
+    g["src_adj_paths_links"] = np.asarray(g["src_adj_paths_links"]).copy()
+    g["src_adj_paths_links"][3] = 10 ** 6
+    with pytest.raises(_lib.EngineError):
+        Batch(eng, [g])
+
+
+def test_ragged_interleave_rejected(gen_fixtures):
+    from tests.test_oracle import QS_DIMS
+    case = [c for c in gen_fixtures if c["name"] == "interleave_ragged"][0]
+    x = dict(case["expected"][0]["data"])
+    mi = Model_information(model_examples.qsize(hidden=16), QS_DIMS)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(0))
+    with pytest.raises(_lib.EngineError, match="different lengths"):
+        Batch(eng, [x])
+
+
+def test_batch_equals_per_graph():
+    """Disjoint-union batching == the reference's per-graph loop + concat (GM:712-724)."""
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("qsize", "nsfnet", 3)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(4, bias_scale=0.1))
+    whole = Batch(eng, graphs).forward().reshape(-1)
+    parts = np.concatenate([Batch(eng, [g]).forward().reshape(-1) for g in graphs])
+    np.testing.assert_array_equal(whole, parts)
+
+
+def test_large_batch_properties():
+    """512 x synth50-size batch: finite, deterministic, and graph g of the batch equals the same
+    graph run alone (size-independent property), plus a few graphs vs the oracle."""
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "synth50", 64)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(1, bias_scale=0.05)
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    b = Batch(eng, graphs)
+    o1 = b.forward().reshape(-1)
+    o2 = b.forward().reshape(-1)
+    np.testing.assert_array_equal(o1, o2)
+    assert np.all(np.isfinite(o1))
+    P = [int(g["num_path"]) for g in graphs]
+    off = np.cumsum([0] + P)
+    for gi in (0, 17, 63):
+        alone = Batch(eng, [graphs[gi]]).forward().reshape(-1)
+        np.testing.assert_array_equal(o1[off[gi]:off[gi + 1]], alone)
+    ref = DenseOracle(desc, dims, prm).forward([graphs[5]])
+    _close(o1[off[5]:off[6]], ref)

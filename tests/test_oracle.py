@@ -1,0 +1,162 @@
+"""Oracle self-checks (CPU): known answers and agreement of the two restatements.
+
+The numeric oracle (oracle/dense_forward.py) cannot be compared with TensorFlow (absent);
+these tests pin it by cases whose answer follows from the Keras definitions alone.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from ignnition_amd import model_examples, synthetic, workloads
+from oracle.dense_forward import DenseOracle, OracleError, gru_cell
+from oracle.packed_forward import PackedOracle
+
+
+def _params(desc, dims, seed=0, bias=0.0):
+    from ignnition_amd.engine import MPPlan
+    from ignnition_amd.json_operations import Model_information
+    return MPPlan.from_model_info(Model_information(desc, dims)).init_params(seed, bias_scale=bias)
+
+
+def test_gru_zero_weights_halves_state():
+    """z = r = sigmoid(0) = 1/2, candidate tanh(0) = 0 -> h' = h/2."""
+    h = np.random.default_rng(0).standard_normal((5, 4))
+    x = np.random.default_rng(1).standard_normal((5, 3))
+    out = gru_cell(x, h, np.zeros((3, 12)), np.zeros((4, 12)), np.zeros((2, 12)))
+    np.testing.assert_allclose(out, h / 2, rtol=0, atol=0)
+
+
+def test_gru_matches_definition():
+    rng = np.random.default_rng(2)
+    x, h = rng.standard_normal((3, 4)), rng.standard_normal((3, 2))
+    W, U, b = rng.standard_normal((4, 6)), rng.standard_normal((2, 6)), rng.standard_normal((2, 6))
+    sig = lambda v: 1 / (1 + np.exp(-v))
+    z = sig(x @ W[:, 0:2] + b[0, 0:2] + h @ U[:, 0:2] + b[1, 0:2])
+    r = sig(x @ W[:, 2:4] + b[0, 2:4] + h @ U[:, 2:4] + b[1, 2:4])
+    c = np.tanh(x @ W[:, 4:6] + b[0, 4:6] + r * (h @ U[:, 4:6] + b[1, 4:6]))
+    np.testing.assert_allclose(gru_cell(x, h, W, U, b), z * h + (1 - z) * c, rtol=1e-12)
+
+
+def test_zero_gru_routenet_known_answer():
+    """With all GRU weights zero every update halves the state: after T iterations a path of
+    L links is scaled by 2^-(T*L), every link by 2^-T.  The readout then sees known states."""
+    desc, dims, mi = workloads.model("routenet")
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", 1)])
+    g = graphs[0]
+    prm = _params(desc, dims)
+    for k in prm:
+        if "_update/" in k:
+            prm[k] = np.zeros_like(prm[k])
+    ora = DenseOracle(desc, dims, prm)
+    state = {}
+    orig = ora._readout
+    ora._readout = lambda st, x: state.update(st) or orig(st, x)
+    ora.forward_graph(g)
+    T = 8
+    L = np.bincount(np.asarray(g["dst_adj_links_paths"]), minlength=g["num_path"])
+    expect_path = np.asarray(g["traffic"], np.float64)[:, None] * (0.5 ** (T * L))[:, None]
+    np.testing.assert_allclose(state["path"][:, :1], expect_path, rtol=1e-12)
+    np.testing.assert_allclose(state["path"][:, 1:], 0)
+    np.testing.assert_allclose(state["link"][:, 0], np.asarray(g["link_capacity"]) * 0.5 ** T, rtol=1e-12)
+
+
+def test_sum_aggregation_integer_exact():
+    """A GRU that passes tanh(x) through (z -> 0): link state = tanh(sum of integer path states)."""
+    desc = model_examples.routenet(hidden=16, iterations=1)
+    desc["message_passing"]["stages"] = desc["message_passing"]["stages"][1:]   # path -> link only
+    sample = synthetic.routenet_sample("nsfnet", 2)
+    dims = {"link_capacity": 1, "traffic": 1, "adj_links_paths": 0, "adj_paths_links": 0}
+    from ignnition_amd.json_operations import Model_information
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [sample], normalize=False)
+    g = graphs[0]
+    g["traffic"] = np.arange(len(g["traffic"]), dtype=np.float64) % 7
+    H = 16
+    prm = _params(desc, dims)
+    W = np.zeros((H, 3 * H))
+    W[:, :H] = 0.0
+    prm["link_update/kernel"] = W.copy()
+    prm["link_update/kernel"][:, 2 * H:] = np.eye(H)             # candidate = tanh(x)
+    prm["link_update/recurrent_kernel"] = np.zeros((H, 3 * H))
+    b = np.zeros((2, 3 * H))
+    b[0, :H] = -60.0                                              # z = sigmoid(-60) ~ 0
+    prm["link_update/bias"] = b
+    ora = DenseOracle(desc, dims, prm)
+    state = {}
+    orig = ora._readout
+    ora._readout = lambda st, x: state.update(st) or orig(st, x)
+    ora.forward_graph(g)
+    agg = np.zeros(g["num_link"])
+    np.add.at(agg, np.asarray(g["dst_adj_paths_links"]), np.asarray(g["traffic"])[np.asarray(g["src_adj_paths_links"])])
+    np.testing.assert_allclose(state["link"][:, 0], np.tanh(agg), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_dense_and_packed_restatements_agree(kind):
+    desc, dims, mi = workloads.model(kind)
+    desc["message_passing"]["num_iterations"] = 2
+    from ignnition_amd.json_operations import Model_information
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", 4, qsize=(kind == "qsize"))])
+    prm = _params(desc, dims, seed=3, bias=0.1)
+    a = DenseOracle(desc, dims, prm).forward(graphs)
+    b = PackedOracle(desc, dims, prm).forward(graphs)
+    np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+
+
+QS_DIMS = {"link_capacity": 1, "traffic": 1, "queue_sizes": 1, "adj_links_paths": 0, "adj_paths_links": 0,
+           "adj_nodes_paths": 0, "adj_paths_nodes": 0}
+
+
+def holes_input():
+    """Interleave with a hole and a dropped position, GEN-consistent indices:
+    p0 has links [l0, l1] and node [n0]; p1 has link [l1] and nodes [n1, n2].  Pattern
+    [node, link] over n_total = 2 + 2 slots -> indices_node = [0, 2], indices_link = [1, 3].
+    p0: final_len 3, link slot 1 lands on position 3 (dropped), position 2 is a hole."""
+    return {
+        "link_capacity": [0.5, -0.25], "traffic": [0.1, 0.7], "queue_sizes": [0.3, -0.6, 0.9],
+        "src_adj_links_paths": [0, 1, 1], "dst_adj_links_paths": [0, 0, 1], "seq_link_path": [0, 1, 0],
+        "src_adj_nodes_paths": [0, 1, 2], "dst_adj_nodes_paths": [0, 1, 1], "seq_node_path": [0, 0, 1],
+        "src_adj_paths_links": [0, 0, 1], "dst_adj_paths_links": [0, 1, 1], "seq_path_link": [0, 0, 1],
+        "src_adj_paths_nodes": [0, 1, 1], "dst_adj_paths_nodes": [0, 1, 2], "seq_path_node": [0, 0, 0],
+        "num_link": 2, "num_path": 2, "num_node": 3,
+        "indices_link_to_path": [1, 3], "indices_node_to_path": [0, 2],
+    }
+
+
+def test_restatements_agree_on_interleave_holes():
+    desc = model_examples.qsize(hidden=16, iterations=2)
+    prm = _params(desc, QS_DIMS, seed=5, bias=0.2)
+    a = DenseOracle(desc, QS_DIMS, prm).forward([holes_input()])
+    b = PackedOracle(desc, QS_DIMS, prm).forward([holes_input()])
+    np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+
+
+def test_ragged_interleave_from_reference_generator_raises(gen_fixtures):
+    """GEN gives index lists of different lengths here; tf.stack (GM:518) then fails."""
+    case = [c for c in gen_fixtures if c["name"] == "interleave_ragged"][0]
+    x = dict(case["expected"][0]["data"])
+    desc = model_examples.qsize(hidden=16, iterations=2)
+    prm = _params(desc, QS_DIMS, seed=5, bias=0.2)
+    with pytest.raises(OracleError):
+        DenseOracle(desc, QS_DIMS, prm).forward([x])
+
+
+def test_oracle_raises_like_tf():
+    desc, dims, mi = workloads.model("routenet")
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", 1)])
+    g = dict(graphs[0])
+    prm = _params(desc, dims)
+    bad = dict(g)
+    bad["src_adj_links_paths"] = list(g["src_adj_links_paths"])
+    bad["src_adj_links_paths"][0] = 10 ** 6
+    with pytest.raises(OracleError):
+        DenseOracle(desc, dims, prm).forward_graph(bad)
+    # a path that receives no link -> gather_nd(-1) in the sorted update (AUX:793-795)
+    bad = dict(g)
+    keep = np.asarray(g["dst_adj_links_paths"]) != 0
+    for k in ("src_adj_links_paths", "dst_adj_links_paths", "seq_link_path"):
+        bad[k] = np.asarray(g[k])[keep]
+    with pytest.raises(OracleError):
+        DenseOracle(desc, dims, prm).forward_graph(bad)
