@@ -62,7 +62,7 @@ class Stats(C.Structure):
                 ("bytes", C.c_double * 8)]
 
 
-KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "other"]
+KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "project", "other"]
 
 AGGR = {"sum": 0, "ordered": 1, "interleave": 2, "concat": 3, "attention": 4, "convolution": 5}
 ACT = {None: 0, "None": 0, "linear": 0, "relu": 1, "selu": 2, "sigmoid": 3, "tanh": 4}

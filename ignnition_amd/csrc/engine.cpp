@@ -50,7 +50,7 @@ int fail(int code, const char* fmt, ...) {
     if (_e != hipSuccess) return fail(IGN_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e));    \
   } while (0)
 
-enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_OTHER = 4, K_KINDS = 5 };
+enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_PROJECT = 4, K_OTHER = 5, K_KINDS = 6 };
 
 struct Tensor {
   int kind, owner;
@@ -115,6 +115,13 @@ struct MPB {
   int32_t* d_step_ptr = nullptr;
   int32_t* d_msg_ptr = nullptr;
   uint32_t* d_msg_src = nullptr;
+  uint32_t* d_step_code = nullptr;
+  float* d_table = nullptr;       // sorted MPs: [sources' rows | zero row | multi rows][3H]
+  std::vector<int64_t> src_off;   // first table row of each source
+  std::vector<int64_t> src_rows;
+  int64_t zero_row = 0, n_multi = 0;
+  int32_t* d_multi_ptr = nullptr;
+  uint32_t* d_multi_rows = nullptr;
   double flops = 0, bytes = 0;    // algorithmic, per launch
 };
 
@@ -179,8 +186,8 @@ int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
 
 int dev_alloc(ign_batch* b, float** out, int64_t n) {
   void* p = nullptr;
-  // +64 floats of slack: kernels may read a whole (masked-off) row at index 0 of an empty table
-  hipError_t e = hipMalloc(&p, (std::max<int64_t>(n, 0) + 64) * sizeof(float));
+  // +256 floats of slack: kernels may read a whole (masked-off) row at index 0 of an empty table
+  hipError_t e = hipMalloc(&p, (std::max<int64_t>(n, 0) + 256) * sizeof(float));
   if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%lld floats): %s", (long long)n, hipGetErrorString(e));
   b->allocs.push_back(p);
   *out = static_cast<float*>(p);
@@ -586,38 +593,67 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         std::vector<int64_t> fill(dcnt.begin(), dcnt.end() - 1);
         for (size_t k = 0; k < mdst.size(); ++k) byd[fill[mdst[k]]++] = (int64_t)k;
       }
-      std::vector<int32_t> len(ND), step_ptr(ND), msg_ptr;
-      std::vector<uint32_t> msrc;
-      msg_ptr.reserve(mdst.size() + 1);
-      msrc.reserve(mdst.size());
-      int64_t steps = 0;
+      // combined projected table: source s occupies rows [src_off[s], src_off[s] + rows_s)
+      int64_t trow = 0;
+      for (int s = 0; s < S; ++s) {
+        mb.src_off.push_back(trow);
+        mb.src_rows.push_back(b->rows[mp.src[s].entity]);
+        trow += b->rows[mp.src[s].entity];
+      }
+      mb.zero_row = trow;
+      auto table_row = [&](uint32_t code) -> int64_t {
+        return mb.src_off[code >> IGN_SLOT_SHIFT] + (code & IGN_ROW_MASK);
+      };
+      std::vector<int32_t> len(ND), step_ptr(ND), multi_ptr(1, 0);
+      std::vector<uint32_t> scode, multi_rows;
+      scode.reserve(mdst.size() + 64);
+      int64_t steps = 0, maxL = 0, n_msgs = 0;
       std::vector<int64_t> tmp;
       for (int64_t i = 0; i < ND; ++i) {
         const int64_t r = order[i];
         const int64_t L = flen[r];
+        maxL = std::max(maxL, L);
         len[i] = (int32_t)L;
         step_ptr[i] = (int32_t)steps;
         tmp.assign(byd.begin() + dcnt[r], byd.begin() + dcnt[r + 1]);
         std::stable_sort(tmp.begin(), tmp.end(), [&](int64_t x, int64_t y) { return mpos[x] < mpos[y]; });
         size_t q = 0;
         for (int64_t t = 0; t < L; ++t) {
-          msg_ptr.push_back((int32_t)msrc.size());
           while (q < tmp.size() && mpos[tmp[q]] < t) ++q;
-          while (q < tmp.size() && mpos[tmp[q]] == t) msrc.push_back(mcode[tmp[q++]]);
+          size_t q0 = q;
+          while (q < tmp.size() && mpos[tmp[q]] == t) ++q;
+          const size_t cnt = q - q0;
+          n_msgs += (int64_t)cnt;
+          if (cnt == 1) {
+            scode.push_back((uint32_t)table_row(mcode[tmp[q0]]));
+          } else if (cnt == 0) {
+            scode.push_back((uint32_t)mb.zero_row);        // hole: zero input
+          } else {                                            // several messages: pre-summed row
+            scode.push_back((uint32_t)(mb.zero_row + 1 + mb.n_multi));
+            for (size_t k = q0; k < q; ++k) multi_rows.push_back((uint32_t)table_row(mcode[tmp[k]]));
+            multi_ptr.push_back((int32_t)multi_rows.size());
+            mb.n_multi++;
+          }
         }
         steps += L;
       }
-      msg_ptr.push_back((int32_t)msrc.size());
-      if (steps >= INT32_MAX || (int64_t)msrc.size() >= INT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
+      for (int64_t k = 0; k < maxL + 8; ++k) scode.push_back((uint32_t)mb.zero_row);  // unconditional reads
+      if (steps >= INT32_MAX || mb.zero_row + 1 + mb.n_multi >= (int64_t)UINT32_MAX)
+        return fail(IGN_ERR_UNSUPPORTED, "MP too large");
       mb.n_steps = steps;
-      mb.n_msgs = (int64_t)msrc.size();
+      mb.n_msgs = n_msgs;
       if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_len, len))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_step_ptr, step_ptr))) return rc;
-      if ((rc = dev_upload(b.get(), &mb.d_msg_ptr, msg_ptr))) return rc;
-      if ((rc = dev_upload(b.get(), &mb.d_msg_src, msrc))) return rc;
-      mb.flops = (double)steps * gru_flops(DIN, H) + (double)mb.n_msgs * DIN;
-      mb.bytes = (double)mb.n_msgs * (4.0 * DIN + 4) + (double)steps * 4 + (double)ND * (8.0 * H + 12);
+      if ((rc = dev_upload(b.get(), &mb.d_step_code, scode))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_multi_ptr, multi_ptr))) return rc;
+      if ((rc = dev_upload(b.get(), &mb.d_multi_rows, multi_rows))) return rc;
+      const int64_t tfloats = (mb.zero_row + 1 + mb.n_multi) * 3LL * H;
+      if ((rc = dev_alloc(b.get(), &mb.d_table, tfloats))) return rc;
+      HIP_TRY(hipMemset(mb.d_table, 0, (tfloats + 256) * sizeof(float)));   // zero row stays zero
+      // per launch of the recurrence: h.U + gates per step; one projected row (3H floats) per step
+      mb.flops = (double)steps * (2.0 * H * 3 * H + 14.0 * H);
+      mb.bytes = (double)steps * (12.0 * H + 4) + (double)ND * (8.0 * H + 12);
       b->gru_steps += steps * p->T;
     } else {
       std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
@@ -753,10 +789,23 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
       const float* hin = b->d_state[b->cur[dst]][dst];
       float* hout = b->d_state[1 - b->cur[dst]][dst];
       if (mp.sorted) {
-        SeqGruArgs a{hin, hout, sbases, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_msg_ptr, mb.d_msg_src,
-                     p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst};
+        const int W3 = 3 * cp.H;
+        for (size_t s = 0; s < mp.src.size(); ++s) {
+          const int64_t rs = mb.src_rows[s];
+          tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3));
+          HIP_TRY(launch_project(sbases.base[s], rs, p->d_packed + cp.pk_w, mb.d_table + mb.src_off[s] * W3,
+                                 mp.din, cp.H, st));
+          tm.end();
+        }
+        if (mb.n_multi) {
+          tm.begin(K_OTHER, 0, 0);
+          HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3, st));
+          tm.end();
+        }
+        SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
+                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst};
         tm.begin(K_SEQ, mb.flops, mb.bytes);
-        HIP_TRY(launch_seq_gru(a, mp.din, cp.H, st));
+        HIP_TRY(launch_seq_gru(a, cp.H, st));
         tm.end();
       } else {
         SumGruArgs a{hin, hout, sbases, mb.d_order, mb.d_msg_ptr, mb.d_msg_src,

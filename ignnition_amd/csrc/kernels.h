@@ -15,17 +15,15 @@ struct SrcBases {
 };
 
 struct SeqGruArgs {
-  const float* h_in;       // [rows][H] destination state before the update
-  float* h_out;            // [rows][H] destination state after the update
-  SrcBases src;
-  const int32_t* order;    // [n_dst] destination rows, sorted by final_len (descending)
-  const int32_t* len;      // [n_dst] final_len per order position
-  const int32_t* step_ptr; // [n_dst] first step of each order position
-  const int32_t* msg_ptr;  // [n_steps + 1] message range of every step
-  const uint32_t* msg_src; // [n_msgs] message source codes
-  const float* Wp;         // packed input-kernel fragments
-  const float* Up;         // packed recurrent-kernel fragments
-  const float* bias;       // [4][H] combined biases
+  const float* h_in;         // [rows][H] destination state before the update
+  float* h_out;              // [rows][H] destination state after the update
+  const float* table;        // projected message table [sources' rows | zero row | multi rows][3H]
+  const int32_t* order;      // [n_dst] destination rows, sorted by final_len (descending)
+  const int32_t* len;        // [n_dst] final_len per order position
+  const int32_t* step_ptr;   // [n_dst] first step of each order position
+  const uint32_t* step_code; // [n_steps + pad] table row of every step (padded with the zero row)
+  const float* Up;           // packed recurrent-kernel fragments
+  const float* bias;         // [4][H] combined biases
   int64_t n_dst;
 };
 
@@ -58,7 +56,10 @@ hipError_t launch_pack_gru(const float* W, const float* U, const float* bias, fl
                            int DIN, int H, hipStream_t st);
 hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStream_t st);
 bool gru_shape_supported(int din, int h);
-hipError_t launch_seq_gru(const SeqGruArgs& args, int din, int h, hipStream_t st);
+hipError_t launch_project(const float* x, int64_t n, const float* Wp, float* out, int din, int h, hipStream_t st);
+hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
+                            const uint32_t* rows, int W, hipStream_t st);
+hipError_t launch_seq_gru(const SeqGruArgs& args, int h, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);

@@ -25,12 +25,16 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Gate nonlinearities on v_exp_f32 + v_rcp_f32 (1 ulp each; an IEEE divide would expand to
+// ~10 VALU instructions and dominate the recurrence's VALU stream).  Both saturate cleanly:
+// exp overflow gives rcp(inf) = 0.
+__device__ __forceinline__ float rcpf_(float x) { return __builtin_amdgcn_rcpf(x); }
+
+__device__ __forceinline__ float sigmoidf_(float x) { return rcpf_(1.0f + __expf(-x)); }
 
 __device__ __forceinline__ float tanhf_(float x) {
-  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for |x| large.
-  float e = __expf(2.0f * x);
-  return 1.0f - 2.0f / (e + 1.0f);
+  // tanh(x) = 1 - 2/(exp(2x)+1)
+  return 1.0f - 2.0f * rcpf_(__expf(2.0f * x) + 1.0f);
 }
 
 __device__ __forceinline__ float act_apply(float x, int act) {
@@ -206,14 +210,74 @@ __device__ __forceinline__ const float* src_ptr(const SrcBases& sb, uint32_t cod
 }
 
 // ---------------------------------------------------------------------------------------------
+// Input projection of a message table: XW[row] = state[row] . W  (W = the destination cell's input
+// kernel [DIN][3H], no bias).  x.W depends only on the source row, so the ordered update below
+// gathers projected rows instead of recomputing x.W for every (destination, step): the
+// recurrence keeps only h.U on the MFMA pipe.  Exact reassociation of the Keras cell
+// (x.W + b_in) + (h.U + b_rec); holes project to 0 and duplicates sum linearly.
+// Output row layout [3H]: gate-major z | r | h, same as the Keras kernel columns.
+template <int DIN, int H>
+__global__ __launch_bounds__(256) void project_kernel(const float* __restrict__ x, int64_t n,
+                                                      const float* __restrict__ Wp, float* __restrict__ out) {
+  // out points at this source's first row inside the MP's combined projected table
+  constexpr int NC = DIN / 16, NT = H / 16, KX = DIN / 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t r = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = r < n;
+  f4 xv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) xv[c] = valid ? ld4(x + r * DIN + 16 * c + 4 * g) : f4{0, 0, 0, 0};
+  f4 acc[3][NT];
+#pragma unroll
+  for (int G = 0; G < 3; ++G)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[G][t] = f4{0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < KX; ++s) {
+    const float xb = xv[s >> 2][s & 3];
+#pragma unroll
+    for (int G = 0; G < 3; ++G)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[G][t] = MFMA(Wp[(((G * NT + t) * KX + s) << 6) + lane], xb, acc[G][t]);
+  }
+  if (valid) {
+#pragma unroll
+    for (int G = 0; G < 3; ++G)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(out + r * 3 * H + G * H + 16 * t + 4 * g, acc[G][t]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Positions that receive several messages (scatter_nd adds them, GM:490): row multi_base + k of
+// the projected table = sum of the projected rows listed for k.  Rare; one thread per float4.
+__global__ void multi_sum_kernel(float* __restrict__ table, int64_t multi_base, int64_t n_multi,
+                                 const int32_t* __restrict__ ptr, const uint32_t* __restrict__ rows, int W) {
+  const int64_t q = W / 4;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n_multi * q; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / q;
+    const int c = (int)(i - k * q) * 4;
+    f4 acc = f4{0, 0, 0, 0};
+    for (int m = ptr[k]; m < ptr[k + 1]; ++m) acc += ld4(table + (int64_t)rows[m] * W + c);
+    st4(table + (multi_base + k) * W + c, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Ordered / interleave / concat(axis 1) update: masked GRU over each destination's message
 // sequence (AUX:767-796 with the dense-padding semantics of GM:477-543).  One wave = 16
 // destinations of similar length (rows sorted by length, descending).  Step t of destination
-// d sums the messages whose position is t (scatter_nd accumulates duplicates; holes are zero
-// inputs); steps t >= final_len[d] leave the state unchanged (sequence_mask).
-template <int DIN, int H>
+// d reads row step_code[step_ptr[d] + t] of the MP's projected table: the projection of its
+// message, the zero row for a hole (a padded position below final_len), or a pre-summed row
+// where several messages share the position.  Steps t >= final_len[d] leave the state
+// unchanged (sequence_mask); their (padded, always valid) codes are still read so the loop
+// has no data-dependent branch or select.
+template <int H>
 __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
-  constexpr int NC = DIN / 16, NT = H / 16;
+  constexpr int NT = H / 16, KH = H / 4;
   __shared__ float sbias[4 * H];
   for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
 
@@ -223,57 +287,77 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
   const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
   const bool valid = pos < a.n_dst;
 
-  GruWeights<DIN, H> W;
-  load_gru_weights<DIN, H>(W, a.Wp, a.Up, lane);
+  float u[3][NT][KH];   // recurrent kernel fragments, resident for the whole sequence
+#pragma unroll
+  for (int G = 0; G < 3; ++G)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < KH; ++s) u[G][t][s] = a.Up[(((G * NT + t) * KH + s) << 6) + lane];
 
   const int row = valid ? a.order[pos] : 0;
   const int L = valid ? a.len[pos] : 0;
-  const int64_t sbase = valid ? a.step_ptr[pos] : 0;
+  const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+  const float* tab = a.table + 16 * 0 + 4 * g;
 
   f4 h[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
 
-  // tile length = max over the wave (rows are sorted, but take the max to be safe)
   int Lmax = L;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
   __syncthreads();
 
-  // gather of step t for this lane: sum of the rows whose position is t
-  auto gather = [&](int t, f4 (&x)[NC]) {
-    const bool act = t < L;
-    const int64_t s = act ? sbase + t : 0;
-    int m0 = a.msg_ptr[s], m1 = a.msg_ptr[s + 1];
-    if (!act) m1 = m0;
-    const int mi = (m1 > m0) ? m0 : 0;
-    const float* p = src_ptr(a.src, a.msg_src[mi], DIN);
-    const bool any = m1 > m0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      f4 v = ld4(p + 16 * c + 4 * g);
-      x[c] = any ? v : f4{0, 0, 0, 0};
-    }
-    for (int m = m0 + 1; m < m1; ++m) {  // rare: several messages at one position
-      const float* q = src_ptr(a.src, a.msg_src[m], DIN);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] += ld4(q + 16 * c + 4 * g);
-    }
-  };
-
-  f4 x[NC], xn[NC];
-  gather(0, x);
+  // Per step: issue the projected row of this step and the code of the next one, run the
+  // h.U MFMAs (independent of x: the accumulators start from the biases), then consume x in the
+  // gate math.  The sched_barriers keep the compiler from sinking the loads below the MFMAs or
+  // hoisting their consumers above them, so the gather latency hides under the MFMA block.
+  uint32_t code = codes[0];
   for (int t = 0; t < Lmax; ++t) {
-    if (t + 1 < Lmax) gather(t + 1, xn);
-    f4 hn[NT];
+    f4 x[3][NT];
+    {
+      const float* p = tab + (int64_t)code * (3 * H);
 #pragma unroll
-    for (int i = 0; i < NT; ++i) hn[i] = h[i];
-    gru_step<DIN, H>(W, sbias, x, hn, g);
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+    }
+    const uint32_t next = codes[t + 1];
+    __builtin_amdgcn_sched_barrier(0);
+    f4 az[NT], ar[NT], ah[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const int u0 = 16 * i + 4 * g;
+      az[i] = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+      ar[i] = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+    }
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      const float hb = h[s >> 2][s & 3];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        az[i] = MFMA(u[0][i][s], hb, az[i]);
+        ar[i] = MFMA(u[1][i][s], hb, ar[i]);
+        ah[i] = MFMA(u[2][i][s], hb, ah[i]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
     const bool act = t < L;
 #pragma unroll
-    for (int i = 0; i < NT; ++i) h[i] = act ? hn[i] : h[i];
+    for (int i = 0; i < NT; ++i) {
+      const f4 bx = *reinterpret_cast<const f4*>(sbias + 2 * H + 16 * i + 4 * g);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) x[c] = xn[c];
+      for (int r = 0; r < 4; ++r) {
+        const float z = sigmoidf_(az[i][r] + x[0][i][r]);
+        const float rr = sigmoidf_(ar[i][r] + x[1][i][r]);
+        const float c = tanhf_(x[2][i][r] + bx[r] + rr * ah[i][r]);
+        const float hn = z * h[i][r] + (1.0f - z) * c;
+        h[i][r] = act ? hn : h[i][r];
+      }
+    }
+    code = next;
   }
   if (valid) {
 #pragma unroll
@@ -486,13 +570,33 @@ bool gru_shape_supported(int din, int h) {
   return (din == 16 || din == 32) && (h == 16 || h == 32);
 }
 
-hipError_t launch_seq_gru(const SeqGruArgs& args, int din, int h, hipStream_t st) {
+hipError_t launch_project(const float* x, int64_t n, const float* Wp, float* out, int din, int h, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 grid(grid_for(n, 64)), block(256);
+  if (din == 32 && h == 32) hipLaunchKernelGGL((project_kernel<32, 32>), grid, block, 0, st, x, n, Wp, out);
+  else if (din == 16 && h == 16) hipLaunchKernelGGL((project_kernel<16, 16>), grid, block, 0, st, x, n, Wp, out);
+  else if (din == 16 && h == 32) hipLaunchKernelGGL((project_kernel<16, 32>), grid, block, 0, st, x, n, Wp, out);
+  else if (din == 32 && h == 16) hipLaunchKernelGGL((project_kernel<32, 16>), grid, block, 0, st, x, n, Wp, out);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
+                            const uint32_t* rows, int W, hipStream_t st) {
+  if (n_multi == 0) return hipSuccess;
+  int64_t total = n_multi * (W / 4);
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(multi_sum_kernel, dim3(blocks), dim3(256), 0, st, table, multi_base, n_multi, ptr, rows, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_seq_gru(const SeqGruArgs& args, int h, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  GRU_DISPATCH(seq_gru_kernel, 32, 32, args, args.n_dst)
-  GRU_DISPATCH(seq_gru_kernel, 16, 16, args, args.n_dst)
-  GRU_DISPATCH(seq_gru_kernel, 16, 32, args, args.n_dst)
-  GRU_DISPATCH(seq_gru_kernel, 32, 16, args, args.n_dst)
-  return hipErrorInvalidValue;
+  dim3 grid(grid_for(args.n_dst, 64)), block(256);
+  if (h == 32) hipLaunchKernelGGL((seq_gru_kernel<32>), grid, block, 0, st, args);
+  else if (h == 16) hipLaunchKernelGGL((seq_gru_kernel<16>), grid, block, 0, st, args);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st) {

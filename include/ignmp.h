@@ -141,7 +141,7 @@ typedef struct {
 } ign_batch_info_t;
 
 /* Per-kernel timing of the last forward (HIP events on the plan stream, enabled by
- * ign_plan_set_timing).  kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 other */
+ * ign_plan_set_timing).  kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 project, 5 other */
 typedef struct {
   int32_t kinds;
   int64_t launches[8];
