@@ -312,8 +312,9 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     in = dp.out;
   }
   if (p->dense.empty()) return fail(IGN_ERR_INVALID, "readout has no Dense layer");
-  p->fused_readout = p->dense.size() == 3 && readout3_supported(width, p->dense[0].out, p->dense[1].out) &&
-                     p->dense[2].out == 1;
+  p->fused_readout = p->dense.size() == 3 &&
+                     readout3_supported(width, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act) &&
+                     p->dense[2].out == 1 && p->dense[0].use_bias && p->dense[1].use_bias;
 
   // parameter layout (256-B aligned tensors)
   auto align = [](int64_t x) { return (x + 63) & ~int64_t(63); };

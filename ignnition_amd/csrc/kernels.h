@@ -61,7 +61,7 @@ hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, c
                             const uint32_t* rows, int W, hipStream_t st);
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st);
-bool readout3_supported(int din, int n1, int n2);
+bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
                                 int out, int act, float* y, hipStream_t st);

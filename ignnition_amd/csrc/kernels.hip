@@ -50,6 +50,18 @@ __device__ __forceinline__ float act_apply(float x, int act) {
   }
 }
 
+template <int ACT>
+__device__ __forceinline__ float act_t(float x) {
+  if constexpr (ACT == IGN_K_ACT_RELU) return x > 0.f ? x : 0.f;
+  else if constexpr (ACT == IGN_K_ACT_SELU) {   // branch-free: exp of min(x, 0), then select
+    const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
+    const float e = __expf(fminf(x, 0.f));
+    return x > 0.f ? lam * x : la * (e - 1.0f);
+  } else if constexpr (ACT == IGN_K_ACT_SIGMOID) return sigmoidf_(x);
+  else if constexpr (ACT == IGN_K_ACT_TANH) return tanhf_(x);
+  else return x;
+}
+
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
@@ -431,9 +443,10 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
 // accumulator layout (N1/16 tiles x 2) and feed layer 2 as B operands; layer 2 is produced
 // 16 units at a time and immediately contracted with the 1-unit output layer, so the second
 // hidden layer is never materialised.  W1/W2 fragments stream from L2 as float4 per lane.
-template <int DIN, int N1, int N2>
+template <int DIN, int N1, int N2, int ACT>
 __global__ __launch_bounds__(256) void readout3_kernel(Readout3Args a) {
   constexpr int C0 = DIN / 16, U1 = N1 / 16, U2 = N2 / 16;
+  __shared__ f4 sw2[2][U1 * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -466,34 +479,58 @@ __global__ __launch_bounds__(256) void readout3_kernel(Readout3Args a) {
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      acc0[r] = act_apply(acc0[r], a.act1);
-      acc1[r] = act_apply(acc1[r], a.act1);
+      acc0[r] = act_t<ACT>(acc0[r]);
+      acc1[r] = act_t<ACT>(acc1[r]);
     }
     h1[u][0] = acc0;
     h1[u][1] = acc1;
   }
 
+  // Layer 2, 16 output units (one 16 KB chunk of packed W2 fragments) at a time.  The chunk is
+  // staged in LDS once per workgroup (4 waves share it) and double-buffered: the next chunk is
+  // loaded into registers while this one feeds the MFMAs, then stored behind one barrier.
+  constexpr int CH = U1 * 64;   // float4 per chunk
+  static_assert(CH % 256 == 0, "chunk must split evenly over the block");
+  constexpr int PER = CH / 256;
+  const f4* W2v = reinterpret_cast<const f4*>(a.W2p);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) sw2[0][tid + 256 * k] = W2v[tid + 256 * k];
+  __syncthreads();
+
   float y0 = 0.f, y1 = 0.f;
 #pragma unroll 1
   for (int v = 0; v < U2; ++v) {
-    f4 b = ld4(a.b2 + 16 * v + 4 * g);
+    const int cur = v & 1;
+    // small per-chunk vectors first: vmcnt retires loads in issue order, so loading them after
+    // the stage loads would make their first use wait for the whole next chunk
+    const f4 b = ld4(a.b2 + 16 * v + 4 * g);
+    const f4 w3 = ld4(a.w3 + 16 * v + 4 * g);
+    // unconditional (wraps to chunk 0 on the last pass): a branch here would make the compiler
+    // wait for these loads at the join before the first use of b
+    const int nv = (v + 1) % U2;
+    f4 stage[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) stage[k] = W2v[(int64_t)nv * CH + tid + 256 * k];
+    __builtin_amdgcn_sched_barrier(0);   // keep the stage loads ahead of this chunk's MFMAs
     f4 acc0 = b, acc1 = b;
-    const float* wv = a.W2p + (((int64_t)v * U1) << 8) + lane * 4;
 #pragma unroll
     for (int c = 0; c < U1; ++c) {
-      f4 w = ld4(wv + (c << 8));
+      const f4 w = sw2[cur][c * 64 + lane];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         acc0 = MFMA(w[q], h1[c][0][q], acc0);
         acc1 = MFMA(w[q], h1[c][1][q], acc1);
       }
     }
-    f4 w3 = ld4(a.w3 + 16 * v + 4 * g);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      y0 += w3[r] * act_apply(acc0[r], a.act2);
-      y1 += w3[r] * act_apply(acc1[r], a.act2);
+      y0 += w3[r] * act_t<ACT>(acc0[r]);
+      y1 += w3[r] * act_t<ACT>(acc1[r]);
     }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) sw2[cur ^ 1][tid + 256 * k] = stage[k];
+    __syncthreads();
   }
   // reduce the four unit groups (lanes j, j+16, j+32, j+48)
   y0 += __shfl_xor(y0, 16);
@@ -608,19 +645,29 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st
   return hipErrorInvalidValue;
 }
 
-bool readout3_supported(int din, int n1, int n2) {
-  return (din == 16 || din == 32 || din == 64) && n1 == 256 && n2 == 256;
+bool readout3_supported(int din, int n1, int n2, int act1, int act2) {
+  return (din == 16 || din == 32 || din == 64) && n1 == 256 && n2 == 256 && act1 == act2;
+}
+
+template <int DIN>
+static hipError_t readout3_din(const Readout3Args& args, int act, dim3 grid, hipStream_t st) {
+  switch (act) {
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_SELU>), grid, dim3(256), 0, st, args); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_RELU>), grid, dim3(256), 0, st, args); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_TANH>), grid, dim3(256), 0, st, args); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_SIGMOID>), grid, dim3(256), 0, st, args); break;
+    default: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_LINEAR>), grid, dim3(256), 0, st, args); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st) {
   if (args.n_rows == 0) return hipSuccess;
-  int blocks = grid_for(args.n_rows, 128);
-  if (n1 == 256 && n2 == 256) {
-    if (din == 32) { hipLaunchKernelGGL((readout3_kernel<32, 256, 256>), dim3(blocks), dim3(256), 0, st, args); return hipGetLastError(); }
-    if (din == 16) { hipLaunchKernelGGL((readout3_kernel<16, 256, 256>), dim3(blocks), dim3(256), 0, st, args); return hipGetLastError(); }
-    if (din == 64) { hipLaunchKernelGGL((readout3_kernel<64, 256, 256>), dim3(blocks), dim3(256), 0, st, args); return hipGetLastError(); }
-  }
-  return hipErrorInvalidValue;
+  if (!readout3_supported(din, n1, n2, args.act1, args.act2)) return hipErrorInvalidValue;
+  dim3 grid(grid_for(args.n_rows, 128));
+  if (din == 32) return readout3_din<32>(args, args.act1, grid, st);
+  if (din == 16) return readout3_din<16>(args, args.act1, grid, st);
+  return readout3_din<64>(args, args.act1, grid, st);
 }
 
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
