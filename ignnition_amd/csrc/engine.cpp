@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -97,6 +98,11 @@ struct ign_plan {
   bool params_set = false;
   bool fused_readout = false;
   int ro_width = 0;
+  int seq_variant = 2;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves)
+  // Measured on 512 x synth50 (profiles/r01): one global length sort without XCD remap is the
+  // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
+  bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
+  int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev;     // pairs
@@ -196,6 +202,20 @@ int dev_alloc(ign_batch* b, float** out, int64_t n) {
 
 int act_ok(int a) { return a >= IGN_ACT_LINEAR && a <= IGN_ACT_TANH; }
 
+// Destination processing order.  Default: one global sort by message count, descending (tiles of
+// equal length; the longest sequences start first).  graph_major: per graph by count, so tiles
+// stay inside one graph (with the XCD-aware block mapping one graph's tiles share an L2).
+void sort_order(std::vector<int32_t>& order, const std::vector<int64_t>& cnt, const std::vector<int64_t>& goff,
+                bool graph_major) {
+  auto by_cnt = [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; };
+  if (!graph_major) {
+    std::stable_sort(order.begin(), order.end(), by_cnt);
+    return;
+  }
+  for (size_t g = 0; g + 1 < goff.size(); ++g)
+    std::stable_sort(order.begin() + goff[g], order.begin() + goff[g + 1], by_cnt);
+}
+
 // Per-launch algorithmic cost: one GRU application = 2*3H*(DIN+H) + 14H flops.
 double gru_flops(int din, int H) { return 2.0 * 3 * H * (din + H) + 14.0 * H; }
 
@@ -222,6 +242,9 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = atoi(v) == 1 ? 1 : 2;
+  if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
+  if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -584,7 +607,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if (flen[r] == 0)   // AUX:793-795: gather_nd(outputs, [d, final_len-1]) with -1
           return fail(IGN_ERR_INVALID, "destination row %lld receives no message: the reference's sorted update"
                       " gathers position -1 (AUX:793-795)", (long long)r);
-      std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
+      sort_order(order, flen, b->row_off[dst], p->graph_major);
       // bucket messages by destination (stable), keep those with pos < final_len, sort by pos
       std::vector<int64_t> dcnt(ND + 1, 0);
       for (size_t k = 0; k < mdst.size(); ++k) dcnt[mdst[k] + 1]++;
@@ -657,7 +680,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.bytes = (double)steps * (12.0 * H + 4) + (double)ND * (8.0 * H + 12);
       b->gru_steps += steps * p->T;
     } else {
-      std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
+      sort_order(order, flen, b->row_off[dst], p->graph_major);
       std::vector<int32_t> where(ND);
       for (int64_t i = 0; i < ND; ++i) where[order[i]] = (int32_t)i;
       std::vector<int32_t> ptr(ND + 1, 0);
@@ -804,13 +827,13 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
           tm.end();
         }
         SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
-                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst};
+                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         tm.begin(K_SEQ, mb.flops, mb.bytes);
-        HIP_TRY(launch_seq_gru(a, cp.H, st));
+        HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
         tm.end();
       } else {
         SumGruArgs a{hin, hout, sbases, mb.d_order, mb.d_msg_ptr, mb.d_msg_src,
-                     p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst};
+                     p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         tm.begin(K_SUM, mb.flops, mb.bytes);
         HIP_TRY(launch_sum_gru(a, mp.din, cp.H, st));
         tm.end();

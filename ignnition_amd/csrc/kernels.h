@@ -25,6 +25,7 @@ struct SeqGruArgs {
   const float* Up;           // packed recurrent-kernel fragments
   const float* bias;         // [4][H] combined biases
   int64_t n_dst;
+  int xcd_remap;             // XCD-aware tile order (speed only)
 };
 
 struct SumGruArgs {
@@ -38,6 +39,7 @@ struct SumGruArgs {
   const float* Up;
   const float* bias;
   int64_t n_dst;
+  int xcd_remap;
 };
 
 struct Readout3Args {
@@ -59,7 +61,7 @@ bool gru_shape_supported(int din, int h);
 hipError_t launch_project(const float* x, int64_t n, const float* Wp, float* out, int din, int h, hipStream_t st);
 hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
                             const uint32_t* rows, int W, hipStream_t st);
-hipError_t launch_seq_gru(const SeqGruArgs& args, int h, hipStream_t st);
+hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);

@@ -62,6 +62,18 @@ __device__ __forceinline__ float act_t(float x) {
   else return x;
 }
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (b, b+8, ...
+// share one), so remap so that XCD x runs a contiguous range of tiles (bijective for any grid,
+// cdna_hip_programming.md §5.5).  Consecutive tiles are the same graph -> that graph's source
+// rows stay in one XCD's L2.  Placement only affects speed, never results.
+__device__ __forceinline__ int64_t xcd_block(int enabled) {
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  if (!enabled) return b;
+  const int64_t xcd = b & 7, q = nb >> 3, r = nb & 7;
+  const int64_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
@@ -296,7 +308,7 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const int64_t pos = (xcd_block(a.xcd_remap) * 4 + wave) * 16 + j;
   const bool valid = pos < a.n_dst;
 
   float u[3][NT][KH];   // recurrent kernel fragments, resident for the whole sequence
@@ -378,6 +390,106 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Variant 2 of the ordered update: identical math to seq_gru_kernel, but the recurrent-kernel
+// fragments live in LDS (12 KB per block at H=32, shared by its 4 waves) instead of 48 VGPRs per
+// lane, so more waves fit per SIMD to hide the gather latency.  LDS image: float4 per lane
+// holding 4 consecutive k-steps, [gate][unit tile][k-step/4][lane] -> one ds_read_b128 feeds 4 MFMAs.
+template <int H>
+__device__ __forceinline__ void stage_frag_lds(f4* dst, const float* __restrict__ src, int KS) {
+  // src: packed fragments [3][NT][KS][64]; dst: [3][NT][KS/4][64] of f4
+  const int n = 3 * (H / 16) * KS * 64;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int lane = e & 63;
+    const int f = e >> 6;
+    const int s = f % KS, gt = f / KS;
+    dst[(gt * (KS / 4) + (s >> 2)) * 64 + lane][s & 3] = src[e];
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
+  constexpr int NT = H / 16, KH = H / 4, K4 = KH / 4;
+  __shared__ float sbias[4 * H];
+  __shared__ f4 su[3 * NT * K4 * 64];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+  stage_frag_lds<H>(su, a.Up, KH);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = (xcd_block(a.xcd_remap) * 4 + wave) * 16 + j;
+  const bool valid = pos < a.n_dst;
+  const int row = valid ? a.order[pos] : 0;
+  const int L = valid ? a.len[pos] : 0;
+  const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+  const float* tab = a.table + 4 * g;
+  f4 h[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  int Lmax = L;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  __syncthreads();
+
+  uint32_t code = codes[0];
+  for (int t = 0; t < Lmax; ++t) {
+    f4 x[3][NT];
+    {
+      const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+    }
+    const uint32_t next = codes[t + 1];
+    __builtin_amdgcn_sched_barrier(0);
+    f4 az[NT], ar[NT], ah[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const int u0 = 16 * i + 4 * g;
+      az[i] = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+      ar[i] = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < K4; ++s4) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const f4 wz = su[((0 * NT + i) * K4 + s4) * 64 + lane];
+        const f4 wr = su[((1 * NT + i) * K4 + s4) * 64 + lane];
+        const f4 wh = su[((2 * NT + i) * K4 + s4) * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float hb = h[s4][q];
+          az[i] = MFMA(wz[q], hb, az[i]);
+          ar[i] = MFMA(wr[q], hb, ar[i]);
+          ah[i] = MFMA(wh[q], hb, ah[i]);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const bool act = t < L;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const f4 bx = *reinterpret_cast<const f4*>(sbias + 2 * H + 16 * i + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sigmoidf_(az[i][r] + x[0][i][r]);
+        const float rr = sigmoidf_(ar[i][r] + x[1][i][r]);
+        const float c = tanhf_(x[2][i][r] + bx[r] + rr * ah[i][r]);
+        const float hn = z * h[i][r] + (1.0f - z) * c;
+        h[i][r] = act ? hn : h[i][r];
+      }
+    }
+    code = next;
+  }
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
@@ -390,7 +502,7 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const int64_t pos = (xcd_block(a.xcd_remap) * 4 + wave) * 16 + j;
   const bool valid = pos < a.n_dst;
 
   const int row = valid ? a.order[pos] : 0;
@@ -627,8 +739,15 @@ hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, c
   return hipGetLastError();
 }
 
-hipError_t launch_seq_gru(const SeqGruArgs& args, int h, hipStream_t st) {
+hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
+  if (variant == 2) {
+    dim3 grid(grid_for(args.n_dst, 64)), block(256);
+    if (h == 32) hipLaunchKernelGGL((seq_gru2_kernel<32>), grid, block, 0, st, args);
+    else if (h == 16) hipLaunchKernelGGL((seq_gru2_kernel<16>), grid, block, 0, st, args);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   dim3 grid(grid_for(args.n_dst, 64)), block(256);
   if (h == 32) hipLaunchKernelGGL((seq_gru_kernel<32>), grid, block, 0, st, args);
   else if (h == 16) hipLaunchKernelGGL((seq_gru_kernel<16>), grid, block, 0, st, args);
