@@ -90,11 +90,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # IGN_DIST_BACKEND=gloo + IGN_BENCH_DEVICE=0 rehearse the N>1 path on a one-GPU box
+    backend = os.environ.get("IGN_DIST_BACKEND", "nccl")
+    device = int(os.environ.get("IGN_BENCH_DEVICE", local))
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(device)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     import numpy as np
 
@@ -105,17 +111,18 @@ def main():
         eng.synchronize()
         if dist is not None:
             dist.barrier()
-            import torch
-            torch.cuda.synchronize()
+            eng.synchronize()
 
     # per-rank shard: graphs [rank*G, (rank+1)*G) -> weak scaling, no forward collective
-    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(args.model, args.topology, args.graphs,
-                                                            first_id=rank * args.graphs)
+    ids = workloads.shard_graph_ids(rank, world, args.graphs)
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(args.model, args.topology, len(ids), first_id=ids[0])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(seed=0, bias_scale=0.05)
-    eng = Engine(plan, local if world > 1 else 0)
+    eng = Engine(plan, device if world > 1 else 0)
     eng.set_params(prm)
+    t_build = time.perf_counter()
     batch = Batch(eng, graphs)
+    t_build = time.perf_counter() - t_build
     edges = batch.edges_per_forward
 
     for _ in range(args.warmup):
@@ -128,12 +135,12 @@ def main():
     barrier_sync(eng)
     dt = time.perf_counter() - t0
     stats = eng.stats()
-    if dist is not None:
+    dev = None
+    if dist is not None and backend == "nccl":
         import torch
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    total_edges = edges * args.steps * world
+        dev = torch.device("cuda", device)
+    dt, total_edges_step = workloads.reduce_step_stats(dist, dt, edges, dev)
+    total_edges = total_edges_step * args.steps
     value = total_edges / dt
 
     if rank != 0:
@@ -171,7 +178,8 @@ def main():
         "config": {"workload": workload, "model": args.model, "graphs_per_gpu": args.graphs,
                    "global_batch": args.graphs * world, "hidden": plan.hidden[0], "iterations": plan.iterations,
                    "edges_per_step_per_gpu": edges, "gru_steps_per_forward": batch.gru_steps_per_forward,
-                   "parallelism": "graph-sharded (%d ranks), no collective in the forward" % world},
+                   "parallelism": "graph-sharded (%d ranks), no collective in the forward" % world,
+                   "batch_build_s": round(t_build, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

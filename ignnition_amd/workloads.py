@@ -93,3 +93,28 @@ def edges_per_forward(mi, graphs) -> int:
             for s in mp.source_entities:
                 tot += sum(len(g["src_" + s.adj_vector]) for g in graphs)
     return T * tot
+
+
+# ----------------------------------------------------------------------------------------------
+# Multi-GPU sharding (one process per GPU).  RouteNet / Q-size batches shard by graph: graphs are
+# independent, so each rank owns a disjoint range of graph ids and the forward needs no
+# collective (weak scaling: every rank processes `per_rank` graphs).  Timing is reduced with a
+# MAX over ranks; edge counts with a SUM.
+
+def shard_graph_ids(rank: int, world: int, per_rank: int) -> list:
+    """Graph ids owned by ``rank``: [rank*per_rank, (rank+1)*per_rank)."""
+    if not (0 <= rank < world):
+        raise ValueError("rank out of range")
+    return list(range(rank * per_rank, (rank + 1) * per_rank))
+
+
+def reduce_step_stats(dist, elapsed_s: float, edges: int, device=None):
+    """(max elapsed over ranks, total edges over ranks).  ``dist`` is torch.distributed or None."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return elapsed_s, edges
+    import torch
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
+    e = torch.tensor([edges], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(e, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(e.item())

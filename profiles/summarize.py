@@ -9,13 +9,15 @@ import os
 import sys
 from collections import defaultdict
 
-KINDS = {"seq_gru": "seq_gru_kernel", "sum_gru": "sum_gru_kernel", "readout": "readout3_kernel",
-         "project": "project_kernel", "init_state": "init_state_kernel"}
+import re
+
+KINDS = {"seq_gru": r"seq_gru\d*_kernel", "sum_gru": r"sum_gru\d*_kernel", "readout": r"readout3_kernel",
+         "project": r"project_kernel", "init_state": r"init_state_kernel"}
 
 
 def kind_of(name):
     for k, pat in KINDS.items():
-        if pat in name:
+        if re.search(pat, name):
             return k
     return None
 
