@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libignmp.so")
+# IGN_LIB_PATH selects an alternative in-tree build (used for A/B of compile flags)
+LIB_PATH = os.environ.get("IGN_LIB_PATH", os.path.join(HERE, "libignmp.so"))
 
 i32, i64, f32 = C.c_int32, C.c_int64, C.c_float
 

@@ -103,6 +103,7 @@ struct ign_plan {
   // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
   bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
+  int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev;     // pairs
@@ -245,6 +246,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = atoi(v) == 1 ? 1 : 2;
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
+  if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -827,7 +829,8 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
           tm.end();
         }
         SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
-                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
+                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
+                     mb.n_steps};
         tm.begin(K_SEQ, mb.flops, mb.bytes);
         HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
         tm.end();

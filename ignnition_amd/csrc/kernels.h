@@ -26,6 +26,8 @@ struct SeqGruArgs {
   const float* bias;         // [4][H] combined biases
   int64_t n_dst;
   int xcd_remap;             // XCD-aware tile order (speed only)
+  int ablate;                // diagnostics: 1 = every step reads the zero row (see kernel)
+  int64_t zero_slot;         // index in step_code of a padding entry (= zero row)
 };
 
 struct SumGruArgs {

@@ -421,7 +421,10 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
   const bool valid = pos < a.n_dst;
   const int row = valid ? a.order[pos] : 0;
   const int L = valid ? a.len[pos] : 0;
-  const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+  // ablation (diagnostics only, IGN_SEQ_ABLATE=1): every step reads the zero row's code slot,
+  // so the gather hits one cached row while the instruction stream stays the same
+  const uint32_t* codes = a.ablate ? a.step_code + a.zero_slot
+                                   : a.step_code + (valid ? a.step_ptr[pos] : 0);
   const float* tab = a.table + 4 * g;
   f4 h[NT];
 #pragma unroll
