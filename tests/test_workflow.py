@@ -1,0 +1,56 @@
+"""User workflow through train_options.ini + model_description.json (FO:34-91, 169-268)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ignnition_amd import framework_operations as fo
+from ignnition_amd import generate_model as gm
+from ignnition_amd import workloads
+from examples.make_example import make
+
+
+@pytest.fixture()
+def example_dir(tmp_path):
+    d = make("routenet", str(tmp_path / "rn"), "nsfnet", 3)
+    fo.load_config(os.path.join(d, "train_options.ini"))
+    gm.register_user_functions(workloads.USER_FUNCTIONS)
+    return d
+
+
+def test_create_model_and_debug(example_dir):
+    mi = fo.create_model()
+    assert mi.get_mp_iterations() == 8
+    dims = fo.find_dataset_dimensions(fo.CONFIG["PATHS"]["train_dataset"])
+    assert dims["traffic"] == 1 and dims["adj_links_paths"] == 0
+    dump = fo.debug(mi, out_dir=os.path.join(example_dir, "debug_model"))
+    plan = json.load(open(os.path.join(example_dir, "debug_model", "plan.json")))
+    assert plan["iterations"] == 8 and len(plan["message_passings"]) == 2
+    assert dump["cells"][0][0] == "path"
+
+
+def test_input_fn_batches(example_dir):
+    mi = fo.create_model()
+    gm.set_model_info(mi)
+    it = gm.input_fn(fo.CONFIG["PATHS"]["train_dataset"], training=True, batch_size=2, repeat=False)
+    xs, ys = next(it)
+    assert len(xs) == 2 and len(ys) == 2
+    # labels normalised with `log` (RNJ:107)
+    assert np.all(np.asarray(ys[0]) < 5)
+
+
+@pytest.mark.gpu
+def test_predict_end_to_end(example_dir):
+    from oracle.dense_forward import DenseOracle
+    mi = fo.create_model()
+    prm = __import__("ignnition_amd.engine", fromlist=["MPPlan"]).MPPlan.from_model_info(mi).init_params(3)
+    preds = fo.predict(mi, params=prm, batch_size=2)
+    assert len(preds) == 3
+    gm.set_model_info(mi)
+    graphs = [g for batch in gm.input_fn(fo.CONFIG["PATHS"]["predict_dataset"], training=False, repeat=False)
+              for g in batch]
+    desc = json.load(open(fo.CONFIG["PATHS"]["json_path"]))
+    ref = DenseOracle(desc, fo.find_dataset_dimensions(fo.CONFIG["PATHS"]["train_dataset"]), prm).forward(graphs)
+    got = np.concatenate(preds)   # no label_denormalization in RNJ -> normalised outputs
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
