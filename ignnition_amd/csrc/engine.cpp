@@ -819,13 +819,15 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
         for (size_t s = 0; s < mp.src.size(); ++s) {
           const int64_t rs = mb.src_rows[s];
           tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3));
-          HIP_TRY(launch_project(sbases.base[s], rs, p->d_packed + cp.pk_w, mb.d_table + mb.src_off[s] * W3,
+          HIP_TRY(launch_project(sbases.base[s], rs, p->d_packed + cp.pk_w, p->d_packed + cp.pk_b,
+                                 mb.d_table + mb.src_off[s] * W3, s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr,
                                  mp.din, cp.H, st));
           tm.end();
         }
         if (mb.n_multi) {
           tm.begin(K_OTHER, 0, 0);
-          HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3, st));
+          HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3,
+                                   mb.d_table + mb.zero_row * W3, st));
           tm.end();
         }
         SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,

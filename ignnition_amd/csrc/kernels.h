@@ -17,7 +17,7 @@ struct SrcBases {
 struct SeqGruArgs {
   const float* h_in;         // [rows][H] destination state before the update
   float* h_out;              // [rows][H] destination state after the update
-  const float* table;        // projected message table [sources' rows | zero row | multi rows][3H]
+  const float* table;        // projected message table [sources' rows | bias row | multi rows][3H]
   const int32_t* order;      // [n_dst] destination rows, sorted by final_len (descending)
   const int32_t* len;        // [n_dst] final_len per order position
   const int32_t* step_ptr;   // [n_dst] first step of each order position
@@ -60,9 +60,10 @@ hipError_t launch_pack_gru(const float* W, const float* U, const float* bias, fl
                            int DIN, int H, hipStream_t st);
 hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStream_t st);
 bool gru_shape_supported(int din, int h);
-hipError_t launch_project(const float* x, int64_t n, const float* Wp, float* out, int din, int h, hipStream_t st);
+hipError_t launch_project(const float* x, int64_t n, const float* Wp, const float* bp, float* out, float* bias_row,
+                          int din, int h, hipStream_t st);
 hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
-                            const uint32_t* rows, int W, hipStream_t st);
+                            const uint32_t* rows, int W, const float* bias_row, hipStream_t st);
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);

@@ -37,6 +37,16 @@ __device__ __forceinline__ float tanhf_(float x) {
   return 1.0f - 2.0f * rcpf_(__expf(2.0f * x) + 1.0f);
 }
 
+// GRU gates on pre-scaled pre-activations.  pack_gru scales the z/r columns (and their biases)
+// by -log2(e) and the candidate columns by 2*log2(e), so
+//   sigmoid(a) = 1 / (1 + 2^(a'))      with a' = -log2(e) a
+//   tanh(c)    = 1 - 2 / (1 + 2^(c'))  with c' = 2 log2(e) c   (c' is linear in x, h, biases)
+// i.e. one v_exp_f32 + one v_rcp_f32 per gate and no scaling multiply.
+#define IGN_NLOG2E (-1.4426950408889634f)
+#define IGN_2LOG2E (2.8853900817779268f)
+__device__ __forceinline__ float sig2_(float a) { return rcpf_(1.0f + __builtin_amdgcn_exp2f(a)); }
+__device__ __forceinline__ float tanh2_(float c) { return 1.0f - 2.0f * rcpf_(1.0f + __builtin_amdgcn_exp2f(c)); }
+
 __device__ __forceinline__ float act_apply(float x, int act) {
   switch (act) {
     case IGN_K_ACT_RELU: return x > 0.f ? x : 0.f;
@@ -116,19 +126,20 @@ __global__ void pack_gru_kernel(const float* __restrict__ W, const float* __rest
       int gate = (int)(gt / NT);
       int k = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
       int col = gate * H + 16 * t + (lane & 15);
-      if (isU) Up[idx] = U[(int64_t)k * 3 * H + col];
-      else     Wp[idx] = W[(int64_t)k * 3 * H + col];
+      const float sc = gate == 2 ? IGN_2LOG2E : IGN_NLOG2E;   // see sig2_/tanh2_
+      if (isU) Up[idx] = sc * U[(int64_t)k * 3 * H + col];
+      else     Wp[idx] = sc * W[(int64_t)k * 3 * H + col];
     } else {
-      // combined biases: [0] bz_in+bz_rec, [1] br_in+br_rec, [2] bh_in, [3] bh_rec
+      // combined, pre-scaled biases: [0] bz_in+bz_rec, [1] br_in+br_rec, [2] bh_in, [3] bh_rec
       int b = (int)(e - nW - nU);
       int which = b / H, u = b % H;
       const float* bin = bias;            // bias[0][:]
       const float* brec = bias + 3 * H;   // bias[1][:]
       float v;
-      if (which == 0) v = bin[u] + brec[u];
-      else if (which == 1) v = bin[H + u] + brec[H + u];
-      else if (which == 2) v = bin[2 * H + u];
-      else v = brec[2 * H + u];
+      if (which == 0) v = IGN_NLOG2E * (bin[u] + brec[u]);
+      else if (which == 1) v = IGN_NLOG2E * (bin[H + u] + brec[H + u]);
+      else if (which == 2) v = IGN_2LOG2E * bin[2 * H + u];
+      else v = IGN_2LOG2E * brec[2 * H + u];
       bp[b] = v;
     }
   }
@@ -215,10 +226,10 @@ __device__ __forceinline__ void gru_step(const GruWeights<DIN, H>& W, const floa
   for (int t = 0; t < NT; ++t) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float z = sigmoidf_(az[t][r]);
-      float rr = sigmoidf_(ar[t][r]);
-      float c = tanhf_(ax[t][r] + rr * ah[t][r]);
-      h[t][r] = z * h[t][r] + (1.0f - z) * c;
+      const float z = sig2_(az[t][r]);
+      const float rr = sig2_(ar[t][r]);
+      const float c = tanh2_(ax[t][r] + rr * ah[t][r]);
+      h[t][r] = c + z * (h[t][r] - c);
     }
   }
 }
@@ -242,9 +253,14 @@ __device__ __forceinline__ const float* src_ptr(const SrcBases& sb, uint32_t cod
 // Output row layout [3H]: gate-major z | r | h, same as the Keras kernel columns.
 template <int DIN, int H>
 __global__ __launch_bounds__(256) void project_kernel(const float* __restrict__ x, int64_t n,
-                                                      const float* __restrict__ Wp, float* __restrict__ out) {
-  // out points at this source's first row inside the MP's combined projected table
+                                                      const float* __restrict__ Wp, const float* __restrict__ bp,
+                                                      float* __restrict__ out, float* __restrict__ bias_row) {
+  // out points at this source's first row inside the MP's combined projected table.  Rows hold
+  // x.W' + b' (pre-scaled, input-side biases [bz, br, bh_in]); bias_row (if set) receives b'
+  // alone: the table row of a hole (zero input).
   constexpr int NC = DIN / 16, NT = H / 16, KX = DIN / 4;
+  if (bias_row && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) bias_row[i] = bp[i];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -257,7 +273,7 @@ __global__ __launch_bounds__(256) void project_kernel(const float* __restrict__ 
 #pragma unroll
   for (int G = 0; G < 3; ++G)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[G][t] = f4{0, 0, 0, 0};
+    for (int t = 0; t < NT; ++t) acc[G][t] = ld4(bp + G * H + 16 * t + 4 * g);
 #pragma unroll
   for (int s = 0; s < KX; ++s) {
     const float xb = xv[s >> 2][s & 3];
@@ -278,7 +294,9 @@ __global__ __launch_bounds__(256) void project_kernel(const float* __restrict__ 
 // Positions that receive several messages (scatter_nd adds them, GM:490): row multi_base + k of
 // the projected table = sum of the projected rows listed for k.  Rare; one thread per float4.
 __global__ void multi_sum_kernel(float* __restrict__ table, int64_t multi_base, int64_t n_multi,
-                                 const int32_t* __restrict__ ptr, const uint32_t* __restrict__ rows, int W) {
+                                 const int32_t* __restrict__ ptr, const uint32_t* __restrict__ rows, int W,
+                                 const float* __restrict__ bias_row) {
+  // every projected row carries the input bias once; a sum of k rows must carry it once too
   const int64_t q = W / 4;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n_multi * q; i += (int64_t)gridDim.x * blockDim.x) {
@@ -286,6 +304,7 @@ __global__ void multi_sum_kernel(float* __restrict__ table, int64_t multi_base, 
     const int c = (int)(i - k * q) * 4;
     f4 acc = f4{0, 0, 0, 0};
     for (int m = ptr[k]; m < ptr[k + 1]; ++m) acc += ld4(table + (int64_t)rows[m] * W + c);
+    acc -= (float)(ptr[k + 1] - ptr[k] - 1) * ld4(bias_row + c);
     st4(table + (multi_base + k) * W + c, acc);
   }
 }
@@ -352,10 +371,9 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
     f4 az[NT], ar[NT], ah[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const int u0 = 16 * i + 4 * g;
-      az[i] = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
-      ar[i] = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
-      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+      az[i] = f4{0, 0, 0, 0};
+      ar[i] = f4{0, 0, 0, 0};
+      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
     }
 #pragma unroll
     for (int s = 0; s < KH; ++s) {
@@ -371,13 +389,12 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
     const bool act = t < L;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const f4 bx = *reinterpret_cast<const f4*>(sbias + 2 * H + 16 * i + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = sigmoidf_(az[i][r] + x[0][i][r]);
-        const float rr = sigmoidf_(ar[i][r] + x[1][i][r]);
-        const float c = tanhf_(x[2][i][r] + bx[r] + rr * ah[i][r]);
-        const float hn = z * h[i][r] + (1.0f - z) * c;
+      for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
+        const float z = sig2_(az[i][r] + x[0][i][r]);
+        const float rr = sig2_(ar[i][r] + x[1][i][r]);
+        const float c = tanh2_(x[2][i][r] + rr * ah[i][r]);
+        const float hn = c + z * (h[i][r] - c);
         h[i][r] = act ? hn : h[i][r];
       }
     }
@@ -453,10 +470,9 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
     f4 az[NT], ar[NT], ah[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const int u0 = 16 * i + 4 * g;
-      az[i] = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
-      ar[i] = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
-      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+      az[i] = f4{0, 0, 0, 0};
+      ar[i] = f4{0, 0, 0, 0};
+      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
     }
 #pragma unroll
     for (int s4 = 0; s4 < K4; ++s4) {
@@ -478,13 +494,12 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
     const bool act = t < L;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const f4 bx = *reinterpret_cast<const f4*>(sbias + 2 * H + 16 * i + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = sigmoidf_(az[i][r] + x[0][i][r]);
-        const float rr = sigmoidf_(ar[i][r] + x[1][i][r]);
-        const float c = tanhf_(x[2][i][r] + bx[r] + rr * ah[i][r]);
-        const float hn = z * h[i][r] + (1.0f - z) * c;
+      for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
+        const float z = sig2_(az[i][r] + x[0][i][r]);
+        const float rr = sig2_(ar[i][r] + x[1][i][r]);
+        const float c = tanh2_(x[2][i][r] + rr * ah[i][r]);
+        const float hn = c + z * (h[i][r] - c);
         h[i][r] = act ? hn : h[i][r];
       }
     }
@@ -730,23 +745,24 @@ bool gru_shape_supported(int din, int h) {
   return (din == 16 || din == 32) && (h == 16 || h == 32);
 }
 
-hipError_t launch_project(const float* x, int64_t n, const float* Wp, float* out, int din, int h, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  dim3 grid(grid_for(n, 64)), block(256);
-  if (din == 32 && h == 32) hipLaunchKernelGGL((project_kernel<32, 32>), grid, block, 0, st, x, n, Wp, out);
-  else if (din == 16 && h == 16) hipLaunchKernelGGL((project_kernel<16, 16>), grid, block, 0, st, x, n, Wp, out);
-  else if (din == 16 && h == 32) hipLaunchKernelGGL((project_kernel<16, 32>), grid, block, 0, st, x, n, Wp, out);
-  else if (din == 32 && h == 16) hipLaunchKernelGGL((project_kernel<32, 16>), grid, block, 0, st, x, n, Wp, out);
+hipError_t launch_project(const float* x, int64_t n, const float* Wp, const float* bp, float* out, float* bias_row,
+                          int din, int h, hipStream_t st) {
+  dim3 grid(std::max(1, grid_for(n, 64))), block(256);
+  if (din == 32 && h == 32) hipLaunchKernelGGL((project_kernel<32, 32>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
+  else if (din == 16 && h == 16) hipLaunchKernelGGL((project_kernel<16, 16>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
+  else if (din == 16 && h == 32) hipLaunchKernelGGL((project_kernel<16, 32>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
+  else if (din == 32 && h == 16) hipLaunchKernelGGL((project_kernel<32, 16>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
-                            const uint32_t* rows, int W, hipStream_t st) {
+                            const uint32_t* rows, int W, const float* bias_row, hipStream_t st) {
   if (n_multi == 0) return hipSuccess;
   int64_t total = n_multi * (W / 4);
   int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(multi_sum_kernel, dim3(blocks), dim3(256), 0, st, table, multi_base, n_multi, ptr, rows, W);
+  hipLaunchKernelGGL(multi_sum_kernel, dim3(blocks), dim3(256), 0, st, table, multi_base, n_multi, ptr, rows, W,
+                     bias_row);
   return hipGetLastError();
 }
 
