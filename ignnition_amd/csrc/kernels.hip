@@ -804,7 +804,7 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
 
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  // one tile per wave: measured faster than the persistent grid for this latency-bound gather
+  // one tile per wave: measured faster than a persistent grid for this latency-bound gather
   // (0.109 vs 0.141 ms on 512 x synth50): more independent waves queue behind the resident ones
   dim3 grid(grid_for(args.n_dst, 64));
 #define SUM_CASE(D, HH)                                                                    \
