@@ -38,7 +38,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graphs", type=int, default=512, help="graphs per GPU")
     ap.add_argument("--topology", default="synth50")
-    ap.add_argument("--model", default="routenet", choices=["routenet", "qsize"])
+    ap.add_argument("--model", default="routenet", choices=["routenet", "qsize", "synthetic"],
+                    help="synthetic = the 1M-node / 10M-edge graph of BASELINE configs[4] (one graph per rank)")
+    ap.add_argument("--nodes", type=int, default=1_000_000, help="synthetic graph size")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -114,8 +116,12 @@ def main():
             eng.synchronize()
 
     # per-rank shard: graphs [rank*G, (rank+1)*G) -> weak scaling, no forward collective
-    ids = workloads.shard_graph_ids(rank, world, args.graphs)
-    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(args.model, args.topology, len(ids), first_id=ids[0])
+    if args.model == "synthetic":
+        args.graphs, args.topology = 1, "1m" if args.nodes == 1_000_000 else str(args.nodes)
+        desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=args.nodes, graph_id=rank)
+    else:
+        ids = workloads.shard_graph_ids(rank, world, args.graphs)
+        desc, dims, mi, graphs, _ = workloads.make_batch_inputs(args.model, args.topology, len(ids), first_id=ids[0])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(seed=0, bias_scale=0.05)
     eng = Engine(plan, device if world > 1 else 0)
@@ -167,7 +173,7 @@ def main():
                                 "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
                             for k, v in stats.items() if v["launches"]}}
     cpu = None
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and args.model != "synthetic":
         cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
     line = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,

@@ -311,7 +311,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (cp.din != din)
       return fail(IGN_ERR_INVALID, "mp %d: cell input_dim %d != message dim %d", m, cp.din, din);
     if (!gru_shape_supported(din, cp.H))
-      return fail(IGN_ERR_UNSUPPORTED, "mp %d: GRU shape (input %d, units %d) not instantiated (16/32)", m, din, cp.H);
+      return fail(IGN_ERR_UNSUPPORTED, "mp %d: GRU shape (input %d, units %d) not instantiated (16/32, 64/64)", m,
+                  din, cp.H);
     cp.used = true;
     p->mps.push_back(mp);
   }
@@ -830,6 +831,8 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
                                    mb.d_table + mb.zero_row * W3, st));
           tm.end();
         }
+        if (cp.H == 64 && p->seq_variant != 2)
+          return fail(IGN_ERR_UNSUPPORTED, "64-unit ordered updates need the LDS variant (IGN_SEQ_VARIANT=2)");
         SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
                      mb.n_steps};

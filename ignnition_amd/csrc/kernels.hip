@@ -103,7 +103,7 @@ __global__ void init_state_kernel(float* __restrict__ state, const float* __rest
 // ---------------------------------------------------------------------------------------------
 // GRU weight packing.  Keras GRUCell v2 layout: kernel [DIN][3H], recurrent_kernel [H][3H],
 // bias [2][3H]; gate column order z, r, h (AUX:748-749).
-// Packed fragment f = ((gate * NT + t) * KS + s), 64 lanes each:
+// Packed fragment (gate, t, s), 64 lanes each, stored float4-grouped over s (see below):
 //   lane l -> M[k(s, l>>4)][gate*H + 16t + (l&15)]
 __global__ void pack_gru_kernel(const float* __restrict__ W, const float* __restrict__ U,
                                 const float* __restrict__ bias, float* __restrict__ Wp,
@@ -115,13 +115,15 @@ __global__ void pack_gru_kernel(const float* __restrict__ W, const float* __rest
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = i; e < nW + nU + 4LL * H; e += stride) {
     if (e < nW + nU) {
+      // float4-grouped fragments: idx = (((gate*NT + t)*KS/4 + s/4)*64 + lane)*4 + s%4, so one
+      // 16-B read per lane yields 4 consecutive k-steps (global dwordx4, ds_read_b128, LDS copy)
       bool isU = e >= nW;
       int64_t idx = isU ? e - nW : e;
       int KS = isU ? H / 4 : DIN / 4;
-      int lane = (int)(idx & 63);
-      int64_t f = idx >> 6;
-      int s = (int)(f % KS);
-      int64_t gt = f / KS;
+      int lane = (int)((idx >> 2) & 63);
+      int64_t f4i = idx >> 8;               // (gate*NT + t)*KS/4 + s/4
+      int s = (int)((f4i % (KS / 4)) * 4 + (idx & 3));
+      int64_t gt = f4i / (KS / 4);
       int t = (int)(gt % NT);
       int gate = (int)(gt / NT);
       int k = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
@@ -167,6 +169,11 @@ __global__ void pack_dense_kernel(const float* __restrict__ W, float* __restrict
 // One GRU step for the wave's 16 rows (reset_after=True, AUX:764 / Keras GRUCell v2):
 //   z = s(x Wz + h Uz + bz) ; r = s(x Wr + h Ur + br) ; c = tanh(x Wh + bhx + r (h Uh + bhh))
 //   h' = z h + (1 - z) c
+// element (gate-tile gt, k-step s, lane) of a float4-grouped fragment array with KS k-steps
+__device__ __forceinline__ int64_t frag_idx(int gt, int s, int KS, int lane) {
+  return ((((int64_t)gt * (KS / 4) + (s >> 2)) * 64 + lane) << 2) + (s & 3);
+}
+
 template <int DIN, int H>
 struct GruWeights {
   static constexpr int NT = H / 16, KX = DIN / 4, KH = H / 4;
@@ -183,9 +190,9 @@ __device__ __forceinline__ void load_gru_weights(GruWeights<DIN, H>& W, const fl
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
-      for (int s = 0; s < KX; ++s) W.w[g][t][s] = Wp[(((g * NT + t) * KX + s) << 6) + lane];
+      for (int s = 0; s < KX; ++s) W.w[g][t][s] = Wp[frag_idx(g * NT + t, s, KX, lane)];
 #pragma unroll
-      for (int s = 0; s < KH; ++s) W.u[g][t][s] = Up[(((g * NT + t) * KH + s) << 6) + lane];
+      for (int s = 0; s < KH; ++s) W.u[g][t][s] = Up[frag_idx(g * NT + t, s, KH, lane)];
     }
 }
 
@@ -280,7 +287,7 @@ __global__ __launch_bounds__(256) void project_kernel(const float* __restrict__ 
 #pragma unroll
     for (int G = 0; G < 3; ++G)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[G][t] = MFMA(Wp[(((G * NT + t) * KX + s) << 6) + lane], xb, acc[G][t]);
+      for (int t = 0; t < NT; ++t) acc[G][t] = MFMA(Wp[frag_idx(G * NT + t, s, KX, lane)], xb, acc[G][t]);
   }
   if (valid) {
 #pragma unroll
@@ -336,7 +343,7 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < KH; ++s) u[G][t][s] = a.Up[(((G * NT + t) * KH + s) << 6) + lane];
+      for (int s = 0; s < KH; ++s) u[G][t][s] = a.Up[frag_idx(G * NT + t, s, KH, lane)];
 
   const int row = valid ? a.order[pos] : 0;
   const int L = valid ? a.len[pos] : 0;
@@ -413,14 +420,10 @@ __global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
 // holding 4 consecutive k-steps, [gate][unit tile][k-step/4][lane] -> one ds_read_b128 feeds 4 MFMAs.
 template <int H>
 __device__ __forceinline__ void stage_frag_lds(f4* dst, const float* __restrict__ src, int KS) {
-  // src: packed fragments [3][NT][KS][64]; dst: [3][NT][KS/4][64] of f4
-  const int n = 3 * (H / 16) * KS * 64;
-  for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int lane = e & 63;
-    const int f = e >> 6;
-    const int s = f % KS, gt = f / KS;
-    dst[(gt * (KS / 4) + (s >> 2)) * 64 + lane][s & 3] = src[e];
-  }
+  // src is already float4-grouped ([3][NT][KS/4][64] x f4): a straight vector copy
+  const int n = 3 * (H / 16) * (KS / 4) * 64;
+  const f4* s4 = reinterpret_cast<const f4*>(src);
+  for (int e = threadIdx.x; e < n; e += blockDim.x) dst[e] = s4[e];
 }
 
 template <int H>
@@ -572,6 +575,100 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sum update for wide cells (H or DIN = 64, e.g. the 1M-node synthetic graph): the 2 x 3H x K
+// weight fragments (96 KB at 64/64) fit neither in registers nor comfortably in LDS, so they
+// stream from L2 as float4 (4 k-steps) per lane, reused across the 16 rows of the tile.
+template <int DIN, int H>
+__global__ __launch_bounds__(256) void sum_gru_wide_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16;
+  __shared__ float sbias[4 * H];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = (xcd_block(a.xcd_remap) * 4 + wave) * 16 + j;
+  const bool valid = pos < a.n_dst;
+  const int row = valid ? a.order[pos] : 0;
+  const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+  const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+
+  f4 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+  int64_t m = m0;
+  for (; m + 2 <= m1; m += 2) {
+    const float* p0 = src_ptr(a.src, a.msg_src[m], DIN);
+    const float* p1 = src_ptr(a.src, a.msg_src[m + 1], DIN);
+    f4 v0[NC], v1[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      v0[c] = ld4(p0 + 16 * c + 4 * g);
+      v1[c] = ld4(p1 + 16 * c + 4 * g);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
+  }
+  for (; m < m1; ++m) {
+    const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+  }
+  f4 h[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  __syncthreads();
+
+  const f4* W4 = reinterpret_cast<const f4*>(a.Wp);
+  const f4* U4 = reinterpret_cast<const f4*>(a.Up);
+  f4 hn[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int u0 = 16 * t + 4 * g;
+    f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+    f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+    f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
+    f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+#pragma unroll
+    for (int s4 = 0; s4 < X4; ++s4) {
+      const f4 wz = W4[((0 * NT + t) * X4 + s4) * 64 + lane];
+      const f4 wr = W4[((1 * NT + t) * X4 + s4) * 64 + lane];
+      const f4 wh = W4[((2 * NT + t) * X4 + s4) * 64 + lane];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float xb = x[s4][q];
+        az = MFMA(wz[q], xb, az);
+        ar = MFMA(wr[q], xb, ar);
+        ax = MFMA(wh[q], xb, ax);
+      }
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < H4; ++s4) {
+      const f4 wz = U4[((0 * NT + t) * H4 + s4) * 64 + lane];
+      const f4 wr = U4[((1 * NT + t) * H4 + s4) * 64 + lane];
+      const f4 wh = U4[((2 * NT + t) * H4 + s4) * 64 + lane];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float hb = h[s4][q];
+        az = MFMA(wz[q], hb, az);
+        ar = MFMA(wr[q], hb, ar);
+        ah = MFMA(wh[q], hb, ah);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = sig2_(az[r]);
+      const float rr = sig2_(ar[r]);
+      const float c = tanh2_(ax[r] + rr * ah[r]);
+      hn[t][r] = c + z * (h[t][r] - c);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
   }
 }
 
@@ -742,7 +839,7 @@ hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStre
   }
 
 bool gru_shape_supported(int din, int h) {
-  return (din == 16 || din == 32) && (h == 16 || h == 32);
+  return ((din == 16 || din == 32) && (h == 16 || h == 32)) || (din == 64 && h == 64);
 }
 
 hipError_t launch_project(const float* x, int64_t n, const float* Wp, const float* bp, float* out, float* bias_row,
@@ -752,6 +849,7 @@ hipError_t launch_project(const float* x, int64_t n, const float* Wp, const floa
   else if (din == 16 && h == 16) hipLaunchKernelGGL((project_kernel<16, 16>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
   else if (din == 16 && h == 32) hipLaunchKernelGGL((project_kernel<16, 32>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
   else if (din == 32 && h == 16) hipLaunchKernelGGL((project_kernel<32, 16>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
+  else if (din == 64 && h == 64) hipLaunchKernelGGL((project_kernel<64, 64>), grid, block, 0, st, x, n, Wp, bp, out, bias_row);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -792,6 +890,9 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
     } else if (h == 16) {
       auto k = seq_gru2_kernel<16>;
       hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
+    } else if (h == 64) {
+      auto k = seq_gru2_kernel<64>;
+      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
     } else return hipErrorInvalidValue;
     return hipGetLastError();
   }
@@ -817,6 +918,10 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st
   SUM_CASE(16, 32)
   SUM_CASE(32, 16)
 #undef SUM_CASE
+  if (din == 64 && h == 64) {
+    hipLaunchKernelGGL((sum_gru_wide_kernel<64, 64>), grid, dim3(256), 0, st, args);
+    return hipGetLastError();
+  }
   return hipErrorInvalidValue;
 }
 

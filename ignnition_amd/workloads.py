@@ -118,3 +118,14 @@ def reduce_step_stats(dist, elapsed_s: float, edges: int, device=None):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(e, op=dist.ReduceOp.SUM)
     return float(t.item()), int(e.item())
+
+
+def make_synthetic_inputs(n_nodes: int = 1_000_000, hidden: int = 64, iterations: int = 8, graph_id: int = 0,
+                          **kw):
+    """The large synthetic graph: (description, dims, Model_information, [inputs], [labels])."""
+    desc = model_examples.synthetic_graph(hidden=hidden, iterations=iterations)
+    dims = {"node_feature": 1, "target": 1, "entities": 0, "adj_nodes_nodes": 0}
+    mi = Model_information(desc, dims)
+    arr = synthetic.synthetic_graph_arrays(n_nodes=n_nodes, graph_id=graph_id, **kw)
+    label = arr.pop("target")
+    return desc, dims, mi, [arr], [label]

@@ -6,6 +6,8 @@ Fixtures: tests/golden/gen_fixtures.json, produced by tests/golden/make_golden.p
 import json
 
 import numpy as np
+
+import numpy as np
 import pytest
 
 from ignnition_amd import generator as G
@@ -79,3 +81,18 @@ def test_synthetic_layout_matches_migrate():
     assert len(s["traffic"]) == 182 and len(s["link_capacity"]) == n_links == 42
     again = synthetic.routenet_sample("nsfnet", 3)
     assert json.dumps(again) == json.dumps(s)
+
+
+def test_synthetic_large_graph_arrays_match_generator():
+    """The vectorised 1M-node generator emits exactly what the generator (GEN:134-190) makes of
+    the equivalent dict sample (checked on a small instance)."""
+    arr = synthetic.synthetic_graph_arrays(n_nodes=500, window=20, graph_id=3)
+    sample = synthetic.synthetic_sample(arr)
+    data, y = G.sample_to_data(sample, ["node_feature"], "target", [["adj_nodes_nodes", "node", "node", "False"]],
+                               [], [], True)
+    for k in ("src_adj_nodes_nodes", "dst_adj_nodes_nodes", "seq_node_node"):
+        assert data[k] == arr[k].tolist(), k
+    assert data["num_node"] == 500
+    assert y == [float(v) for v in arr["target"]]
+    deg = np.bincount(arr["dst_adj_nodes_nodes"], minlength=500)
+    assert deg.max() <= 30 and abs(deg.mean() - 10) < 1.0

@@ -56,7 +56,7 @@ def test_forward_matches_oracle(kind, topo, n):
     assert b.edges_per_forward == workloads.edges_per_forward(mi, graphs)
 
 
-@pytest.mark.parametrize("hidden", [16, 32])
+@pytest.mark.parametrize("hidden", [16, 32, 64])
 def test_hidden_sizes(hidden):
     desc = model_examples.routenet(hidden=hidden, iterations=3)
     _, dims, _ = workloads.model("routenet")
@@ -194,3 +194,12 @@ def test_large_batch_properties():
         np.testing.assert_array_equal(o1[off[gi]:off[gi + 1]], alone)
     ref = DenseOracle(desc, dims, prm).forward([graphs[5]])
     _close(o1[off[5]:off[6]], ref)
+
+
+def test_synthetic_graph_h64_matches_oracle():
+    """The 1M-node config's model (single entity, sum + 64-unit GRU, 3-layer readout) on a
+    2 000-node instance of the same generator."""
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=2000, iterations=3, window=64)
+    out, ref, b, _ = _run(desc, dims, graphs, seed=4, bias=0.1)
+    _close(out, ref)
+    assert b.edges_per_forward == 3 * len(graphs[0]["src_adj_nodes_nodes"])
