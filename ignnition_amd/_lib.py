@@ -50,7 +50,8 @@ class BatchDesc(C.Structure):
     _fields_ = [("num_graphs", i32), ("num_nodes", C.POINTER(i64)), ("features", C.POINTER(C.POINTER(f32))),
                 ("adj_edges", C.POINTER(i64)), ("adj_src", C.POINTER(C.POINTER(i64))),
                 ("adj_dst", C.POINTER(C.POINTER(i64))), ("adj_seq", C.POINTER(C.POINTER(i64))),
-                ("interleave_len", C.POINTER(i64)), ("interleave_idx", C.POINTER(C.POINTER(i64)))]
+                ("interleave_len", C.POINTER(i64)), ("interleave_idx", C.POINTER(C.POINTER(i64))),
+                ("halo_rows", C.POINTER(i64))]
 
 
 class BatchInfo(C.Structure):
@@ -72,10 +73,23 @@ ACT = {None: 0, "None": 0, "linear": 0, "relu": 1, "selu": 2, "sigmoid": 3, "tan
 SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_create", "ign_plan_destroy",
            "ign_plan_num_params", "ign_plan_num_param_tensors", "ign_plan_param_tensor", "ign_plan_set_params",
            "ign_plan_set_timing", "ign_plan_set_stream", "ign_batch_create", "ign_batch_destroy", "ign_batch_info",
-           "ign_forward", "ign_synchronize", "ign_batch_predictions", "ign_batch_state", "ign_stats"]
+           "ign_forward", "ign_synchronize", "ign_batch_predictions", "ign_batch_state", "ign_stats",
+           "ign_forward_begin", "ign_forward_mp", "ign_forward_end", "ign_batch_mp_split", "ign_batch_bind_state",
+           "ign_batch_state_slot", "ign_gather_rows"]
+
+ABI_VERSION = 2
+PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
 def _load():
+    # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's): whichever loads first
+    # serves the whole process.  Load torch's first so that the engine and torch share one HIP
+    # runtime (streams and device pointers cross between them in partition.py); with /opt/rocm's
+    # loaded first, torch finds no devices.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError("libignmp.so not built: run `python -m ignnition_amd.build` (or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)
@@ -100,6 +114,13 @@ def _load():
         "ign_batch_predictions": (C.c_int, [VP, P(VP)]),
         "ign_batch_state": (C.c_int, [VP, VP, i32, VP]),
         "ign_stats": (C.c_int, [VP, P(Stats)]),
+        "ign_forward_begin": (C.c_int, [VP, VP]),
+        "ign_forward_mp": (C.c_int, [VP, VP, i32, i32]),
+        "ign_forward_end": (C.c_int, [VP, VP, VP]),
+        "ign_batch_mp_split": (C.c_int, [VP, i32, P(i64), P(i64)]),
+        "ign_batch_bind_state": (C.c_int, [VP, VP, i32, VP, VP, i64]),
+        "ign_batch_state_slot": (C.c_int, [VP, i32, P(i32)]),
+        "ign_gather_rows": (C.c_int, [VP, VP, i64, VP, i64, i32, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -109,6 +130,9 @@ def _load():
 
 
 lib = _load()
+if lib.ign_abi_version() != ABI_VERSION:
+    raise ImportError("libignmp.so ABI %d, bindings expect %d: rebuild (python -m ignnition_amd.build)"
+                      % (lib.ign_abi_version(), ABI_VERSION))
 
 
 class EngineError(RuntimeError):

@@ -84,6 +84,7 @@ struct ign_plan {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  bool external_stream = false;   // set by ign_plan_set_stream (may be the null stream)
   int T = 0;
   std::vector<ign_entity_desc> ents;
   int n_adj = 0, n_il = 0;
@@ -109,6 +110,7 @@ struct ign_plan {
   std::vector<hipEvent_t> ev;     // pairs
   std::vector<int> ev_kind;
   std::vector<double> ev_flops, ev_bytes;
+  int ev_slot = 0;                // events recorded since ign_forward_begin
   ign_stats_t stats{};
 };
 
@@ -127,6 +129,7 @@ struct MPB {
   std::vector<int64_t> src_off;   // first table row of each source
   std::vector<int64_t> src_rows;
   int64_t zero_row = 0, n_multi = 0;
+  int64_t n_interior = 0;         // sum MPs: order[0, n_interior) reads no halo row
   int32_t* d_multi_ptr = nullptr;
   uint32_t* d_multi_rows = nullptr;
   double flops = 0, bytes = 0;    // algorithmic, per launch
@@ -137,7 +140,8 @@ struct MPB {
 struct ign_batch {
   ign_plan* plan = nullptr;
   int G = 0;
-  std::vector<int64_t> rows;                    // per entity
+  std::vector<int64_t> rows;                    // per entity (owned rows)
+  std::vector<int64_t> halo;                    // per entity: peer rows after the owned ones (§8e)
   std::vector<std::vector<int64_t>> row_off;    // [entity][graph]
   std::vector<float*> d_feat;                   // per entity [rows][F] or null
   std::vector<float*> d_state[2];               // per entity ping-pong
@@ -171,7 +175,7 @@ int ensure_device(ign_plan* p) {
     HIP_TRY(hipMemset(p->d_params, 0, std::max<int64_t>(p->n_params, 1) * sizeof(float)));
     HIP_TRY(hipMalloc(&p->d_packed, std::max<int64_t>(p->n_packed, 1) * sizeof(float)));
   }
-  if (!p->stream) {
+  if (!p->stream && !p->external_stream) {
     HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->own_stream = true;
   }
@@ -454,6 +458,7 @@ int ign_plan_set_stream(ign_plan* p, void* s) {
     hipStreamDestroy(p->stream);
   }
   p->own_stream = false;
+  p->external_stream = true;
   p->stream = static_cast<hipStream_t>(s);
   return IGN_OK;
 }
@@ -479,8 +484,17 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       b->row_off[e][g + 1] = b->row_off[e][g] + n;
     }
     b->rows[e] = b->row_off[e][G];
-    if (b->rows[e] >= (int64_t)IGN_ROW_MASK) return fail(IGN_ERR_UNSUPPORTED, "entity %d: too many rows", e);
   }
+  b->halo.assign(E, 0);
+  if (d->halo_rows) {
+    for (int e = 0; e < E; ++e) {
+      if (d->halo_rows[e] < 0) return fail(IGN_ERR_INVALID, "entity %d: negative halo_rows", e);
+      b->halo[e] = d->halo_rows[e];
+      if (b->halo[e] && G != 1) return fail(IGN_ERR_INVALID, "halo rows need num_graphs == 1 (one partition)");
+    }
+  }
+  for (int e = 0; e < E; ++e)
+    if (b->rows[e] + b->halo[e] >= (int64_t)IGN_ROW_MASK) return fail(IGN_ERR_UNSUPPORTED, "entity %d: too many rows", e);
   // edge offsets per adjacency
   std::vector<std::vector<int64_t>> eoff(p->n_adj, std::vector<int64_t>(G + 1, 0));
   for (int a = 0; a < p->n_adj; ++a)
@@ -505,8 +519,11 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       std::vector<float> f(d->features[e], d->features[e] + b->rows[e] * F);
       if ((rc = dev_upload(b.get(), &b->d_feat[e], f))) return rc;
     }
-    if ((rc = dev_alloc(b.get(), &b->d_state[0][e], b->rows[e] * H))) return rc;
-    if ((rc = dev_alloc(b.get(), &b->d_state[1][e], b->rows[e] * H))) return rc;
+    const int64_t sr = (b->rows[e] + b->halo[e]) * H;
+    for (int k = 0; k < 2; ++k) {
+      if ((rc = dev_alloc(b.get(), &b->d_state[k][e], sr))) return rc;
+      if (b->halo[e]) HIP_TRY(hipMemset(b->d_state[k][e], 0, sr * sizeof(float)));   // halo defined before use
+    }
   }
 
   // per-MP CSR / step tables
@@ -568,7 +585,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         const int a = mp.src[s].adjacency;
         const int se = mp.src[s].entity;
         const int64_t e0 = eoff[a][g], e1 = eoff[a][g + 1];
-        const int64_t nsrc = b->row_off[se][g + 1] - b->row_off[se][g];
+        const int64_t nsrc = b->row_off[se][g + 1] - b->row_off[se][g] + b->halo[se];   // halo: G == 1
         const int64_t ndst = b->row_off[dst][g + 1] - b->row_off[dst][g];
         for (int64_t k = e0; k < e1; ++k) {
           int64_t si = d->adj_src[a][k], di = d->adj_dst[a][k], sq = d->adj_seq[a][k];
@@ -624,8 +641,9 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       int64_t trow = 0;
       for (int s = 0; s < S; ++s) {
         mb.src_off.push_back(trow);
-        mb.src_rows.push_back(b->rows[mp.src[s].entity]);
-        trow += b->rows[mp.src[s].entity];
+        const int se = mp.src[s].entity;
+        mb.src_rows.push_back(b->rows[se] + b->halo[se]);
+        trow += b->rows[se] + b->halo[se];
       }
       mb.zero_row = trow;
       auto table_row = [&](uint32_t code) -> int64_t {
@@ -684,6 +702,15 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       b->gru_steps += steps * p->T;
     } else {
       sort_order(order, flen, b->row_off[dst], p->graph_major);
+      // edge-cut partitions: destinations reading a halo row go last (they wait for the exchange)
+      std::vector<char> bnd(ND, 0);
+      for (size_t k = 0; k < mdst.size(); ++k) {
+        const uint32_t c = mcode[k];
+        const int se = mp.src[c >> IGN_SLOT_SHIFT].entity;
+        if ((int64_t)(c & IGN_ROW_MASK) >= b->rows[se]) bnd[mdst[k]] = 1;
+      }
+      std::stable_partition(order.begin(), order.end(), [&](int32_t r) { return !bnd[r]; });
+      mb.n_interior = std::count(bnd.begin(), bnd.end(), 0);
       std::vector<int32_t> where(ND);
       for (int64_t i = 0; i < ND; ++i) where[order[i]] = (int32_t)i;
       std::vector<int32_t> ptr(ND + 1, 0);
@@ -757,9 +784,9 @@ namespace {
 
 struct Timer {
   ign_plan* p;
-  int slot = 0;
   void begin(int kind, double flops, double bytes) {
     if (!p->timing) return;
+    const int slot = p->ev_slot;
     size_t need = 2 * (slot + 1);
     while (p->ev.size() < need) {
       hipEvent_t e;
@@ -778,77 +805,101 @@ struct Timer {
   }
   void end() {
     if (!p->timing) return;
-    hipEventRecord(p->ev[2 * slot + 1], p->stream);
-    ++slot;
+    hipEventRecord(p->ev[2 * p->ev_slot + 1], p->stream);
+    ++p->ev_slot;
   }
 };
 
-}  // namespace
-
-int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
+int check_pb(ign_plan* p, ign_batch* b) {
   if (!p || !b) return fail(IGN_ERR_INVALID, "null argument");
   if (b->plan != p) return fail(IGN_ERR_INVALID, "batch was created for another plan");
   if (!p->params_set) return fail(IGN_ERR_INVALID, "parameters not set (ign_plan_set_params)");
-  int rc = set_device(p->device);
-  if (rc) return rc;
-  hipStream_t st = p->stream;
-  Timer tm{p};
-  const int E = (int)p->ents.size();
+  return set_device(p->device);
+}
 
-  for (int e = 0; e < E; ++e) {   // GM:396-400
+}  // namespace
+
+int ign_forward_begin(ign_plan* p, ign_batch* b) {
+  int rc = check_pb(p, b);
+  if (rc) return rc;
+  p->ev_slot = 0;
+  Timer tm{p};
+  for (int e = 0; e < (int)p->ents.size(); ++e) {   // GM:396-400 (owned rows; halo rows come from peers)
     const int H = p->ents[e].hidden_dim, F = p->ents[e].feature_total;
     tm.begin(K_INIT, 0, (double)b->rows[e] * (4.0 * F + 4.0 * H));
-    HIP_TRY(launch_init_state(b->d_state[0][e], b->d_feat[e], b->rows[e], H, F, st));
+    HIP_TRY(launch_init_state(b->d_state[0][e], b->d_feat[e], b->rows[e], H, F, p->stream));
     tm.end();
     b->cur[e] = 0;
   }
-  for (int it = 0; it < p->T; ++it) {              // GM:406
-    for (size_t mi = 0; mi < p->mps.size(); ++mi) { // GM:410-414 (stages flattened in order)
-      const MPP& mp = p->mps[mi];
-      const MPB& mb = b->mp[mi];
-      const CellP& cp = p->cells[mp.cell];
-      SrcBases sbases{};
-      for (size_t s = 0; s < mp.src.size(); ++s) {
-        int se = mp.src[s].entity;
-        sbases.base[s] = b->d_state[b->cur[se]][se];
-      }
-      const int dst = mp.dst;
-      const float* hin = b->d_state[b->cur[dst]][dst];
-      float* hout = b->d_state[1 - b->cur[dst]][dst];
-      if (mp.sorted) {
-        const int W3 = 3 * cp.H;
-        for (size_t s = 0; s < mp.src.size(); ++s) {
-          const int64_t rs = mb.src_rows[s];
-          tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3));
-          HIP_TRY(launch_project(sbases.base[s], rs, p->d_packed + cp.pk_w, p->d_packed + cp.pk_b,
-                                 mb.d_table + mb.src_off[s] * W3, s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr,
-                                 mp.din, cp.H, st));
-          tm.end();
-        }
-        if (mb.n_multi) {
-          tm.begin(K_OTHER, 0, 0);
-          HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3,
-                                   mb.d_table + mb.zero_row * W3, st));
-          tm.end();
-        }
-        if (cp.H == 64 && p->seq_variant != 2)
-          return fail(IGN_ERR_UNSUPPORTED, "64-unit ordered updates need the LDS variant (IGN_SEQ_VARIANT=2)");
-        SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
-                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
-                     mb.n_steps};
-        tm.begin(K_SEQ, mb.flops, mb.bytes);
-        HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
-        tm.end();
-      } else {
-        SumGruArgs a{hin, hout, sbases, mb.d_order, mb.d_msg_ptr, mb.d_msg_src,
-                     p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
-        tm.begin(K_SUM, mb.flops, mb.bytes);
-        HIP_TRY(launch_sum_gru(a, mp.din, cp.H, st));
-        tm.end();
-      }
-      b->cur[dst] ^= 1;   // GM:602: the destination state is overwritten
+  return IGN_OK;
+}
+
+int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
+  int rc = check_pb(p, b);
+  if (rc) return rc;
+  if (mi < 0 || mi >= (int)p->mps.size()) return fail(IGN_ERR_INVALID, "mp index %d out of range", mi);
+  if (part < IGN_PART_ALL || part > IGN_PART_BOUNDARY) return fail(IGN_ERR_INVALID, "part %d", part);
+  hipStream_t st = p->stream;
+  Timer tm{p};
+  const MPP& mp = p->mps[mi];
+  const MPB& mb = b->mp[mi];
+  const CellP& cp = p->cells[mp.cell];
+  SrcBases sbases{};
+  for (size_t s = 0; s < mp.src.size(); ++s) {
+    int se = mp.src[s].entity;
+    sbases.base[s] = b->d_state[b->cur[se]][se];
+  }
+  const int dst = mp.dst;
+  const float* hin = b->d_state[b->cur[dst]][dst];
+  float* hout = b->d_state[1 - b->cur[dst]][dst];
+  if (mp.sorted) {
+    if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split is for sum MPs only");
+    const int W3 = 3 * cp.H;
+    for (size_t s = 0; s < mp.src.size(); ++s) {
+      const int64_t rs = mb.src_rows[s];
+      tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3));
+      HIP_TRY(launch_project(sbases.base[s], rs, p->d_packed + cp.pk_w, p->d_packed + cp.pk_b,
+                             mb.d_table + mb.src_off[s] * W3, s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr,
+                             mp.din, cp.H, st));
+      tm.end();
+    }
+    if (mb.n_multi) {
+      tm.begin(K_OTHER, 0, 0);
+      HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3,
+                               mb.d_table + mb.zero_row * W3, st));
+      tm.end();
+    }
+    if (cp.H == 64 && p->seq_variant != 2)
+      return fail(IGN_ERR_UNSUPPORTED, "64-unit ordered updates need the LDS variant (IGN_SEQ_VARIANT=2)");
+    SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
+                 p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
+                 mb.n_steps};
+    tm.begin(K_SEQ, mb.flops, mb.bytes);
+    HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
+    tm.end();
+  } else {
+    // destinations [first, first + count) of the order array
+    const int64_t first = part == IGN_PART_BOUNDARY ? mb.n_interior : 0;
+    const int64_t count = part == IGN_PART_INTERIOR ? mb.n_interior
+                        : part == IGN_PART_BOUNDARY ? mb.n_dst - mb.n_interior : mb.n_dst;
+    if (count > 0) {
+      SumGruArgs a{hin, hout, sbases, mb.d_order + first, mb.d_msg_ptr + first, mb.d_msg_src,
+                   p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count, p->xcd_remap};
+      const double frac = mb.n_dst ? (double)count / mb.n_dst : 0.0;
+      tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac);
+      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, st));
+      tm.end();
     }
   }
+  if (part != IGN_PART_INTERIOR) b->cur[dst] ^= 1;   // GM:602: the destination state is overwritten
+  return IGN_OK;
+}
+
+int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = check_pb(p, b);
+  if (rc) return rc;
+  hipStream_t st = p->stream;
+  Timer tm{p};
   // readout (GM:611-629)
   const int64_t P = b->n_pred;
   const float* x = b->d_state[b->cur[p->ro_in[0]]][p->ro_in[0]];
@@ -869,8 +920,6 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
                    p->d_packed + l2.pk_w, l2.use_bias ? prm + l2.off_b : nullptr,
                    prm + l3.off_w, l3.use_bias ? prm + l3.off_b : nullptr,
                    l1.act, l2.act, l3.act, b->d_pred};
-    // a null bias pointer means "no bias": point at a zero region instead for the fused kernel
-    static_assert(sizeof(Readout3Args) > 0, "");
     if (!a.b1 || !a.b2) return fail(IGN_ERR_UNSUPPORTED, "fused readout requires use_bias on hidden layers");
     double flops = 2.0 * P * ((double)l1.in * l1.out + (double)l2.in * l2.out + l3.in);
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0));
@@ -898,7 +947,7 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
     HIP_TRY(hipStreamSynchronize(st));
     ign_stats_t& s = p->stats;
     s.kinds = K_KINDS;
-    for (int i = 0; i < tm.slot; ++i) {
+    for (int i = 0; i < p->ev_slot; ++i) {
       float ms = 0;
       hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]);
       int k = p->ev_kind[i];
@@ -908,6 +957,58 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
       s.bytes[k] += p->ev_bytes[i];
     }
   }
+  p->ev_slot = 0;
+  return IGN_OK;
+}
+
+int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = ign_forward_begin(p, b);
+  if (rc) return rc;
+  for (int it = 0; it < p->T; ++it)                     // GM:406
+    for (int mi = 0; mi < (int)p->mps.size(); ++mi)     // GM:410-414 (stages flattened in order)
+      if ((rc = ign_forward_mp(p, b, mi, IGN_PART_ALL))) return rc;
+  return ign_forward_end(p, b, pred_out);
+}
+
+int ign_batch_mp_split(const ign_batch* b, int32_t mi, int64_t* interior, int64_t* boundary) {
+  if (!b || !interior || !boundary) return fail(IGN_ERR_INVALID, "null argument");
+  if (mi < 0 || mi >= (int)b->mp.size()) return fail(IGN_ERR_INVALID, "mp index %d out of range", mi);
+  const MPB& mb = b->mp[mi];
+  *interior = mb.sorted ? mb.n_dst : mb.n_interior;
+  *boundary = mb.n_dst - *interior;
+  return IGN_OK;
+}
+
+int ign_batch_bind_state(ign_plan* p, ign_batch* b, int32_t e, float* dev0, float* dev1, int64_t capacity) {
+  if (!p || !b || !dev0 || !dev1) return fail(IGN_ERR_INVALID, "null argument");
+  if (b->plan != p) return fail(IGN_ERR_INVALID, "batch was created for another plan");
+  if (e < 0 || e >= (int)p->ents.size()) return fail(IGN_ERR_INVALID, "entity index");
+  const int64_t need = (b->rows[e] + b->halo[e]) * p->ents[e].hidden_dim + 256;
+  if (capacity < need) return fail(IGN_ERR_INVALID, "state buffers hold %lld floats, need %lld",
+                                   (long long)capacity, (long long)need);
+  if ((reinterpret_cast<uintptr_t>(dev0) | reinterpret_cast<uintptr_t>(dev1)) & 15)
+    return fail(IGN_ERR_INVALID, "state buffers must be 16-byte aligned");
+  b->d_state[0][e] = dev0;
+  b->d_state[1][e] = dev1;
+  b->cur[e] = 0;
+  return IGN_OK;
+}
+
+int ign_batch_state_slot(const ign_batch* b, int32_t e, int32_t* slot) {
+  if (!b || !slot) return fail(IGN_ERR_INVALID, "null argument");
+  if (e < 0 || e >= (int)b->cur.size()) return fail(IGN_ERR_INVALID, "entity index");
+  *slot = b->cur[e];
+  return IGN_OK;
+}
+
+int ign_gather_rows(ign_plan* p, const float* src, int64_t ld, const int32_t* idx, int64_t n, int32_t cols,
+                    float* dst) {
+  if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  if (n < 0 || cols <= 0 || cols % 4 || ld < cols || ld % 4) return fail(IGN_ERR_INVALID, "gather_rows shape");
+  if (n && (!src || !idx || !dst)) return fail(IGN_ERR_INVALID, "null argument");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  HIP_TRY(launch_gather_rows(src, ld, idx, n, cols, dst, p->stream));
   return IGN_OK;
 }
 

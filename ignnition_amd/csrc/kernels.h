@@ -72,3 +72,5 @@ hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride,
                                 int out, int act, float* y, hipStream_t st);
 hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,
                               hipStream_t st);
+hipError_t launch_gather_rows(const float* src, int64_t ld, const int32_t* idx, int64_t n, int cols, float* dst,
+                              hipStream_t st);

@@ -809,6 +809,20 @@ __global__ void concat_cols_kernel(float* __restrict__ dst, int64_t n, int dst_s
   }
 }
 
+// Halo pack: dst[i] = src[idx[i]] for rows of `cols` floats.  One float4 per lane,
+// consecutive lanes walk one row, so each gathered row is a coalesced 16*cols/4-byte read.
+__global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ld, const int32_t* __restrict__ idx,
+                                   int64_t n, int cols, float* __restrict__ dst) {
+  const int q = cols >> 2;                      // float4 per row
+  const int64_t total = n * q;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / q;
+    const int c = (int)(i - r * q);
+    const float4 v = reinterpret_cast<const float4*>(src + (int64_t)idx[r] * ld)[c];
+    reinterpret_cast<float4*>(dst + r * cols)[c] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Host-side launchers
 static inline int grid_for(int64_t n, int per_block) { return (int)((n + per_block - 1) / per_block); }
@@ -965,5 +979,14 @@ hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, c
   int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(concat_cols_kernel, dim3(blocks), dim3(256), 0, st, dst, n, dst_stride, col0, src, width);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const float* src, int64_t ld, const int32_t* idx, int64_t n, int cols, float* dst,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t total = n * (cols / 4);
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, st, src, ld, idx, n, cols, dst);
   return hipGetLastError();
 }

@@ -255,6 +255,17 @@ class Engine:
     def synchronize(self):
         check(lib.ign_synchronize(self.handle))
 
+    def set_stream(self, hip_stream: int):
+        """Run on an external HIP stream (e.g. ``torch.cuda.current_stream().cuda_stream``)."""
+        check(lib.ign_plan_set_stream(self.handle, C.c_void_p(hip_stream)))
+
+    def gather_rows(self, src, idx, dst):
+        """dst[i] = src[idx[i]] (device tensors: src [R, C] fp32, idx [n] int32, dst [n, C])."""
+        n = idx.numel()
+        cols = src.shape[1]
+        check(lib.ign_gather_rows(self.handle, C.c_void_p(src.data_ptr()), src.stride(0), C.c_void_p(idx.data_ptr()),
+                                  n, cols, C.c_void_p(dst.data_ptr())))
+
     def close(self):
         h = getattr(self, "handle", None)
         if h:
@@ -275,7 +286,8 @@ class Batch:
     ``graphs``: list of feature dicts with the input_fn keys (GM:127-158), features already
     normalised.  Graph-local indices are kept; the engine offsets them per graph."""
 
-    def __init__(self, engine: Engine, graphs: list):
+    def __init__(self, engine: Engine, graphs: list, halo_rows: dict = None):
+        """``halo_rows``: {entity: extra rows} for one edge-cut partition (see partition.py)."""
         p = engine.plan
         self.engine = engine
         G = len(graphs)
@@ -319,8 +331,13 @@ class Batch:
         lp = C.POINTER(C.c_int64)
         feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
         mk = lambda arrs: (lp * max(len(arrs), 1))(*[a.ctypes.data_as(lp) for a in arrs])
+        halo = None
+        if halo_rows:
+            halo = np.array([int(halo_rows.get(name, 0)) for name in p.entities], np.int64)
+        self.halo = [0] * E if halo is None else [int(v) for v in halo]
         desc = _lib.BatchDesc(G, num.ctypes.data_as(lp), feat_ptrs, cnt.ctypes.data_as(lp), mk(srcs), mk(dsts),
-                              mk(seqs), il_len.ctypes.data_as(lp), mk(ils))
+                              mk(seqs), il_len.ctypes.data_as(lp), mk(ils),
+                              halo.ctypes.data_as(lp) if halo is not None else lp())
         h = C.c_void_p()
         check(lib.ign_batch_create(engine.handle, C.byref(desc), C.byref(h)))
         self.handle = h
@@ -335,6 +352,39 @@ class Batch:
         self.rows = list(info.rows)[:E]
         self.graph_rows = num
         self._arrays = None  # the engine copied what it needs
+        self._bound = {}
+
+    # ---- stepped forward (edge-cut partitions) -----------------------------------
+    def begin(self):
+        check(lib.ign_forward_begin(self.engine.handle, self.handle))
+
+    def run_mp(self, mp: int, part: str = "all"):
+        check(lib.ign_forward_mp(self.engine.handle, self.handle, mp, _lib.PART[part]))
+
+    def end(self, to_host: bool = True):
+        out = np.empty((self.predictions, self.output_units), np.float32) if to_host else None
+        check(lib.ign_forward_end(self.engine.handle, self.handle,
+                                  out.ctypes.data_as(C.c_void_p) if to_host else None))
+        return out
+
+    def mp_split(self, mp: int):
+        """(interior, boundary) destination counts of MP ``mp``."""
+        a, b = C.c_int64(), C.c_int64()
+        check(lib.ign_batch_mp_split(self.handle, mp, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def bind_state(self, entity: str, buf0, buf1):
+        """Use two caller-owned device buffers (torch tensors) as the entity's state buffers."""
+        e = self.engine.plan.entities.index(entity)
+        cap = min(buf0.numel(), buf1.numel())
+        check(lib.ign_batch_bind_state(self.engine.handle, self.handle, e, C.c_void_p(buf0.data_ptr()),
+                                       C.c_void_p(buf1.data_ptr()), cap))
+        self._bound[entity] = (buf0, buf1)
+
+    def state_slot(self, entity: str) -> int:
+        s = C.c_int32()
+        check(lib.ign_batch_state_slot(self.handle, self.engine.plan.entities.index(entity), C.byref(s)))
+        return s.value
 
     def forward(self, to_host: bool = True):
         eng = self.engine

@@ -1,0 +1,285 @@
+"""Edge-cut partitioning of one large graph across GPUs, with halo exchange.
+
+The reference runs every graph whole on one device (``model_fn``'s per-graph loop, GM:712-724);
+a graph that outgrows one GPU (the 1M-node / 10M-edge synthetic config, BASELINE configs[4])
+is split here instead:
+
+* **Partition**: contiguous id ranges per entity (``node_ranges``), owner computes by
+  destination. A partition keeps every in-edge of its owned destinations (edge-cut), so each
+  destination's messages and their summation order are the same as in the unpartitioned graph.
+* **Halo**: the distinct remote source rows a partition reads. They are stored after the owned
+  rows in the entity's state buffer, grouped by owner rank, ascending id. The engine gets them
+  through ``ign_batch_desc.halo_rows``.
+* **Requests**: each partition sends every owner the ids it needs, once at setup, with one
+  all-to-all. The reply lists become the owner's send lists. No rank needs the global graph.
+* **Exchange**: before an MP reads an entity whose halo is stale, each rank packs its send rows
+  with ``ign_gather_rows`` (HIP). One ``all_to_all_single`` (RCCL over xGMI) then delivers them
+  straight into the halo rows of the peer's current state buffer. There is no unpack copy.
+* **Overlap**: destinations that read no halo row (``IGN_PART_INTERIOR``) run while the exchange
+  is in flight. The boundary destinations run after it completes.
+
+Only ``sum`` MPs are partitioned. ``ordered`` / ``interleave`` pad per graph (GM:477-543), so
+splitting a graph would change the reference's slot layout; those models shard by graph
+(workloads.shard_graph_ids).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .engine import Batch, Engine, MPPlan
+
+
+def node_ranges(n: int, world: int) -> np.ndarray:
+    """Contiguous balanced id ranges: rank r owns [b[r], b[r+1])."""
+    return np.array([(n * r) // world for r in range(world + 1)], np.int64)
+
+
+@dataclass
+class HaloPlan:
+    entity: str
+    n_owned: int
+    halo_ids: np.ndarray        # global ids of the halo rows (ascending, hence grouped by owner)
+    recv_counts: list           # halo rows received from each rank
+    send_rows: np.ndarray       # local owned rows sent, grouped by destination rank (int32)
+    send_counts: list
+
+    @property
+    def n_halo(self) -> int:
+        return int(len(self.halo_ids))
+
+
+@dataclass
+class LocalPart:
+    rank: int
+    inputs: dict                # input_fn dict of the partition (local ids; halo rows after owned rows)
+    ranges: dict                # entity -> node_ranges
+    needs: dict                 # entity -> [ids needed from each rank]
+    halos: dict = None          # entity -> HaloPlan (after exchange_requests)
+
+
+def _check_plan(plan: MPPlan):
+    for m in plan.mps:
+        if m["aggr"] != "sum":
+            raise ValueError("edge-cut partitioning supports sum MPs only (ordered/interleave pad per graph, "
+                             "GM:477-543); shard such batches by graph")
+
+
+def local_part(inputs: dict, plan: MPPlan, rank: int, world: int) -> LocalPart:
+    """The partition of ``rank`` from a graph's input_fn dict (global ids)."""
+    _check_plan(plan)
+    ranges = {}
+    for name in plan.entities:
+        ranges[name] = node_ranges(int(np.asarray(inputs["num_" + name]).reshape(())), world)
+    out = {}
+    for e, name in enumerate(plan.entities):
+        lo, hi = ranges[name][rank], ranges[name][rank + 1]
+        out["num_" + name] = np.int64(hi - lo)
+        n = int(np.asarray(inputs["num_" + name]).reshape(()))
+        for fname, size in plan.features[e]:
+            rows = np.asarray(inputs[fname]).reshape(n, size)[lo:hi]
+            out[fname] = rows.reshape(-1) if size == 1 else rows
+    # remote source ids per source entity
+    remote = {name: [] for name in plan.entities}
+    kept = []
+    for slot in plan.adj_slots:
+        ks, kd, kq = slot.keys
+        s = np.asarray(inputs[ks], np.int64).reshape(-1)
+        d = np.asarray(inputs[kd], np.int64).reshape(-1)
+        q = np.asarray(inputs[kq], np.int64).reshape(-1)
+        dlo, dhi = ranges[slot.dst][rank], ranges[slot.dst][rank + 1]
+        keep = (d >= dlo) & (d < dhi)            # owner computes: every in-edge of an owned destination
+        s, d, q = s[keep], d[keep] - dlo, q[keep]
+        slo, shi = ranges[slot.src][rank], ranges[slot.src][rank + 1]
+        rem = (s < slo) | (s >= shi)
+        remote[slot.src].append(s[rem])
+        kept.append((slot, s, d, q, rem))
+    halo_ids = {name: np.unique(np.concatenate(remote[name])) if remote[name] else np.zeros(0, np.int64)
+                for name in plan.entities}
+    for slot, s, d, q, rem in kept:
+        ks, kd, kq = slot.keys
+        slo, shi = ranges[slot.src][rank], ranges[slot.src][rank + 1]
+        ls = s - slo
+        ls[rem] = (shi - slo) + np.searchsorted(halo_ids[slot.src], s[rem])
+        out[ks], out[kd], out[kq] = ls, d, q
+    needs = {}
+    for name in plan.entities:
+        owner = np.searchsorted(ranges[name], halo_ids[name], side="right") - 1
+        needs[name] = [halo_ids[name][owner == p] for p in range(world)]
+    part = LocalPart(rank, out, ranges, needs)
+    part.halos = {name: HaloPlan(name, int(ranges[name][rank + 1] - ranges[name][rank]), halo_ids[name],
+                                 [len(x) for x in needs[name]], None, None) for name in plan.entities}
+    return part
+
+
+def exchange_requests(parts: list, comm) -> None:
+    """Setup all-to-all: each owner learns which of its rows every peer reads (fills send lists)."""
+    names = list(parts[0].needs)
+    for name in names:
+        got = comm.alltoall_ids([p.needs[name] for p in parts])
+        for p, g in zip(parts, got):
+            lo = p.ranges[name][p.rank]
+            h = p.halos[name]
+            h.send_rows = (np.concatenate(g) - lo).astype(np.int32) if g else np.zeros(0, np.int32)
+            h.send_counts = [len(x) for x in g]
+            if len(h.send_rows) and (h.send_rows.min() < 0 or h.send_rows.max() >= h.n_owned):
+                raise RuntimeError("halo request for a row this rank does not own")
+
+
+# ---------------------------------------------------------------------------------------------
+# Transports.  Both move a list of partitions' packed rows; TorchComm holds exactly one partition
+# (one process per GPU), LoopbackComm all of them (tests on one device).
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class TorchComm:
+    """torch.distributed all-to-all: RCCL ('nccl' backend) over xGMI on GPUs, gloo on CPU."""
+
+    def __init__(self, dist, device=None, group=None, host_staged: bool = False):
+        """``host_staged``: device rows go through host memory (gloo rehearsal of the N>1 path
+        with several ranks on one GPU, where RCCL refuses duplicate devices)."""
+        self.dist, self.device, self.group, self.host_staged = dist, device, group, host_staged
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+
+    def alltoall_ids(self, sends: list) -> list:
+        import torch
+        (send,) = sends
+        cnt = torch.tensor([len(x) for x in send], dtype=torch.int64, device=self.device)
+        rcnt = torch.empty_like(cnt)
+        self.dist.all_to_all_single(rcnt, cnt, group=self.group)
+        flat = np.concatenate(send).astype(np.int64) if send else np.zeros(0, np.int64)
+        sbuf = torch.from_numpy(flat).to(self.device)
+        rc = rcnt.cpu().tolist()
+        rbuf = torch.empty(sum(rc), dtype=torch.int64, device=self.device)
+        self.dist.all_to_all_single(rbuf, sbuf, rc, cnt.cpu().tolist(), group=self.group)
+        r = rbuf.cpu().numpy()
+        offs = np.cumsum([0] + rc)
+        return [[r[offs[i]:offs[i + 1]] for i in range(self.world)]]
+
+    def exchange(self, sends: list, send_counts: list, recvs: list, recv_counts: list, async_op: bool):
+        (send,), (sc,), (recv,), (rc,) = sends, send_counts, recvs, recv_counts
+        if self.host_staged:
+            hrecv = recv.new_empty(recv.shape, device="cpu")
+            self.dist.all_to_all_single(hrecv, send.cpu(), rc, sc, group=self.group)
+            recv.copy_(hrecv)
+            return _Done()
+        w = self.dist.all_to_all_single(recv, send, rc, sc, group=self.group, async_op=async_op)
+        return w if async_op else _Done()
+
+
+class LoopbackComm:
+    """All partitions in one process (single-device tests): the all-to-all as copies."""
+
+    def __init__(self, world: int):
+        self.rank, self.world = 0, world
+
+    def alltoall_ids(self, sends: list) -> list:
+        return [[sends[src][dst] for src in range(self.world)] for dst in range(self.world)]
+
+    def exchange(self, sends, send_counts, recvs, recv_counts, async_op):
+        W = self.world
+        soff = [np.cumsum([0] + list(c)) for c in send_counts]
+        roff = [np.cumsum([0] + list(c)) for c in recv_counts]
+        for src in range(W):
+            for dst in range(W):
+                n = send_counts[src][dst]
+                if n != recv_counts[dst][src]:
+                    raise RuntimeError("halo count mismatch %d->%d" % (src, dst))
+                if n:
+                    recvs[dst][roff[dst][src]:roff[dst][src] + n].copy_(sends[src][soff[src][dst]:soff[src][dst] + n])
+        return _Done()
+
+
+# ---------------------------------------------------------------------------------------------
+class EdgeCutForward:
+    """Forward of a partitioned graph through the stepped C ABI.
+
+    ``parts``: the LocalParts this process runs (one per process with TorchComm).  All of them
+    share ``engine`` (one plan per device) and the torch current stream, which the engine is
+    bound to so that packing, RCCL and the MP kernels are stream-ordered."""
+
+    def __init__(self, engine: Engine, parts: list, comm, overlap: bool = True):
+        import torch
+        self.torch = torch
+        self.engine, self.parts, self.comm, self.overlap = engine, parts, comm, overlap
+        plan = engine.plan
+        self.plan = plan
+        engine.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.batches, self.bufs, self.send_idx, self.send_buf = [], [], [], []
+        # every rank must call the same collectives: the exchanged entities are those read as a source
+        srcs = {s.src for s in plan.adj_slots}
+        halo_ents = [n for n in plan.entities if n in srcs] if comm.world > 1 else []
+        self.halo_ents = halo_ents
+        dev = torch.device("cuda", torch.cuda.current_device())
+        for p in parts:
+            b = Batch(engine, [p.inputs], halo_rows={n: p.halos[n].n_halo for n in plan.entities})
+            bufs, sidx, sbuf = {}, {}, {}
+            for n in halo_ents:
+                e = plan.entities.index(n)
+                H = plan.hidden[e]
+                h = p.halos[n]
+                cap = (h.n_owned + h.n_halo) * H + 256
+                pair = (torch.empty(cap, dtype=torch.float32, device=dev), torch.empty(cap, dtype=torch.float32, device=dev))
+                for t in pair:
+                    t.zero_()
+                b.bind_state(n, *pair)
+                bufs[n] = pair
+                sidx[n] = torch.from_numpy(np.ascontiguousarray(h.send_rows, np.int32)).to(dev)
+                sbuf[n] = torch.empty((len(h.send_rows), H), dtype=torch.float32, device=dev)
+            self.batches.append(b)
+            self.bufs.append(bufs)
+            self.send_idx.append(sidx)
+            self.send_buf.append(sbuf)
+        self.edges_per_forward = sum(b.edges_per_forward for b in self.batches)
+        self.mp_sources = [sorted({plan.entities[s[0]] for s in m["sources"]}) for m in plan.mps]
+
+    def _exchange(self, name, async_op):
+        e = self.plan.entities.index(name)
+        H = self.plan.hidden[e]
+        sends, recvs, sc, rc = [], [], [], []
+        for i, p in enumerate(self.parts):
+            h = p.halos[name]
+            cur = self.bufs[i][name][self.batches[i].state_slot(name)]
+            state = cur[:(h.n_owned + h.n_halo) * H].view(h.n_owned + h.n_halo, H)
+            if len(h.send_rows):
+                self.engine.gather_rows(state, self.send_idx[i][name], self.send_buf[i][name])
+            sends.append(self.send_buf[i][name])
+            recvs.append(state[h.n_owned:])
+            sc.append(h.send_counts)
+            rc.append(h.recv_counts)
+        return self.comm.exchange(sends, sc, recvs, rc, async_op)
+
+    def forward(self, to_host: bool = True):
+        for b in self.batches:
+            b.begin()
+        stale = set(self.halo_ents)                # halo rows of the initial state come from peers too
+        for _ in range(self.plan.iterations):      # GM:406
+            for mi, m in enumerate(self.plan.mps):
+                need = [n for n in self.mp_sources[mi] if n in stale]
+                if need and self.overlap:
+                    works = [self._exchange(n, True) for n in need]
+                    for b in self.batches:
+                        b.run_mp(mi, "interior")
+                    for w in works:
+                        w.wait()
+                    for b in self.batches:
+                        b.run_mp(mi, "boundary")
+                else:
+                    for n in need:
+                        self._exchange(n, False).wait()
+                    for b in self.batches:
+                        b.run_mp(mi, "all")
+                stale -= set(need)
+                dst = self.plan.entities[m["dst"]]
+                if dst in self.halo_ents:
+                    stale.add(dst)                 # the new buffer's halo rows are two updates old
+        return [b.end(to_host) for b in self.batches]
+
+    def close(self):
+        for b in self.batches:
+            b.close()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 1
+#define IGN_ABI_VERSION 2
 
 enum ign_status {
   IGN_OK = 0,
@@ -129,6 +129,12 @@ typedef struct {
   const int64_t* const* adj_seq;   /* seq_<srcEnt>_<dstEnt> */
   const int64_t* interleave_len;   /* [num_graphs][num_interleave] */
   const int64_t* const* interleave_idx; /* [num_interleave] -> graph-concatenated indices_<src>_to_<dst> */
+  /* Edge-cut partitions (num_graphs must be 1 when used): per entity, extra state rows
+   * after the owned num_<entity> rows that hold peers' hidden states.  Sources may address them
+   * (src index in [num, num + halo)); destinations, features and the readout cover owned rows only.
+   * The caller fills them (ign_batch_bind_state + its own collective) before an MP reads them.
+   * NULL = no halo. */
+  const int64_t* halo_rows;        /* [num_entities] or NULL */
 } ign_batch_desc;
 
 typedef struct {
@@ -179,6 +185,28 @@ int  ign_batch_predictions(ign_batch* batch, const float** dev_ptr);
 /* Copy the current hidden state of an entity (after ign_forward) to host [rows][H]. */
 int  ign_batch_state(ign_plan* plan, ign_batch* batch, int32_t entity, float* host_out);
 int  ign_stats(const ign_plan* plan, ign_stats_t* out);
+
+/* ---- Stepped forward, for edge-cut partitions exchanging halo rows between MPs ----
+ * ign_forward == ign_forward_begin; for it < T: for mp: ign_forward_mp(mp, IGN_PART_ALL);
+ * ign_forward_end.  A sum MP can run as two launches, IGN_PART_INTERIOR (destinations none of
+ * whose messages come from halo rows; may overlap the halo exchange) then IGN_PART_BOUNDARY;
+ * the destination state flips to the new buffer after IGN_PART_ALL or IGN_PART_BOUNDARY.  */
+enum ign_part { IGN_PART_ALL = 0, IGN_PART_INTERIOR = 1, IGN_PART_BOUNDARY = 2 };
+int  ign_forward_begin(ign_plan* plan, ign_batch* batch);
+int  ign_forward_mp(ign_plan* plan, ign_batch* batch, int32_t mp, int32_t part);
+int  ign_forward_end(ign_plan* plan, ign_batch* batch, float* pred_out);
+/* Destinations of MP `mp` in the interior / boundary launch (all destinations are interior
+ * without halo rows). */
+int  ign_batch_mp_split(const ign_batch* batch, int32_t mp, int64_t* interior, int64_t* boundary);
+/* Replace an entity's two state buffers by caller-owned device memory, each at least
+ * (rows + halo) * hidden_dim + 256 floats, 16-byte aligned.  State contents are not copied. */
+int  ign_batch_bind_state(ign_plan* plan, ign_batch* batch, int32_t entity, float* dev0, float* dev1,
+                          int64_t capacity_floats);
+/* Which of the two state buffers (0/1) holds the entity's current state. */
+int  ign_batch_state_slot(const ign_batch* batch, int32_t entity, int32_t* slot);
+/* dst[i][:] = src[idx[i]][:] on the plan stream (halo pack); cols % 4 == 0, device pointers. */
+int  ign_gather_rows(ign_plan* plan, const float* src, int64_t ld, const int32_t* idx, int64_t n, int32_t cols,
+                     float* dst);
 
 #ifdef __cplusplus
 }

@@ -57,3 +57,113 @@ def test_shard_bounds():
     assert workloads.shard_graph_ids(1, 4, 512) == list(range(512, 1024))
     with pytest.raises(ValueError):
         workloads.shard_graph_ids(4, 4, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# Edge-cut partitions of one graph: partition + request all-to-all + halo exchange.
+import numpy as np
+
+from ignnition_amd import partition
+from ignnition_amd.engine import MPPlan
+
+N_SMALL = 3000
+
+
+def _synthetic_plan_and_inputs(n=N_SMALL):
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=n, iterations=2, window=64)
+    return MPPlan.from_model_info(mi), graphs[0]
+
+
+def _state_value(gid, H):
+    """Row content a rank holds for global node id gid: distinct per id and column."""
+    return np.asarray(gid, np.float32)[..., None] * 100.0 + np.arange(H, dtype=np.float32)
+
+
+def _check_halo_exchange(parts, comm, H=8):
+    partition.exchange_requests(parts, comm)
+    sends, recvs, sc, rc, states = [], [], [], [], []
+    for p in parts:
+        h = p.halos["node"]
+        lo = p.ranges["node"][p.rank]
+        state = torch.zeros((h.n_owned + h.n_halo, H))
+        state[:h.n_owned] = torch.from_numpy(_state_value(np.arange(lo, lo + h.n_owned), H))
+        sends.append(state[torch.from_numpy(h.send_rows.astype(np.int64))])
+        recvs.append(state[h.n_owned:])
+        sc.append(h.send_counts)
+        rc.append(h.recv_counts)
+        states.append(state)
+    comm.exchange(sends, sc, recvs, rc, async_op=False).wait()
+    for p, state in zip(parts, states):
+        h = p.halos["node"]
+        np.testing.assert_array_equal(state[h.n_owned:].numpy(), _state_value(h.halo_ids, H))
+    return states
+
+
+def _check_partition_edges(parts, x):
+    """The partitions' in-edges, mapped back to global ids, are the whole graph, each destination's
+    in-edges in their original order (so message sums associate identically)."""
+    s_all, d_all = [], []
+    for p in parts:
+        h = p.halos["node"]
+        lo = p.ranges["node"][p.rank]
+        s = p.inputs["src_adj_nodes_nodes"]
+        glob = s + lo
+        if h.n_halo:
+            glob = np.where(s < h.n_owned, s + lo, h.halo_ids[np.clip(s - h.n_owned, 0, h.n_halo - 1)])
+        s_all.append(glob)
+        d_all.append(p.inputs["dst_adj_nodes_nodes"] + lo)
+        assert p.inputs["num_node"] == h.n_owned
+    s_all, d_all = np.concatenate(s_all), np.concatenate(d_all)
+    order = np.argsort(x["dst_adj_nodes_nodes"], kind="stable")
+    order2 = np.argsort(d_all, kind="stable")
+    np.testing.assert_array_equal(d_all[order2], x["dst_adj_nodes_nodes"][order])
+    np.testing.assert_array_equal(s_all[order2], x["src_adj_nodes_nodes"][order])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_edge_cut_loopback(world):
+    plan, x = _synthetic_plan_and_inputs()
+    parts = [partition.local_part(x, plan, r, world) for r in range(world)]
+    _check_halo_exchange(parts, partition.LoopbackComm(world))
+    _check_partition_edges(parts, x)
+    if world > 1:
+        assert all(p.halos["node"].n_halo > 0 for p in parts)
+
+
+def test_edge_cut_rejects_ordered():
+    desc, dims, mi = workloads.model("routenet")
+    plan = MPPlan.from_model_info(mi)
+    with pytest.raises(ValueError):
+        partition.local_part({}, plan, 0, 2)
+
+
+def _edge_cut_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan, x = _synthetic_plan_and_inputs()
+        part = partition.local_part(x, plan, rank, world)
+        states = _check_halo_exchange([part], partition.TorchComm(dist))
+        h = part.halos["node"]
+        out[rank] = (h.n_owned, h.n_halo, list(h.send_counts), list(h.recv_counts), float(states[0].sum()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_edge_cut_gloo_world2():
+    world = 2
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_edge_cut_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    plan, x = _synthetic_plan_and_inputs()
+    parts = [partition.local_part(x, plan, r, world) for r in range(world)]
+    partition.exchange_requests(parts, partition.LoopbackComm(world))
+    for r in range(world):
+        n_owned, n_halo, sc, rc, _ = res[r]
+        h = parts[r].halos["node"]
+        assert (n_owned, n_halo, sc, rc) == (h.n_owned, h.n_halo, h.send_counts, h.recv_counts)
+        # what r sends to q is what q receives from r
+        assert sc[1 - r] == res[1 - r][3][r]
