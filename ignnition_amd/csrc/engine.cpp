@@ -104,6 +104,9 @@ struct ign_plan {
   // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
   bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
+  int sum_variant = 2;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS; IGN_SUM_VARIANT
+  int sum_order = 0;              // sum MPs: 0 global in-degree sort, 1 sort within 256-row chunks
+                                  // (keeps id locality), 2 id order; IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
   // timing
   bool timing = false;
@@ -250,6 +253,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = atoi(v) == 1 ? 1 : 2;
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
+  if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
+  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 1 ? 1 : 2;
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
@@ -701,7 +706,13 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.bytes = (double)steps * (12.0 * H + 4) + (double)ND * (8.0 * H + 12);
       b->gru_steps += steps * p->T;
     } else {
-      sort_order(order, flen, b->row_off[dst], p->graph_major);
+      if (p->sum_order == 0) {
+        sort_order(order, flen, b->row_off[dst], p->graph_major);
+      } else if (p->sum_order == 1) {
+        auto by_cnt = [&](int32_t x, int32_t y) { return flen[x] > flen[y]; };
+        for (int64_t c = 0; c < ND; c += 256)
+          std::stable_sort(order.begin() + c, order.begin() + std::min<int64_t>(ND, c + 256), by_cnt);
+      }
       // edge-cut partitions: destinations reading a halo row go last (they wait for the exchange)
       std::vector<char> bnd(ND, 0);
       for (size_t k = 0; k < mdst.size(); ++k) {
@@ -887,7 +898,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count, p->xcd_remap};
       const double frac = mb.n_dst ? (double)count / mb.n_dst : 0.0;
       tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac);
-      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, st));
+      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
       tm.end();
     }
   }

@@ -65,7 +65,7 @@ hipError_t launch_project(const float* x, int64_t n, const float* Wp, const floa
 hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
                             const uint32_t* rows, int W, const float* bias_row, hipStream_t st);
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st);
-hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st);
+hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,

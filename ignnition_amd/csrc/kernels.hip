@@ -672,6 +672,112 @@ __global__ __launch_bounds__(256) void sum_gru_wide_kernel(SumGruArgs a) {
   }
 }
 
+// Sum update for wide cells with the weights in LDS: W and U fragments (96 KB at 64/64) are
+// staged once per block, so the per-tile weight stream (96 KB per 16 rows) comes from LDS
+// instead of L2.  One 12-wave block per CU (3 waves per SIMD), persistent over the
+// in-degree-sorted tiles.
+template <int DIN, int H, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void sum_gru_lds_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16;
+  constexpr int WF = 3 * NT * X4 * 64, UF = 3 * NT * H4 * 64;   // float4 fragments
+  __shared__ f4 sW[WF];
+  __shared__ f4 sU[UF];
+  __shared__ float sbias[4 * H];
+  {
+    const f4* gW = reinterpret_cast<const f4*>(a.Wp);
+    const f4* gU = reinterpret_cast<const f4*>(a.Up);
+    for (int i = threadIdx.x; i < WF; i += 64 * WAVES) sW[i] = gW[i];
+    for (int i = threadIdx.x; i < UF; i += 64 * WAVES) sU[i] = gU[i];
+    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) sbias[i] = a.bias[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * WAVES + wave; tile < n_tiles; tile += (int64_t)gridDim.x * WAVES) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+    const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    f4 x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+    int64_t m = m0;
+    for (; m + 2 <= m1; m += 2) {
+      const float* p0 = src_ptr(a.src, a.msg_src[m], DIN);
+      const float* p1 = src_ptr(a.src, a.msg_src[m + 1], DIN);
+      f4 v0[NC], v1[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        v0[c] = ld4(p0 + 16 * c + 4 * g);
+        v1[c] = ld4(p1 + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
+    }
+    for (; m < m1; ++m) {
+      const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+    }
+    // the weight reads are loop-invariant: an opaque offset keeps the compiler from hoisting
+    // all 96 KB of them out of the tile loop into (spilled) registers
+    int wofs = lane;
+    asm volatile("" : "+v"(wofs));
+    f4 hn[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int u0 = 16 * t + 4 * g;
+      f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+      f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+      f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
+      f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+#pragma unroll
+      for (int s4 = 0; s4 < X4; ++s4) {
+        const f4 wz = sW[((0 * NT + t) * X4 + s4) * 64 + wofs];
+        const f4 wr = sW[((1 * NT + t) * X4 + s4) * 64 + wofs];
+        const f4 wh = sW[((2 * NT + t) * X4 + s4) * 64 + wofs];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float xb = x[s4][q];
+          az = MFMA(wz[q], xb, az);
+          ar = MFMA(wr[q], xb, ar);
+          ax = MFMA(wh[q], xb, ax);
+        }
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < H4; ++s4) {
+        const f4 wz = sU[((0 * NT + t) * H4 + s4) * 64 + wofs];
+        const f4 wr = sU[((1 * NT + t) * H4 + s4) * 64 + wofs];
+        const f4 wh = sU[((2 * NT + t) * H4 + s4) * 64 + wofs];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float hb = h[s4][q];
+          az = MFMA(wz[q], hb, az);
+          ar = MFMA(wr[q], hb, ar);
+          ah = MFMA(wh[q], hb, ah);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[r]);
+        const float rr = sig2_(ar[r]);
+        const float c = tanh2_(ax[r] + rr * ah[r]);
+        hn[t][r] = c + z * (h[t][r] - c);
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fused readout MLP (GM:611-629, RNJ:113-142): y = act2(act1(X W1 + b1) W2 + b2) . w3 + b3.
 // One wave = 32 rows (two 16-row B tiles).  Layer-1 activations stay in registers in the
@@ -880,7 +986,7 @@ hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, c
 
 // Grid for a persistent kernel: resident blocks per CU (occupancy API) x CUs, at most the work.
 template <typename K>
-static int persistent_grid(K kernel, int64_t n_blocks_of_work) {
+static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -889,7 +995,7 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work) {
     if (cus <= 0) cus = 256;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
   int64_t g = (int64_t)per_cu * cus;
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, n_blocks_of_work));
 }
@@ -917,7 +1023,7 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st) {
+hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
   // one tile per wave: measured faster than a persistent grid for this latency-bound gather
   // (0.109 vs 0.141 ms on 512 x synth50): more independent waves queue behind the resident ones
@@ -933,7 +1039,14 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, hipStream_t st
   SUM_CASE(32, 16)
 #undef SUM_CASE
   if (din == 64 && h == 64) {
-    hipLaunchKernelGGL((sum_gru_wide_kernel<64, 64>), grid, dim3(256), 0, st, args);
+    if (variant == 2) {
+      constexpr int WV = 12;
+      auto kern = sum_gru_lds_kernel<64, 64, WV>;
+      const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
+      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
+    } else {
+      hipLaunchKernelGGL((sum_gru_wide_kernel<64, 64>), grid, dim3(256), 0, st, args);
+    }
     return hipGetLastError();
   }
   return hipErrorInvalidValue;
