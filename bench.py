@@ -183,13 +183,20 @@ def main():
         launches = max(s["launches"], 1)
         avg_s = s["ms"] / launches / 1e3
         flops_launch = s["flops"] / launches
-        achieved = flops_launch / avg_s / 1e12
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+        bytes_launch = s["bytes"] / launches
+        # the binding roof: whichever of bytes/BW and flops/peak is larger
+        hbm_bound = bytes_launch / (PEAK_HBM_GBS * 1e9) > flops_launch / (PEAK_FP32_MFMA_TFLOPS * 1e12)
+        if hbm_bound:
+            achieved, peak, unit = bytes_launch / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+        else:
+            achieved, peak, unit = flops_launch / avg_s / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+        roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": peak,
+                "unit": unit, "frac": round(achieved / peak, 4),
                 "traffic": load_traffic(dom, workload),
-                "alg_bytes_per_launch": s["bytes"] / launches,
+                "alg_bytes_per_launch": bytes_launch, "alg_flops_per_launch": flops_launch,
                 "avg_launch_ms": round(s["ms"] / launches, 4),
-                "hbm_frac_alg": round(s["bytes"] / launches / avg_s / 1e9 / PEAK_HBM_GBS, 4),
+                "hbm_frac_alg": round(bytes_launch / avg_s / 1e9 / PEAK_HBM_GBS, 4),
+                "mfma_frac_alg": round(flops_launch / avg_s / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
                 "kernels": {k: {"launches": v["launches"], "ms_total": round(v["ms"], 3),
                                 "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2),
                                 "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}

@@ -104,7 +104,10 @@ struct ign_plan {
   // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
   bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
-  int sum_variant = 2;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS; IGN_SUM_VARIANT
+  int sum_variant = 3;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS,
+                                  // 3 = LDS + 4 messages in flight per lane, 4 = warp-specialised
+                                  // (producer waves gather, consumer waves MFMA), 5 = LDS + header /
+                                  // index prefetch one tile ahead; IGN_SUM_VARIANT
   int sum_order = 0;              // sum MPs: 0 global in-degree sort, 1 sort within 256-row chunks
                                   // (keeps id locality), 2 id order; IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
@@ -254,7 +257,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
-  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 1 ? 1 : 2;
+  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(5, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);

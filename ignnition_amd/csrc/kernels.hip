@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256) void sum_gru_wide_kernel(SumGruArgs a) {
 // staged once per block, so the per-tile weight stream (96 KB per 16 rows) comes from LDS
 // instead of L2.  One 12-wave block per CU (3 waves per SIMD), persistent over the
 // in-degree-sorted tiles.
-template <int DIN, int H, int WAVES>
+template <int DIN, int H, int WAVES, int GU>
 __global__ __launch_bounds__(64 * WAVES) void sum_gru_lds_kernel(SumGruArgs a) {
   constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16;
   constexpr int WF = 3 * NT * X4 * 64, UF = 3 * NT * H4 * 64;   // float4 fragments
@@ -708,6 +708,19 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_lds_kernel(SumGruArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
     int64_t m = m0;
+    for (; m + GU <= m1; m += GU) {       // GU messages in flight per lane
+      f4 v[GU][NC];
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const float* p = src_ptr(a.src, a.msg_src[m + u], DIN);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] += v[u][c];
+    }
     for (; m + 2 <= m1; m += 2) {
       const float* p0 = src_ptr(a.src, a.msg_src[m], DIN);
       const float* p1 = src_ptr(a.src, a.msg_src[m + 1], DIN);
@@ -775,6 +788,287 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_lds_kernel(SumGruArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
     }
+  }
+}
+
+// Sum update for wide cells, W/U in LDS, with the gather's dependent loads taken off the
+// critical path: the next tile's header (order, msg_ptr) is loaded while this tile gathers,
+// and its first NI message indices while this tile runs its MFMAs, so a tile's gather starts
+// with all row addresses known and issues GU rows per lane back to back.
+template <int DIN, int H, int WAVES, int GU, int NI>
+__global__ __launch_bounds__(64 * WAVES) void sum_gru_pf_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16;
+  constexpr int WF = 3 * NT * X4 * 64, UF = 3 * NT * H4 * 64;
+  __shared__ f4 sW[WF];
+  __shared__ f4 sU[UF];
+  __shared__ float sbias[4 * H];
+  {
+    const f4* gW = reinterpret_cast<const f4*>(a.Wp);
+    const f4* gU = reinterpret_cast<const f4*>(a.Up);
+    for (int i = threadIdx.x; i < WF; i += 64 * WAVES) sW[i] = gW[i];
+    for (int i = threadIdx.x; i < UF; i += 64 * WAVES) sU[i] = gU[i];
+    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) sbias[i] = a.bias[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  const int64_t step = (int64_t)gridDim.x * WAVES;
+  int64_t tile = xcd_block(a.xcd_remap) * WAVES + wave;
+
+  int row_n;
+  int64_t m0_n, m1_n;
+  uint32_t idx_n[NI];
+  auto load_hdr = [&](int64_t t) {
+    const int64_t pos = t * 16 + j;
+    const bool ok = t < n_tiles && pos < a.n_dst;
+    row_n = ok ? a.order[pos] : -1;
+    m0_n = ok ? a.msg_ptr[pos] : 0;
+    m1_n = ok ? a.msg_ptr[pos + 1] : 0;
+  };
+  auto load_idx = [&]() {
+#pragma unroll
+    for (int k = 0; k < NI; ++k) idx_n[k] = m0_n + k < m1_n ? a.msg_src[m0_n + k] : 0u;
+  };
+  load_hdr(tile);
+  load_idx();
+  for (; tile < n_tiles; tile += step) {
+    const int row = row_n;
+    const int64_t m0 = m0_n, m1 = m1_n;
+    uint32_t idx[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) idx[k] = idx_n[k];
+    load_hdr(tile + step);                   // consumed after the gather
+    const bool valid = row >= 0;
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    const int deg = (int)(m1 - m0);
+    int dmax = deg;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o));
+    f4 x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+#pragma unroll
+    for (int c0 = 0; c0 < NI; c0 += GU) {
+      if (c0 < dmax) {
+        f4 v[GU][NC];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          const float* p = src_ptr(a.src, idx[c0 + u], DIN);
+#pragma unroll
+          for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          const bool ok = c0 + u < deg;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) x[c] = ok ? x[c] + v[u][c] : x[c];
+        }
+      }
+    }
+    for (int64_t m = m0 + NI; m < m1; ++m) {   // rows with more than NI messages
+      const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+    }
+    load_idx();                              // next tile's indices land during the MFMAs
+    int wofs = lane;
+    asm volatile("" : "+v"(wofs));
+    f4 hn[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int u0 = 16 * t + 4 * g;
+      f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+      f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+      f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
+      f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+#pragma unroll
+      for (int s4 = 0; s4 < X4; ++s4) {
+        const f4 wz = sW[((0 * NT + t) * X4 + s4) * 64 + wofs];
+        const f4 wr = sW[((1 * NT + t) * X4 + s4) * 64 + wofs];
+        const f4 wh = sW[((2 * NT + t) * X4 + s4) * 64 + wofs];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float xb = x[s4][q];
+          az = MFMA(wz[q], xb, az);
+          ar = MFMA(wr[q], xb, ar);
+          ax = MFMA(wh[q], xb, ax);
+        }
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < H4; ++s4) {
+        const f4 wz = sU[((0 * NT + t) * H4 + s4) * 64 + wofs];
+        const f4 wr = sU[((1 * NT + t) * H4 + s4) * 64 + wofs];
+        const f4 wh = sU[((2 * NT + t) * H4 + s4) * 64 + wofs];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float hb = h[s4][q];
+          az = MFMA(wz[q], hb, az);
+          ar = MFMA(wr[q], hb, ar);
+          ah = MFMA(wh[q], hb, ah);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[r]);
+        const float rr = sig2_(ar[r]);
+        const float c = tanh2_(ax[r] + rr * ah[r]);
+        hn[t][r] = c + z * (h[t][r] - c);
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
+    }
+  }
+}
+
+// Warp-specialised sum update for wide cells.  A 16-wave block per CU: 8 producer waves gather
+// and sum the messages of the next 8 tiles (16 destinations each) into an LDS x buffer while 8
+// consumer waves run the GRU MFMAs of the current 8 tiles with W/U fragments from LDS.  The
+// gather latency is then hidden behind the MFMA pipe instead of stalling it.  Per phase:
+//   consumers copy their x tile from LDS to registers and issue their h loads | barrier |
+//   producers gather phase p+1 into LDS; consumers compute phase p           | barrier
+template <int DIN, int H, int GU>
+__global__ __launch_bounds__(1024) void sum_gru_ws_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16, CW = 8;
+  constexpr int WF = 3 * NT * X4 * 64, UF = 3 * NT * H4 * 64;
+  __shared__ f4 sW[WF];
+  __shared__ f4 sU[UF];
+  __shared__ f4 sx[CW * NC * 64];
+  __shared__ float sbias[4 * H];
+  {
+    const f4* gW = reinterpret_cast<const f4*>(a.Wp);
+    const f4* gU = reinterpret_cast<const f4*>(a.Up);
+    for (int i = threadIdx.x; i < WF; i += 1024) sW[i] = gW[i];
+    for (int i = threadIdx.x; i < UF; i += 1024) sU[i] = gU[i];
+    for (int i = threadIdx.x; i < 4 * H; i += 1024) sbias[i] = a.bias[i];
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const bool producer = wave >= CW;
+  const int slot = wave & (CW - 1);          // tile of the phase this wave produces / consumes
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  const int64_t n_groups = (n_tiles + CW - 1) / CW;
+  const int64_t stride = gridDim.x;
+  int64_t q = xcd_block(a.xcd_remap);
+
+  auto gather = [&](int64_t grp) {           // producers: x of tile (grp, slot) -> sx
+    const int64_t pos = (grp * CW + slot) * 16 + j;
+    const bool valid = grp < n_groups && pos < a.n_dst;
+    const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+    const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+    f4 x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+    int64_t m = m0;
+    for (; m + GU <= m1; m += GU) {
+      f4 v[GU][NC];
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const float* p = src_ptr(a.src, a.msg_src[m + u], DIN);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] += v[u][c];
+    }
+    for (; m + 2 <= m1; m += 2) {
+      const float* p0 = src_ptr(a.src, a.msg_src[m], DIN);
+      const float* p1 = src_ptr(a.src, a.msg_src[m + 1], DIN);
+      f4 v0[NC], v1[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        v0[c] = ld4(p0 + 16 * c + 4 * g);
+        v1[c] = ld4(p1 + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
+    }
+    for (; m < m1; ++m) {
+      const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) sx[(slot * NC + c) * 64 + lane] = x[c];
+  };
+
+  if (producer && q < n_groups) gather(q);
+  __syncthreads();
+  for (; q < n_groups; q += stride) {
+    f4 x[NC], h[NT];
+    int row = 0;
+    bool valid = false;
+    if (!producer) {
+      const int64_t pos = (q * CW + slot) * 16 + j;
+      valid = pos < a.n_dst;
+      row = valid ? a.order[pos] : 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] = sx[(slot * NC + c) * 64 + lane];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    }
+    __syncthreads();
+    if (producer) {
+      if (q + stride < n_groups) gather(q + stride);
+    } else {
+      int wofs = lane;                       // opaque: keeps the weight reads inside the loop
+      asm volatile("" : "+v"(wofs));
+      f4 hn[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int u0 = 16 * t + 4 * g;
+        f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+        f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+        f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
+        f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+#pragma unroll
+        for (int s4 = 0; s4 < X4; ++s4) {
+          const f4 wz = sW[((0 * NT + t) * X4 + s4) * 64 + wofs];
+          const f4 wr = sW[((1 * NT + t) * X4 + s4) * 64 + wofs];
+          const f4 wh = sW[((2 * NT + t) * X4 + s4) * 64 + wofs];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const float xb = x[s4][qq];
+            az = MFMA(wz[qq], xb, az);
+            ar = MFMA(wr[qq], xb, ar);
+            ax = MFMA(wh[qq], xb, ax);
+          }
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < H4; ++s4) {
+          const f4 wz = sU[((0 * NT + t) * H4 + s4) * 64 + wofs];
+          const f4 wr = sU[((1 * NT + t) * H4 + s4) * 64 + wofs];
+          const f4 wh = sU[((2 * NT + t) * H4 + s4) * 64 + wofs];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const float hb = h[s4][qq];
+            az = MFMA(wz[qq], hb, az);
+            ar = MFMA(wr[qq], hb, ar);
+            ah = MFMA(wh[qq], hb, ah);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = sig2_(az[r]);
+          const float rr = sig2_(ar[r]);
+          const float c = tanh2_(ax[r] + rr * ah[r]);
+          hn[t][r] = c + z * (h[t][r] - c);
+        }
+      }
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1039,9 +1333,18 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
   SUM_CASE(32, 16)
 #undef SUM_CASE
   if (din == 64 && h == 64) {
-    if (variant == 2) {
+    if (variant == 5) {
       constexpr int WV = 12;
-      auto kern = sum_gru_lds_kernel<64, 64, WV>;
+      auto kern = sum_gru_pf_kernel<64, 64, WV, 4, 16>;
+      const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
+      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
+    } else if (variant == 4) {
+      auto kern = sum_gru_ws_kernel<64, 64, 4>;
+      const int64_t work = (args.n_dst + 127) / 128;
+      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 1024)), dim3(1024), 0, st, args);
+    } else if (variant >= 2) {
+      constexpr int WV = 12;
+      auto kern = variant == 3 ? sum_gru_lds_kernel<64, 64, WV, 4> : sum_gru_lds_kernel<64, 64, WV, 2>;
       const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
       hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
     } else {

@@ -1,0 +1,14 @@
+"""Summarise bench.py JSON lines: ms/step and average per-launch ms per kernel kind."""
+import json
+import sys
+
+for path in sys.argv[1:]:
+    try:
+        line = [l for l in open(path) if l.startswith("{")][-1]
+        d = json.loads(line)
+    except Exception as exc:  # noqa: BLE001
+        print(path, "no result:", exc)
+        continue
+    k = (d.get("roofline") or {}).get("kernels", {})
+    per = {a: round(b["ms_total"] / b["launches"], 4) for a, b in k.items()}
+    print("%-28s %.3e edges/s %.3f ms/step" % (path.split("/")[-1], d["value"], d["ms_per_step"]), per)
