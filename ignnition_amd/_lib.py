@@ -75,7 +75,7 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_plan_set_timing", "ign_plan_set_stream", "ign_batch_create", "ign_batch_destroy", "ign_batch_info",
            "ign_forward", "ign_synchronize", "ign_batch_predictions", "ign_batch_state", "ign_stats",
            "ign_forward_begin", "ign_forward_mp", "ign_forward_end", "ign_batch_mp_split", "ign_batch_bind_state",
-           "ign_batch_state_slot", "ign_gather_rows"]
+           "ign_batch_state_slot", "ign_gather_rows", "ign_plan_set_timing_kinds"]
 
 ABI_VERSION = 2
 PART = {"all": 0, "interior": 1, "boundary": 2}
@@ -121,6 +121,7 @@ def _load():
         "ign_batch_bind_state": (C.c_int, [VP, VP, i32, VP, VP, i64]),
         "ign_batch_state_slot": (C.c_int, [VP, i32, P(i32)]),
         "ign_gather_rows": (C.c_int, [VP, VP, i64, VP, i64, i32, VP]),
+        "ign_plan_set_timing_kinds": (C.c_int, [VP, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

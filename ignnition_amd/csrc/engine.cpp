@@ -113,10 +113,12 @@ struct ign_plan {
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
   // timing
   bool timing = false;
+  uint32_t timing_kinds = ~0u;    // kernel kinds that get event pairs (ign_plan_set_timing_kinds)
   std::vector<hipEvent_t> ev;     // pairs
   std::vector<int> ev_kind;
   std::vector<double> ev_flops, ev_bytes;
   int ev_slot = 0;                // events recorded since ign_forward_begin
+  bool use_graph = true;          // replay ign_forward as one captured hipGraph; IGN_HIP_GRAPH=0 disables
   ign_stats_t stats{};
 };
 
@@ -159,6 +161,11 @@ struct ign_batch {
   int64_t n_pred = 0, out_units = 1;
   int64_t edges_per_forward = 0, gru_steps = 0;
   std::vector<void*> allocs;
+  // captured ign_forward (init .. readout) for replay; the event slots it records
+  hipGraphExec_t graph = nullptr;
+  bool graph_timing = false;
+  std::vector<int> graph_kind;
+  std::vector<double> graph_flops, graph_bytes;
 };
 
 namespace {
@@ -257,6 +264,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
+  if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(5, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   p->T = d->num_iterations;
@@ -453,6 +461,13 @@ int ign_plan_set_params(ign_plan* p, const float* params, int32_t on_device) {
 int ign_plan_set_timing(ign_plan* p, int32_t enabled) {
   if (!p) return fail(IGN_ERR_INVALID, "null plan");
   p->timing = enabled != 0;
+  p->stats = ign_stats_t{};
+  return IGN_OK;
+}
+
+int ign_plan_set_timing_kinds(ign_plan* p, uint32_t kinds) {
+  if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  p->timing_kinds = kinds;
   p->stats = ign_stats_t{};
   return IGN_OK;
 }
@@ -771,6 +786,7 @@ void ign_batch_destroy(ign_batch* b) {
     hipSetDevice(b->plan->device);
     if (b->plan->stream) hipStreamSynchronize(b->plan->stream);
   }
+  if (b->graph) hipGraphExecDestroy(b->graph);
   for (void* a : b->allocs) hipFree(a);
   delete b;
 }
@@ -798,8 +814,10 @@ namespace {
 
 struct Timer {
   ign_plan* p;
+  bool on = false;
   void begin(int kind, double flops, double bytes) {
-    if (!p->timing) return;
+    on = p->timing && ((p->timing_kinds >> kind) & 1u);
+    if (!on) return;
     const int slot = p->ev_slot;
     size_t need = 2 * (slot + 1);
     while (p->ev.size() < need) {
@@ -818,7 +836,7 @@ struct Timer {
     hipEventRecord(p->ev[2 * slot], p->stream);
   }
   void end() {
-    if (!p->timing) return;
+    if (!on) return;
     hipEventRecord(p->ev[2 * p->ev_slot + 1], p->stream);
     ++p->ev_slot;
   }
@@ -909,9 +927,25 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   return IGN_OK;
 }
 
-int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
-  int rc = check_pb(p, b);
-  if (rc) return rc;
+namespace {
+
+int accumulate_stats(ign_plan* p, int n, const int* kind, const double* flops, const double* bytes) {
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  ign_stats_t& s = p->stats;
+  s.kinds = K_KINDS;
+  for (int i = 0; i < n; ++i) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]);
+    s.launches[kind[i]] += 1;
+    s.ms[kind[i]] += ms;
+    s.flops[kind[i]] += flops[i];
+    s.bytes[kind[i]] += bytes[i];
+  }
+  return IGN_OK;
+}
+
+// readout launches (GM:611-629); no host synchronisation, so it can be captured
+int readout(ign_plan* p, ign_batch* b) {
   hipStream_t st = p->stream;
   Timer tm{p};
   // readout (GM:611-629)
@@ -953,35 +987,98 @@ int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
       in_stride = dl.out;
     }
   }
-  if (pred_out) {
-    HIP_TRY(hipMemcpyAsync(pred_out, b->d_pred, P * b->out_units * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-  }
-  if (p->timing) {
-    HIP_TRY(hipStreamSynchronize(st));
-    ign_stats_t& s = p->stats;
-    s.kinds = K_KINDS;
-    for (int i = 0; i < p->ev_slot; ++i) {
-      float ms = 0;
-      hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]);
-      int k = p->ev_kind[i];
-      s.launches[k] += 1;
-      s.ms[k] += ms;
-      s.flops[k] += p->ev_flops[i];
-      s.bytes[k] += p->ev_bytes[i];
-    }
-  }
-  p->ev_slot = 0;
   return IGN_OK;
 }
 
-int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
+int copy_out(ign_plan* p, ign_batch* b, float* pred_out) {
+  if (pred_out) {
+    HIP_TRY(hipMemcpyAsync(pred_out, b->d_pred, b->n_pred * b->out_units * sizeof(float), hipMemcpyDeviceToHost,
+                           p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+  }
+  return IGN_OK;
+}
+
+int forward_body(ign_plan* p, ign_batch* b) {
   int rc = ign_forward_begin(p, b);
   if (rc) return rc;
   for (int it = 0; it < p->T; ++it)                     // GM:406
     for (int mi = 0; mi < (int)p->mps.size(); ++mi)     // GM:410-414 (stages flattened in order)
       if ((rc = ign_forward_mp(p, b, mi, IGN_PART_ALL))) return rc;
-  return ign_forward_end(p, b, pred_out);
+  return readout(p, b);
+}
+
+// Capture the whole forward (init, T x MPs, readout; HIP event records included when timing is
+// on) into one hipGraph per batch.  The null stream cannot be captured: no graph there.
+int capture(ign_plan* p, ign_batch* b) {
+  if (b->graph) {
+    hipGraphExecDestroy(b->graph);
+    b->graph = nullptr;
+  }
+  if (!p->stream) return IGN_ERR_UNSUPPORTED;
+  hipGraph_t g = nullptr;
+  HIP_TRY(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
+  int rc = forward_body(p, b);
+  hipError_t e = hipStreamEndCapture(p->stream, &g);
+  if (rc || e != hipSuccess || !g) {
+    if (g) hipGraphDestroy(g);
+    hipGetLastError();
+    return rc ? rc : fail(IGN_ERR_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  }
+  e = hipGraphInstantiate(&b->graph, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    b->graph = nullptr;
+    return fail(IGN_ERR_DEVICE, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  }
+  b->graph_timing = p->timing;
+  const int n = p->timing ? p->ev_slot : 0;
+  b->graph_kind.assign(p->ev_kind.begin(), p->ev_kind.begin() + n);
+  b->graph_flops.assign(p->ev_flops.begin(), p->ev_flops.begin() + n);
+  b->graph_bytes.assign(p->ev_bytes.begin(), p->ev_bytes.begin() + n);
+  p->ev_slot = 0;
+  return IGN_OK;
+}
+
+}  // namespace
+
+int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = check_pb(p, b);
+  if (rc) return rc;
+  if ((rc = readout(p, b))) return rc;
+  if ((rc = copy_out(p, b, pred_out))) return rc;
+  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_flops.data(), p->ev_bytes.data())))
+    return rc;
+  p->ev_slot = 0;
+  return IGN_OK;
+}
+
+int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = check_pb(p, b);
+  if (rc) return rc;
+  // HIP event records captured into a graph report 0 ms on this runtime, so timed forwards
+  // launch directly; untimed ones replay the captured graph
+  if (p->use_graph && p->stream && !p->timing) {
+    if (!b->graph) {
+      if ((rc = capture(p, b))) {
+        p->use_graph = false;        // not capturable here: run the launches directly from now on
+        b->graph = nullptr;
+        return ign_forward(p, b, pred_out);
+      }
+    }
+    HIP_TRY(hipGraphLaunch(b->graph, p->stream));
+    if ((rc = copy_out(p, b, pred_out))) return rc;
+    if (p->timing)
+      return accumulate_stats(p, (int)b->graph_kind.size(), b->graph_kind.data(), b->graph_flops.data(),
+                              b->graph_bytes.data());
+    return IGN_OK;
+  }
+  if ((rc = forward_body(p, b))) return rc;
+  if ((rc = copy_out(p, b, pred_out))) return rc;
+  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_flops.data(), p->ev_bytes.data())))
+    return rc;
+  p->ev_slot = 0;
+  return IGN_OK;
 }
 
 int ign_batch_mp_split(const ign_batch* b, int32_t mi, int64_t* interior, int64_t* boundary) {

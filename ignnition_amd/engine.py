@@ -243,8 +243,12 @@ class Engine:
             flat[off:off + v.size] = v
         check(lib.ign_plan_set_params(self.handle, flat.ctypes.data_as(C.c_void_p), 0))
 
-    def set_timing(self, on: bool):
+    def set_timing(self, on: bool, kinds=None):
+        """Per-launch HIP event timing (resets the statistics); ``kinds``: kernel kind names to
+        instrument (default all)."""
         check(lib.ign_plan_set_timing(self.handle, int(on)))
+        mask = 0xFFFFFFFF if kinds is None else sum(1 << _lib.KERNEL_KINDS.index(k) for k in kinds)
+        check(lib.ign_plan_set_timing_kinds(self.handle, mask))
 
     def stats(self) -> dict:
         s = _lib.Stats()

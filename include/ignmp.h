@@ -169,7 +169,10 @@ int  ign_plan_num_param_tensors(const ign_plan* plan, int32_t* n);
 int  ign_plan_param_tensor(const ign_plan* plan, int32_t i, int32_t* kind, int32_t* owner,
                            int64_t* offset, int32_t* rows, int32_t* cols);
 int  ign_plan_set_params(ign_plan* plan, const float* params, int32_t on_device);
-int  ign_plan_set_timing(ign_plan* plan, int32_t enabled);
+int  ign_plan_set_timing(ign_plan* plan, int32_t enabled);   /* also resets the statistics */
+/* Restrict the event pairs to kernel kinds in the bit mask (bit k = kind k of ign_stats_t);
+ * default all.  Each event pair costs a few microseconds of queue time. */
+int  ign_plan_set_timing_kinds(ign_plan* plan, uint32_t kinds);
 int  ign_plan_set_stream(ign_plan* plan, void* hip_stream);
 
 int  ign_batch_create(ign_plan* plan, const ign_batch_desc* desc, ign_batch** out);
@@ -177,7 +180,9 @@ void ign_batch_destroy(ign_batch* batch);
 int  ign_batch_info(const ign_batch* batch, ign_batch_info_t* out);
 
 /* Full forward (hidden-state init, T x stages x MPs, readout) on the plan stream.
- * pred_out: host pointer (copied + synchronised) or NULL (stays on device, async).  */
+ * pred_out: host pointer (copied + synchronised) or NULL (stays on device, async).
+ * Untimed forwards on a non-null stream replay one hipGraph captured per batch on first use
+ * (IGN_HIP_GRAPH=0 disables it).  */
 int  ign_forward(ign_plan* plan, ign_batch* batch, float* pred_out);
 int  ign_synchronize(ign_plan* plan);
 /* Device pointer of the batch's prediction buffer (valid until ign_batch_destroy). */

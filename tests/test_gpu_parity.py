@@ -203,3 +203,45 @@ def test_synthetic_graph_h64_matches_oracle():
     out, ref, b, _ = _run(desc, dims, graphs, seed=4, bias=0.1)
     _close(out, ref)
     assert b.edges_per_forward == 3 * len(graphs[0]["src_adj_nodes_nodes"])
+
+
+def test_hip_graph_replay_matches_direct(monkeypatch):
+    """The captured hipGraph replays the same launches: bitwise-equal predictions.  Timed
+    forwards launch directly, and the per-kernel event timing covers every launch."""
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "geant2", 3)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(1, bias_scale=0.1)
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IGN_HIP_GRAPH", mode)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        first = b.forward()                      # graph captured here (mode 1)
+        second = b.forward()                     # ... and replayed
+        np.testing.assert_array_equal(first, second)
+        eng.set_timing(True)
+        timed = b.forward()
+        b.forward()
+        st = eng.stats()
+        np.testing.assert_array_equal(first, timed)
+        assert st["seq_gru"]["launches"] == 2 * plan.iterations
+        assert st["sum_gru"]["launches"] == 2 * plan.iterations
+        assert st["readout"]["launches"] == 2 and st["seq_gru"]["ms"] > 0
+        outs[mode] = first
+        b.close()
+        eng.close()
+    np.testing.assert_array_equal(outs["0"], outs["1"])
+
+
+def test_timing_kinds_mask():
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(0))
+    b = Batch(eng, graphs)
+    eng.set_timing(True, kinds=["seq_gru"])
+    b.forward()
+    st = eng.stats()
+    assert st["seq_gru"]["launches"] == plan.iterations and st["seq_gru"]["ms"] > 0
+    assert st["readout"]["launches"] == 0 and st["sum_gru"]["launches"] == 0
