@@ -214,7 +214,7 @@ def main():
         if synthetic:
             # bounded sample: a 25k-node graph from the same generator (same degree law and locality)
             sd, sdims, _, sg, _ = workloads.make_synthetic_inputs(n_nodes=25_000)
-            cpu = cpu_baseline(sd, sdims, prm, sg * 4, args.cpu_seconds, "25k-node / 250k-edge synthetic graphs")
+            cpu = cpu_baseline(sd, sdims, prm, sg * 16, args.cpu_seconds, "25k-node / 250k-edge synthetic graphs")
         else:
             cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
     line = {
