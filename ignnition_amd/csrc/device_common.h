@@ -1,0 +1,77 @@
+// device_common.h — device helpers shared by kernels.hip (inference) and train_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kernels.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+// Gate nonlinearities on v_exp_f32 + v_rcp_f32 (1 ulp each; an IEEE divide would expand to
+// ~10 VALU instructions and dominate the recurrence's VALU stream).  Both saturate cleanly:
+// exp overflow gives rcp(inf) = 0.
+__device__ __forceinline__ float rcpf_(float x) { return __builtin_amdgcn_rcpf(x); }
+
+__device__ __forceinline__ float sigmoidf_(float x) { return rcpf_(1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float tanhf_(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1)
+  return 1.0f - 2.0f * rcpf_(__expf(2.0f * x) + 1.0f);
+}
+
+// GRU gates on pre-scaled pre-activations.  pack_gru scales the z/r columns (and their biases)
+// by -log2(e) and the candidate columns by 2*log2(e), so
+//   sigmoid(a) = 1 / (1 + 2^(a'))      with a' = -log2(e) a
+//   tanh(c)    = 1 - 2 / (1 + 2^(c'))  with c' = 2 log2(e) c   (c' is linear in x, h, biases)
+// i.e. one v_exp_f32 + one v_rcp_f32 per gate and no scaling multiply.
+#define IGN_NLOG2E (-1.4426950408889634f)
+#define IGN_2LOG2E (2.8853900817779268f)
+__device__ __forceinline__ float sig2_(float a) { return rcpf_(1.0f + __builtin_amdgcn_exp2f(a)); }
+__device__ __forceinline__ float tanh2_(float c) { return 1.0f - 2.0f * rcpf_(1.0f + __builtin_amdgcn_exp2f(c)); }
+
+__device__ __forceinline__ float act_apply(float x, int act) {
+  switch (act) {
+    case IGN_K_ACT_RELU: return x > 0.f ? x : 0.f;
+    case IGN_K_ACT_SELU: {
+      const float lam = 1.0507009873554805f, alpha = 1.6732632423543772f;
+      return x > 0.f ? lam * x : lam * alpha * (__expf(x) - 1.0f);
+    }
+    case IGN_K_ACT_SIGMOID: return sigmoidf_(x);
+    case IGN_K_ACT_TANH: return tanhf_(x);
+    default: return x;
+  }
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float x) {
+  if constexpr (ACT == IGN_K_ACT_RELU) return x > 0.f ? x : 0.f;
+  else if constexpr (ACT == IGN_K_ACT_SELU) {   // branch-free: exp of min(x, 0), then select
+    const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
+    const float e = __expf(fminf(x, 0.f));
+    return x > 0.f ? lam * x : la * (e - 1.0f);
+  } else if constexpr (ACT == IGN_K_ACT_SIGMOID) return sigmoidf_(x);
+  else if constexpr (ACT == IGN_K_ACT_TANH) return tanhf_(x);
+  else return x;
+}
+
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (b, b+8, ...
+// share one), so remap so that XCD x runs a contiguous range of tiles (bijective for any grid,
+// cdna_hip_programming.md §5.5).  Consecutive tiles are the same graph -> that graph's source
+// rows stay in one XCD's L2.  Placement only affects speed, never results.
+__device__ __forceinline__ int64_t xcd_block(int enabled) {
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  if (!enabled) return b;
+  const int64_t xcd = b & 7, q = nb >> 3, r = nb & 7;
+  const int64_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// element (gate-tile gt, k-step s, lane) of a float4-grouped fragment array with KS k-steps
+__device__ __forceinline__ int64_t frag_idx(int gt, int s, int KS, int lane) {
+  return ((((int64_t)gt * (KS / 4) + (s >> 2)) * 64 + lane) << 2) + (s & 3);
+}
+

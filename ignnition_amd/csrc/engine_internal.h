@@ -1,0 +1,160 @@
+// engine_internal.h — plan / batch structures shared by engine.cpp (inference) and train.cpp
+// (training).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/ignmp.h"
+#include "kernels.h"
+
+struct TrainState;                 // train.cpp
+void train_state_destroy(TrainState* t);
+
+namespace ign {
+
+int fail(int code, const char* fmt, ...);
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return fail(IGN_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e));    \
+  } while (0)
+
+enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_PROJECT = 4, K_OTHER = 5, K_KINDS = 6 };
+
+struct Tensor {
+  int kind, owner;
+  int64_t offset;
+  int rows, cols;
+};
+
+struct CellP {
+  int din, H;
+  int64_t off_k, off_rk, off_b;   // raw Keras-layout params
+  int64_t pk_w, pk_u, pk_b;       // packed fragments (in d_packed)
+  bool used = false;
+};
+
+struct DenseP {
+  int in, out, act, use_bias;
+  int64_t off_w, off_b, pk_w;
+};
+
+struct MPP {
+  int dst, aggr, concat_axis, cell;
+  std::vector<ign_source_desc> src;
+  bool sorted;                    // sorted (sequence) update vs single-step update
+  int din;
+};
+
+
+struct MPB {
+  bool sorted = false;
+  int64_t n_dst = 0, n_steps = 0, n_msgs = 0, edges = 0;
+  int32_t* d_order = nullptr;
+  int32_t* d_len = nullptr;
+  int32_t* d_step_ptr = nullptr;
+  int32_t* d_msg_ptr = nullptr;
+  uint32_t* d_msg_src = nullptr;
+  uint32_t* d_step_code = nullptr;
+  float* d_table = nullptr;       // sorted MPs: [sources' rows | zero row | multi rows][3H]
+  std::vector<int64_t> src_off;   // first table row of each source
+  std::vector<int64_t> src_rows;
+  int64_t zero_row = 0, n_multi = 0;
+  int64_t n_interior = 0;         // sum MPs: order[0, n_interior) reads no halo row
+  int32_t* d_multi_ptr = nullptr;
+  uint32_t* d_multi_rows = nullptr;
+  double flops = 0, bytes = 0;    // algorithmic, per launch
+};
+
+
+}  // namespace ign
+
+using namespace ign;
+
+struct ign_plan {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  bool external_stream = false;   // set by ign_plan_set_stream (may be the null stream)
+  int T = 0;
+  std::vector<ign_entity_desc> ents;
+  int n_adj = 0, n_il = 0;
+  std::vector<MPP> mps;
+  std::vector<CellP> cells;
+  std::vector<int> ro_in;
+  std::vector<DenseP> dense;
+  std::vector<Tensor> tensors;
+  int64_t n_params = 0, n_packed = 0;
+  float* d_params = nullptr;
+  float* d_packed = nullptr;
+  bool params_set = false;
+  bool fused_readout = false;
+  int ro_width = 0;
+  int seq_variant = 2;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves)
+  // Measured on 512 x synth50 (profiles/r01): one global length sort without XCD remap is the
+  // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
+  bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
+  int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
+  int sum_variant = 3;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS,
+                                  // 3 = LDS + 4 messages in flight per lane, 4 = warp-specialised
+                                  // (producer waves gather, consumer waves MFMA), 5 = LDS + header /
+                                  // index prefetch one tile ahead; IGN_SUM_VARIANT
+  int sum_order = 0;              // sum MPs: 0 global in-degree sort, 1 sort within 256-row chunks
+                                  // (keeps id locality), 2 id order; IGN_SUM_ORDER
+  int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
+  // timing
+  bool timing = false;
+  uint32_t timing_kinds = ~0u;    // kernel kinds that get event pairs (ign_plan_set_timing_kinds)
+  std::vector<hipEvent_t> ev;     // pairs
+  std::vector<int> ev_kind;
+  std::vector<double> ev_flops, ev_bytes;
+  int ev_slot = 0;                // events recorded since ign_forward_begin
+  bool use_graph = true;          // replay ign_forward as one captured hipGraph; IGN_HIP_GRAPH=0 disables
+  ign_stats_t stats{};
+};
+
+struct ign_batch {
+  ign_plan* plan = nullptr;
+  int G = 0;
+  std::vector<int64_t> rows;                    // per entity (owned rows)
+  std::vector<int64_t> halo;                    // per entity: peer rows after the owned ones (§8e)
+  std::vector<std::vector<int64_t>> row_off;    // [entity][graph]
+  std::vector<float*> d_feat;                   // per entity [rows][F] or null
+  std::vector<float*> d_state[2];               // per entity ping-pong
+  std::vector<int> cur;
+  std::vector<MPB> mp;
+  float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
+  std::vector<float*> d_ro_tmp;                 // generic readout intermediates
+  float* d_pred = nullptr;
+  int64_t n_pred = 0, out_units = 1;
+  int64_t edges_per_forward = 0, gru_steps = 0;
+  std::vector<void*> allocs;
+  // captured ign_forward (init .. readout) for replay; the event slots it records
+  hipGraphExec_t graph = nullptr;
+  bool graph_timing = false;
+  std::vector<int> graph_kind;
+  std::vector<double> graph_flops, graph_bytes;
+};
+
+namespace ign {
+int set_device(int dev);
+int ensure_device(ign_plan* p);
+int dev_alloc(ign_batch* b, float** out, int64_t n);
+template <typename T>
+int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
+  size_t n = std::max<size_t>(host.size(), 1);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+  b->allocs.push_back(p);
+  if (!host.empty()) HIP_TRY(hipMemcpy(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+  else HIP_TRY(hipMemset(p, 0, sizeof(T)));
+  *out = static_cast<T*>(p);
+  return IGN_OK;
+}
+}  // namespace ign
