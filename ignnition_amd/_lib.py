@@ -35,7 +35,7 @@ class CellDesc(C.Structure):
 
 
 class DenseDesc(C.Structure):
-    _fields_ = [("units", i32), ("activation", i32), ("use_bias", i32)]
+    _fields_ = [("units", i32), ("activation", i32), ("use_bias", i32), ("l2", f32)]
 
 
 class PlanDesc(C.Structure):
@@ -75,9 +75,11 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_plan_set_timing", "ign_plan_set_stream", "ign_batch_create", "ign_batch_destroy", "ign_batch_info",
            "ign_forward", "ign_synchronize", "ign_batch_predictions", "ign_batch_state", "ign_stats",
            "ign_forward_begin", "ign_forward_mp", "ign_forward_end", "ign_batch_mp_split", "ign_batch_bind_state",
-           "ign_batch_state_slot", "ign_gather_rows", "ign_plan_set_timing_kinds"]
+           "ign_batch_state_slot", "ign_gather_rows", "ign_plan_set_timing_kinds",
+           "ign_batch_enable_training", "ign_forward_train", "ign_backward", "ign_mse_loss", "ign_l2_loss",
+           "ign_adam_step", "ign_plan_get_params"]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -122,6 +124,13 @@ def _load():
         "ign_batch_state_slot": (C.c_int, [VP, i32, P(i32)]),
         "ign_gather_rows": (C.c_int, [VP, VP, i64, VP, i64, i32, VP]),
         "ign_plan_set_timing_kinds": (C.c_int, [VP, C.c_uint32]),
+        "ign_batch_enable_training": (C.c_int, [VP, VP]),
+        "ign_forward_train": (C.c_int, [VP, VP, VP]),
+        "ign_backward": (C.c_int, [VP, VP, VP, VP]),
+        "ign_mse_loss": (C.c_int, [VP, VP, VP, i64, VP, P(C.c_double)]),
+        "ign_l2_loss": (C.c_int, [VP, P(C.c_double)]),
+        "ign_adam_step": (C.c_int, [VP, VP, VP, VP, i64, f32, f32, f32, f32]),
+        "ign_plan_get_params": (C.c_int, [VP, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -32,6 +32,7 @@
 #include "kernels.h"
 
 #include "engine_internal.h"
+#include "train_kernels.h"
 
 namespace ign {
 
@@ -105,6 +106,27 @@ double gru_flops(int din, int H) { return 2.0 * 3 * H * (din + H) + 14.0 * H; }
 
 }  // namespace ign
 
+
+int ign::repack(ign_plan* p) {
+  for (auto& cp : p->cells) {
+    if (!cp.used) continue;
+    HIP_TRY(launch_pack_gru(p->d_params + cp.off_k, p->d_params + cp.off_rk, p->d_params + cp.off_b,
+                            p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
+                            p->stream));
+    if (cp.pk_wt >= 0) {
+      HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
+      HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
+    }
+  }
+  if (p->fused_readout) {
+    for (int l = 0; l < 2; ++l)
+      HIP_TRY(launch_pack_dense(p->d_params + p->dense[l].off_w, p->d_packed + p->dense[l].pk_w, p->dense[l].in,
+                                p->dense[l].out, p->stream));
+  }
+  for (auto& dp : p->dense)
+    if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
+  return IGN_OK;
+}
 
 // =============================================================================================
 extern "C" {
@@ -219,6 +241,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     dp.out = d->dense[l].units;
     dp.act = d->dense[l].activation;
     dp.use_bias = d->dense[l].use_bias;
+    dp.l2 = d->dense[l].l2;
     if (dp.out <= 0) return fail(IGN_ERR_INVALID, "dense layer %d: units must be > 0", l);
     if (!act_ok(dp.act)) return fail(IGN_ERR_UNSUPPORTED, "dense layer %d: activation %d", l, dp.act);
     p->dense.push_back(dp);
@@ -256,6 +279,17 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     p->dense[0].pk_w = pk; pk = align(pk + (int64_t)p->dense[0].in * p->dense[0].out);
     p->dense[1].pk_w = pk; pk = align(pk + (int64_t)p->dense[1].in * p->dense[1].out);
   }
+  // backward fragments (training): W^T / U^T per cell, W^T per Dense layer where the MFMA
+  // row GEMM is instantiated
+  for (auto& cp : p->cells) {
+    if (!cp.used || !bwd_shape_supported(cp.din, cp.H)) continue;
+    cp.pk_wt = pk; pk = align(pk + 3LL * cp.din * cp.H);
+    cp.pk_ut = pk; pk = align(pk + 3LL * cp.H * cp.H);
+  }
+  for (auto& dp : p->dense) {
+    if (!row_gemm_supported(dp.out, dp.in)) continue;
+    dp.pk_wt = pk; pk = align(pk + (int64_t)dp.in * dp.out);
+  }
   p->n_packed = pk;
 
   // Device resources are allocated on first use (ensure_device), so plan validation and the
@@ -275,6 +309,7 @@ void ign_plan_destroy(ign_plan* p) {
   for (auto e : p->ev) hipEventDestroy(e);
   if (p->d_params) hipFree(p->d_params);
   if (p->d_packed) hipFree(p->d_packed);
+  if (p->d_red) hipFree(p->d_red);
   if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
   delete p;
 }
@@ -309,17 +344,7 @@ int ign_plan_set_params(ign_plan* p, const float* params, int32_t on_device) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(p->d_params, params, p->n_params * sizeof(float),
                          on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, p->stream));
-  for (auto& cp : p->cells) {
-    if (!cp.used) continue;
-    HIP_TRY(launch_pack_gru(p->d_params + cp.off_k, p->d_params + cp.off_rk, p->d_params + cp.off_b,
-                            p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
-                            p->stream));
-  }
-  if (p->fused_readout) {
-    for (int l = 0; l < 2; ++l)
-      HIP_TRY(launch_pack_dense(p->d_params + p->dense[l].off_w, p->d_packed + p->dense[l].pk_w, p->dense[l].in,
-                                p->dense[l].out, p->stream));
-  }
+  if ((rc = repack(p))) return rc;
   HIP_TRY(hipStreamSynchronize(p->stream));
   p->params_set = true;
   return IGN_OK;
@@ -583,6 +608,12 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       if ((rc = dev_upload(b.get(), &mb.d_step_code, scode))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_multi_ptr, multi_ptr))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_multi_rows, multi_rows))) return rc;
+      mb.h_order = std::move(order);
+      mb.h_len = std::move(len);
+      mb.h_step_ptr = std::move(step_ptr);
+      mb.h_step_code = std::move(scode);
+      mb.h_multi_ptr = std::move(multi_ptr);
+      mb.h_multi_rows = std::move(multi_rows);
       const int64_t tfloats = (mb.zero_row + 1 + mb.n_multi) * 3LL * H;
       if ((rc = dev_alloc(b.get(), &mb.d_table, tfloats))) return rc;
       HIP_TRY(hipMemset(mb.d_table, 0, (tfloats + 256) * sizeof(float)));   // zero row stays zero
@@ -621,11 +652,14 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_msg_ptr, ptr))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_msg_src, msrc))) return rc;
+      mb.h_order = std::move(order);
+      mb.h_msg_ptr = std::move(ptr);
+      mb.h_msg_src = std::move(msrc);
       mb.flops = (double)ND * gru_flops(DIN, H) + (double)mb.n_msgs * DIN;
       mb.bytes = (double)mb.n_msgs * (4.0 * DIN + 4) + (double)ND * (8.0 * H + 8);
       b->gru_steps += ND * p->T;
     }
-    b->mp.push_back(mb);
+    b->mp.push_back(std::move(mb));
   }
 
   // readout buffers
@@ -654,6 +688,7 @@ void ign_batch_destroy(ign_batch* b) {
     if (b->plan->stream) hipStreamSynchronize(b->plan->stream);
   }
   if (b->graph) hipGraphExecDestroy(b->graph);
+  if (b->train) train_state_destroy(b->train);
   for (void* a : b->allocs) hipFree(a);
   delete b;
 }

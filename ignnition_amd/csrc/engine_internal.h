@@ -36,12 +36,15 @@ struct CellP {
   int din, H;
   int64_t off_k, off_rk, off_b;   // raw Keras-layout params
   int64_t pk_w, pk_u, pk_b;       // packed fragments (in d_packed)
+  int64_t pk_wt = -1, pk_ut = -1; // backward: unscaled W^T / U^T fragments (pack_a)
   bool used = false;
 };
 
 struct DenseP {
   int in, out, act, use_bias;
+  float l2 = 0.f;
   int64_t off_w, off_b, pk_w;
+  int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
 };
 
 struct MPP {
@@ -69,6 +72,9 @@ struct MPB {
   int32_t* d_multi_ptr = nullptr;
   uint32_t* d_multi_rows = nullptr;
   double flops = 0, bytes = 0;    // algorithmic, per launch
+  // host copies of the index tables (the training path builds their transposes)
+  std::vector<int32_t> h_order, h_len, h_step_ptr, h_msg_ptr, h_multi_ptr;
+  std::vector<uint32_t> h_step_code, h_msg_src, h_multi_rows;
 };
 
 
@@ -114,6 +120,7 @@ struct ign_plan {
   std::vector<int> ev_kind;
   std::vector<double> ev_flops, ev_bytes;
   int ev_slot = 0;                // events recorded since ign_forward_begin
+  double* d_red = nullptr;        // loss reductions (training)
   bool use_graph = true;          // replay ign_forward as one captured hipGraph; IGN_HIP_GRAPH=0 disables
   ign_stats_t stats{};
 };
@@ -134,6 +141,7 @@ struct ign_batch {
   int64_t n_pred = 0, out_units = 1;
   int64_t edges_per_forward = 0, gru_steps = 0;
   std::vector<void*> allocs;
+  TrainState* train = nullptr;                  // ign_batch_enable_training
   // captured ign_forward (init .. readout) for replay; the event slots it records
   hipGraphExec_t graph = nullptr;
   bool graph_timing = false;
@@ -145,6 +153,7 @@ namespace ign {
 int set_device(int dev);
 int ensure_device(ign_plan* p);
 int dev_alloc(ign_batch* b, float** out, int64_t n);
+int repack(ign_plan* p);                      // fragments from d_params (set_params, optimizer)
 template <typename T>
 int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
   size_t n = std::max<size_t>(host.size(), 1);

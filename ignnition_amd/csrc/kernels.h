@@ -28,6 +28,8 @@ struct SeqGruArgs {
   int xcd_remap;             // XCD-aware tile order (speed only)
   int ablate;                // diagnostics: 1 = every step reads the zero row (see kernel)
   int64_t zero_slot;         // index in step_code of a padding entry (= zero row)
+  float* hs_save = nullptr;  // training: [n_steps + n_dst][H], order position p writes rows
+                             // step_ptr[p] + p (state before) .. + len[p] (after each step)
 };
 
 struct SumGruArgs {
@@ -42,6 +44,7 @@ struct SumGruArgs {
   const float* bias;
   int64_t n_dst;
   int xcd_remap;
+  float* x_save = nullptr;   // training: [rows][DIN] aggregated messages, by destination row
 };
 
 struct Readout3Args {

@@ -357,7 +357,7 @@ __device__ __forceinline__ void stage_frag_lds(f4* dst, const float* __restrict_
   for (int e = threadIdx.x; e < n; e += blockDim.x) dst[e] = s4[e];
 }
 
-template <int H>
+template <int H, bool SAVE>
 __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
   constexpr int NT = H / 16, KH = H / 4, K4 = KH / 4;
   __shared__ float sbias[4 * H];
@@ -388,6 +388,14 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
   int Lmax = L;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  float* hsv = nullptr;
+  if constexpr (SAVE) {          // training: keep h_0 .. h_L of the sequence for the backward
+    hsv = a.hs_save + (valid ? (int64_t)a.step_ptr[pos] + pos : 0) * H + 4 * g;
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
+    }
+  }
 
   uint32_t code = codes[0];
   for (int t = 0; t < Lmax; ++t) {
@@ -435,6 +443,12 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
         const float c = tanh2_(x[2][i][r] + rr * ah[i][r]);
         const float hn = c + z * (h[i][r] - c);
         h[i][r] = act ? hn : h[i][r];
+      }
+    }
+    if constexpr (SAVE) {
+      if (act && valid) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) st4(hsv + (int64_t)(t + 1) * H + 16 * i, h[i]);
       }
     }
     code = next;
@@ -501,6 +515,10 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
     f4 h[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    if (a.x_save && valid) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+    }
     gru_step<DIN, H>(W, sbias, x, h, g);
     if (valid) {
 #pragma unroll
@@ -551,6 +569,10 @@ __global__ __launch_bounds__(256) void sum_gru_wide_kernel(SumGruArgs a) {
   f4 h[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  if (a.x_save && valid) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+  }
   __syncthreads();
 
   const f4* W4 = reinterpret_cast<const f4*>(a.Wp);
@@ -668,6 +690,10 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_lds_kernel(SumGruArgs a) {
       const float* p = src_ptr(a.src, a.msg_src[m], DIN);
 #pragma unroll
       for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+    }
+    if (a.x_save && valid) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
     }
     // the weight reads are loop-invariant: an opaque offset keeps the compiler from hoisting
     // all 96 KB of them out of the tile loop into (spilled) registers
@@ -1230,13 +1256,13 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
   if (variant == 2) {
     const int64_t work = grid_for(args.n_dst, 64);
     if (h == 32) {
-      auto k = seq_gru2_kernel<32>;
+      auto k = args.hs_save ? seq_gru2_kernel<32, true> : seq_gru2_kernel<32, false>;
       hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
     } else if (h == 16) {
-      auto k = seq_gru2_kernel<16>;
+      auto k = args.hs_save ? seq_gru2_kernel<16, true> : seq_gru2_kernel<16, false>;
       hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
     } else if (h == 64) {
-      auto k = seq_gru2_kernel<64>;
+      auto k = args.hs_save ? seq_gru2_kernel<64, true> : seq_gru2_kernel<64, false>;
       hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
     } else return hipErrorInvalidValue;
     return hipGetLastError();

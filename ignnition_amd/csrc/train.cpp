@@ -1,0 +1,498 @@
+// train.cpp — the training step behind the C ABI: model_fn's TRAIN branch
+// (code/utils/generate_model.py:697-830 = GM).
+//
+//   ign_forward_train   the forward of ComnetModel.call (GM:384-658), keeping what the backward
+//                       needs: every hidden-state version (no ping-pong), the per-step states of
+//                       each ordered update, the aggregated messages of each sum update, and
+//                       the readout activations
+//   ign_backward        tf.gradients(total_loss, trainable_variables) (GM:790) for a given
+//                       dLoss/dpredictions, plus the Dense l2 regularizer terms (AUX:833-834)
+//   ign_mse_loss        MeanSquaredError over the batch's flat predictions (GM:716-753)
+//   ign_adam_step       Keras Adam with the host-evaluated ExponentialDecay rate (GM:797-818)
+//
+// Backward schedule: readout Dense stack in reverse, then the MP instances of the forward in
+// reverse order.  Per entity one gradient buffer tracks dLoss/d(current version); an MP turns
+// the gradient of its output version into that of its input version (GRU backward) and adds
+// the message gradients to its sources.  Weight gradients are row-contractions
+// (tsgemm_add) reduced in a fixed order: the result is deterministic.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "engine_internal.h"
+#include "train_kernels.h"
+
+struct MPTrain {
+  std::vector<float*> hs;     // sorted MPs: per iteration [(n_steps + n_dst)][H]
+  std::vector<float*> xs;     // sum MPs: per iteration [rows][DIN]
+  int64_t hs_rows = 0;
+  std::vector<int32_t*> tptr, tidx;   // per source slot: source row -> steps (sorted) / dst rows (sum)
+  std::vector<int64_t> trows;
+};
+
+struct MPRec {
+  int mi, it, v_in;
+  int src_v[IGN_MAX_SLOTS];
+};
+
+struct TrainState {
+  std::vector<std::vector<float*>> ver;   // [entity][version] hidden states
+  std::vector<int> cur;                   // current version per entity (after the forward)
+  std::vector<MPTrain> mp;
+  std::vector<MPRec> recs;
+  float* ga = nullptr;
+  float* gu = nullptr;
+  float* dx = nullptr;
+  float* dtab = nullptr;
+  std::vector<float*> dS[2];
+  std::vector<float*> act;                // readout activations of layers 0 .. L-2
+  float* dz[2] = {nullptr, nullptr};
+  float* part = nullptr;
+  float* ro_x = nullptr;                  // concatenated readout input (several input entities)
+  float* dro = nullptr;
+  bool forward_done = false;
+  std::vector<void*> allocs;
+};
+
+void train_state_destroy(TrainState* t) {
+  if (!t) return;
+  for (void* a : t->allocs) hipFree(a);
+  delete t;
+}
+
+namespace {
+
+int talloc(TrainState* t, float** out, int64_t n) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, (std::max<int64_t>(n, 0) + 256) * sizeof(float));
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: hipMalloc(%lld floats): %s", (long long)n,
+                                   hipGetErrorString(e));
+  t->allocs.push_back(p);
+  *out = static_cast<float*>(p);
+  return IGN_OK;
+}
+
+template <typename T>
+int tupload(TrainState* t, T** out, const std::vector<T>& h) {
+  void* p = nullptr;
+  size_t n = std::max<size_t>(h.size(), 1);
+  hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: hipMalloc: %s", hipGetErrorString(e));
+  t->allocs.push_back(p);
+  if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = static_cast<T*>(p);
+  return IGN_OK;
+}
+
+// CSR of (key, value) pairs over n_keys keys, values kept in insertion order per key
+void build_csr(int64_t n_keys, const std::vector<std::pair<int64_t, int32_t>>& kv, std::vector<int32_t>& ptr,
+               std::vector<int32_t>& idx) {
+  ptr.assign(n_keys + 1, 0);
+  for (auto& p : kv) ptr[p.first + 1]++;
+  for (int64_t k = 0; k < n_keys; ++k) ptr[k + 1] += ptr[k];
+  idx.resize(kv.size());
+  std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
+  for (auto& p : kv) idx[fill[p.first]++] = p.second;
+}
+
+int check_train(ign_plan* p, ign_batch* b) {
+  if (!p || !b) return fail(IGN_ERR_INVALID, "null argument");
+  if (b->plan != p) return fail(IGN_ERR_INVALID, "batch was created for another plan");
+  if (!b->train) return fail(IGN_ERR_INVALID, "training not enabled on this batch (ign_batch_enable_training)");
+  if (!p->params_set) return fail(IGN_ERR_INVALID, "parameters not set (ign_plan_set_params)");
+  return set_device(p->device);
+}
+
+// project every source of sorted MP mb into its table, from the given source states
+int build_table(ign_plan* p, const MPP& mp, const MPB& mb, const CellP& cp, const float* const* src) {
+  const int W3 = 3 * cp.H;
+  for (size_t s = 0; s < mp.src.size(); ++s)
+    HIP_TRY(launch_project(src[s], mb.src_rows[s], p->d_packed + cp.pk_w, p->d_packed + cp.pk_b,
+                           mb.d_table + mb.src_off[s] * W3, s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr, mp.din,
+                           cp.H, p->stream));
+  if (mb.n_multi)
+    HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3,
+                             mb.d_table + mb.zero_row * W3, p->stream));
+  return IGN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
+  if (!p || !b) return fail(IGN_ERR_INVALID, "null argument");
+  if (b->plan != p) return fail(IGN_ERR_INVALID, "batch was created for another plan");
+  if (b->train) return IGN_OK;
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  const int E = (int)p->ents.size();
+  for (int e = 0; e < E; ++e)
+    if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
+  for (auto& cp : p->cells)
+    if (cp.used && cp.pk_wt < 0)
+      return fail(IGN_ERR_UNSUPPORTED, "no backward kernel for GRU shape (input %d, units %d)", cp.din, cp.H);
+  std::unique_ptr<TrainState, void (*)(TrainState*)> t(new TrainState(), train_state_destroy);
+  const int64_t P = b->n_pred;
+  // hidden-state versions: 1 + T x (MPs updating the entity)
+  std::vector<int> nver(E, 1);
+  for (auto& mp : p->mps) nver[mp.dst] += p->T;
+  t->ver.resize(E);
+  t->cur.assign(E, 0);
+  for (int e = 0; e < E; ++e) {
+    const int64_t n = b->rows[e] * p->ents[e].hidden_dim;
+    for (int v = 0; v < nver[e]; ++v) {
+      float* f = nullptr;
+      if ((rc = talloc(t.get(), &f, n))) return rc;
+      t->ver[e].push_back(f);
+    }
+    for (int k = 0; k < 2; ++k) {
+      float* f = nullptr;
+      if ((rc = talloc(t.get(), &f, n))) return rc;
+      t->dS[k].push_back(f);
+    }
+  }
+  int64_t ga_n = 0, gu_n = 0, dx_n = 0, dtab_n = 0, part_n = 0;
+  auto need_part = [&](int64_t rows, int M, int N) {
+    part_n = std::max(part_n, tsgemm_partial_floats(rows, M, N));
+  };
+  for (size_t mi = 0; mi < p->mps.size(); ++mi) {
+    const MPP& mp = p->mps[mi];
+    const MPB& mb = b->mp[mi];
+    const CellP& cp = p->cells[mp.cell];
+    const int H = cp.H, DIN = mp.din, S = (int)mp.src.size();
+    MPTrain mt;
+    std::vector<std::vector<std::pair<int64_t, int32_t>>> kv(S);
+    if (mb.sorted) {
+      mt.hs_rows = mb.n_steps + mb.n_dst;
+      for (int it = 0; it < p->T; ++it) {
+        float* f = nullptr;
+        if ((rc = talloc(t.get(), &f, mt.hs_rows * H))) return rc;
+        mt.hs.push_back(f);
+      }
+      // source row -> steps whose input contains it (directly or through a pre-summed row)
+      auto add_row = [&](uint32_t trow, int32_t step) {
+        for (int s = S - 1; s >= 0; --s)
+          if ((int64_t)trow >= mb.src_off[s]) {
+            kv[s].push_back({(int64_t)trow - mb.src_off[s], step});
+            return;
+          }
+      };
+      for (int64_t pos = 0; pos < mb.n_dst; ++pos)
+        for (int32_t tt = 0; tt < mb.h_len[pos]; ++tt) {
+          const int32_t i = mb.h_step_ptr[pos] + tt;
+          const uint32_t code = mb.h_step_code[i];
+          if ((int64_t)code < mb.zero_row) {
+            add_row(code, i);
+          } else if ((int64_t)code > mb.zero_row) {
+            const int64_t k = code - mb.zero_row - 1;
+            for (int32_t m = mb.h_multi_ptr[k]; m < mb.h_multi_ptr[k + 1]; ++m) add_row(mb.h_multi_rows[m], i);
+          }
+        }
+      ga_n = std::max(ga_n, mb.n_steps * 3 * H);
+      gu_n = std::max(gu_n, mt.hs_rows * 3 * H);
+      need_part(mt.hs_rows, H, 3 * H);
+      for (int s = 0; s < S; ++s) {
+        dtab_n = std::max(dtab_n, mb.src_rows[s] * 3 * H);
+        need_part(mb.src_rows[s], DIN, 3 * H);
+      }
+    } else {
+      for (int it = 0; it < p->T; ++it) {
+        float* f = nullptr;
+        if ((rc = talloc(t.get(), &f, mb.n_dst * DIN))) return rc;
+        mt.xs.push_back(f);
+      }
+      for (int64_t pos = 0; pos < mb.n_dst; ++pos)
+        for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) {
+          const uint32_t code = mb.h_msg_src[m];
+          kv[code >> IGN_SLOT_SHIFT].push_back({(int64_t)(code & IGN_ROW_MASK), mb.h_order[pos]});
+        }
+      ga_n = std::max(ga_n, mb.n_dst * 3 * H);
+      gu_n = std::max(gu_n, mb.n_dst * 3 * H);
+      dx_n = std::max(dx_n, mb.n_dst * DIN);
+      need_part(mb.n_dst, std::max(DIN, H), 3 * H);
+    }
+    need_part(std::max<int64_t>(mb.n_steps, mb.n_dst), 1, 3 * H);   // colsum
+    for (int s = 0; s < S; ++s) {
+      const int se = mp.src[s].entity;
+      std::vector<int32_t> ptr, idx;
+      build_csr(b->rows[se], kv[s], ptr, idx);
+      int32_t *dp = nullptr, *di = nullptr;
+      if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
+      mt.tptr.push_back(dp);
+      mt.tidx.push_back(di);
+      mt.trows.push_back(b->rows[se]);
+    }
+    t->mp.push_back(std::move(mt));
+  }
+  if ((rc = talloc(t.get(), &t->ga, ga_n)) || (rc = talloc(t.get(), &t->gu, gu_n)) ||
+      (rc = talloc(t.get(), &t->dx, dx_n)) || (rc = talloc(t.get(), &t->dtab, dtab_n)))
+    return rc;
+  // readout
+  int64_t widest = p->ro_width;
+  for (size_t l = 0; l < p->dense.size(); ++l) {
+    const DenseP& d = p->dense[l];
+    widest = std::max<int64_t>(widest, d.out);
+    need_part(P, d.in, d.out);
+    if (l + 1 < p->dense.size()) {
+      float* f = nullptr;
+      if ((rc = talloc(t.get(), &f, P * d.out))) return rc;
+      t->act.push_back(f);
+    }
+  }
+  if ((rc = talloc(t.get(), &t->dz[0], P * widest)) || (rc = talloc(t.get(), &t->dz[1], P * widest))) return rc;
+  if (p->ro_in.size() > 1 &&
+      ((rc = talloc(t.get(), &t->ro_x, P * p->ro_width)) || (rc = talloc(t.get(), &t->dro, P * p->ro_width))))
+    return rc;
+  if ((rc = talloc(t.get(), &t->part, part_n))) return rc;
+  b->train = t.release();
+  return IGN_OK;
+}
+
+int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = check_train(p, b);
+  if (rc) return rc;
+  TrainState* t = b->train;
+  hipStream_t st = p->stream;
+  const int E = (int)p->ents.size();
+  for (int e = 0; e < E; ++e) {   // GM:396-400
+    HIP_TRY(launch_init_state(t->ver[e][0], b->d_feat[e], b->rows[e], p->ents[e].hidden_dim,
+                              p->ents[e].feature_total, st));
+    t->cur[e] = 0;
+  }
+  t->recs.clear();
+  for (int it = 0; it < p->T; ++it) {
+    for (int mi = 0; mi < (int)p->mps.size(); ++mi) {
+      const MPP& mp = p->mps[mi];
+      const MPB& mb = b->mp[mi];
+      const CellP& cp = p->cells[mp.cell];
+      MPTrain& mt = t->mp[mi];
+      MPRec rec{mi, it, t->cur[mp.dst], {0, 0, 0, 0}};
+      SrcBases sb{};
+      const float* srcs[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+      for (size_t s = 0; s < mp.src.size(); ++s) {
+        const int se = mp.src[s].entity;
+        rec.src_v[s] = t->cur[se];
+        srcs[s] = sb.base[s] = t->ver[se][t->cur[se]];
+      }
+      const float* hin = t->ver[mp.dst][rec.v_in];
+      float* hout = t->ver[mp.dst][rec.v_in + 1];
+      if (mp.sorted) {
+        if ((rc = build_table(p, mp, mb, cp, srcs))) return rc;
+        SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
+                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, 0, mb.n_steps};
+        a.hs_save = mt.hs[it];
+        HIP_TRY(launch_seq_gru(a, cp.H, 2, st));
+      } else {
+        SumGruArgs a{hin, hout, sb, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, p->d_packed + cp.pk_w,
+                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
+        a.x_save = mt.xs[it];
+        HIP_TRY(launch_sum_gru(a, mp.din, cp.H, cp.H == 64 ? 3 : p->sum_variant, st));
+      }
+      t->cur[mp.dst] = rec.v_in + 1;
+      t->recs.push_back(rec);
+    }
+  }
+  // readout with every activation kept (GM:611-629)
+  const int64_t P = b->n_pred;
+  const float* x = t->ver[p->ro_in[0]][t->cur[p->ro_in[0]]];
+  if (p->ro_in.size() > 1) {
+    int col = 0;
+    for (int e : p->ro_in) {
+      HIP_TRY(launch_concat_cols(t->ro_x, P, p->ro_width, col, t->ver[e][t->cur[e]], p->ents[e].hidden_dim, st));
+      col += p->ents[e].hidden_dim;
+    }
+    x = t->ro_x;
+  }
+  const float* in = x;
+  int in_stride = p->ro_width;
+  for (size_t l = 0; l < p->dense.size(); ++l) {
+    const DenseP& d = p->dense[l];
+    float* o = l + 1 == p->dense.size() ? b->d_pred : t->act[l];
+    HIP_TRY(launch_dense_generic(in, P, d.in, in_stride, p->d_params + d.off_w, d.use_bias ? p->d_params + d.off_b : nullptr,
+                                 d.out, d.act, o, st));
+    in = o;
+    in_stride = d.out;
+  }
+  if (pred_out) {
+    HIP_TRY(hipMemcpyAsync(pred_out, b->d_pred, P * b->out_units * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  t->forward_done = true;
+  return IGN_OK;
+}
+
+int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
+  int rc = check_train(p, b);
+  if (rc) return rc;
+  if (!dpred || !grads) return fail(IGN_ERR_INVALID, "null argument");
+  TrainState* t = b->train;
+  if (!t->forward_done) return fail(IGN_ERR_INVALID, "ign_backward needs a preceding ign_forward_train");
+  hipStream_t st = p->stream;
+  const int E = (int)p->ents.size();
+  const int64_t P = b->n_pred;
+  HIP_TRY(hipMemsetAsync(grads, 0, p->n_params * sizeof(float), st));
+  std::vector<int> dcur(E, 0);
+  for (int e = 0; e < E; ++e)
+    HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, b->rows[e] * p->ents[e].hidden_dim * sizeof(float), st));
+
+  // ---- readout (GM:611-629) in reverse
+  const int L = (int)p->dense.size();
+  const float* X = p->ro_in.size() > 1 ? t->ro_x : t->ver[p->ro_in[0]][t->cur[p->ro_in[0]]];
+  int zi = 0;
+  HIP_TRY(launch_act_bwd(dpred, b->d_pred, P * p->dense[L - 1].out, p->dense[L - 1].act, t->dz[0], st));
+  for (int l = L - 1; l >= 0; --l) {
+    const DenseP& d = p->dense[l];
+    const float* A = l == 0 ? X : t->act[l - 1];
+    HIP_TRY(launch_tsgemm_add(A, d.in, t->dz[zi], d.out, P, d.in, d.out, t->part, grads + d.off_w, st));
+    if (d.use_bias) HIP_TRY(launch_colsum_add(t->dz[zi], d.out, P, d.out, t->part, grads + d.off_b, st));
+    if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)d.in * d.out, st));
+    float* out;
+    int act = -1, acc = 0;
+    const float* aprev = nullptr;
+    if (l > 0) {
+      out = t->dz[1 - zi];
+      act = p->dense[l - 1].act;
+      aprev = t->act[l - 1];
+    } else if (p->ro_in.size() > 1) {
+      out = t->dro;
+    } else {
+      out = t->dS[0][p->ro_in[0]];
+      acc = 1;
+    }
+    if (d.pk_wt >= 0)
+      HIP_TRY(launch_row_gemm_t(t->dz[zi], P, d.out, p->d_packed + d.pk_wt, d.in, out, acc, act, aprev, st));
+    else
+      HIP_TRY(launch_row_gemm_t_generic(t->dz[zi], P, d.out, p->d_params + d.off_w, d.in, out, acc, act, aprev, st));
+    zi = 1 - zi;
+  }
+  if (p->ro_in.size() > 1) {   // split dX by columns into the input entities (concat axis 1)
+    int col = 0;
+    for (int e : p->ro_in) {
+      const int h = p->ents[e].hidden_dim;
+      HIP_TRY(launch_split_cols_add(t->dS[0][e], P, h, t->dro, p->ro_width, col, st));
+      col += h;
+    }
+  }
+
+  // ---- MP instances in reverse (GM:404-603)
+  for (int ri = (int)t->recs.size() - 1; ri >= 0; --ri) {
+    const MPRec& rec = t->recs[ri];
+    const MPP& mp = p->mps[rec.mi];
+    const MPB& mb = b->mp[rec.mi];
+    const CellP& cp = p->cells[mp.cell];
+    const MPTrain& mt = t->mp[rec.mi];
+    const int dst = mp.dst, H = cp.H, DIN = mp.din, H3 = 3 * cp.H;
+    float* dh_in = t->dS[dcur[dst]][dst];
+    float* dh_out = t->dS[1 - dcur[dst]][dst];
+    const float* srcs[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+    for (size_t s = 0; s < mp.src.size(); ++s) srcs[s] = t->ver[mp.src[s].entity][rec.src_v[s]];
+    float* gk = grads + cp.off_k;
+    float* grk = grads + cp.off_rk;
+    float* gb = grads + cp.off_b;
+    if (mp.sorted) {
+      if ((rc = build_table(p, mp, mb, cp, srcs))) return rc;
+      HIP_TRY(hipMemsetAsync(t->gu, 0, mt.hs_rows * H3 * sizeof(float), st));
+      SeqBwdArgs a{mt.hs[rec.it], mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
+                   p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
+                   t->ga, t->gu, mb.n_dst};
+      HIP_TRY(launch_seq_gru_bwd(a, H, st));
+      HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, st));
+      HIP_TRY(launch_colsum_add(t->gu, H3, mt.hs_rows, H3, t->part, gb + H3, st));
+      HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, gb, st));
+      for (size_t s = 0; s < mp.src.size(); ++s) {
+        const int se = mp.src[s].entity;
+        HIP_TRY(launch_csr_gather_add(t->dtab, mt.trows[s], mt.tptr[s], mt.tidx[s], t->ga, H3, 0, st));
+        HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, st));
+        float* target = se == dst ? dh_out : t->dS[dcur[se]][se];
+        HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, 1, -1, nullptr, st));
+      }
+    } else {
+      const float* hin = t->ver[dst][rec.v_in];
+      SumBwdArgs a{mt.xs[rec.it], hin, p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b,
+                   p->d_packed + cp.pk_wt, p->d_packed + cp.pk_ut, dh_in, dh_out, t->dx, t->ga, t->gu, mb.n_dst};
+      HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
+      HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, st));
+      HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, st));
+      HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_dst, H3, t->part, gb, st));
+      HIP_TRY(launch_colsum_add(t->gu, H3, mb.n_dst, H3, t->part, gb + H3, st));
+      for (size_t s = 0; s < mp.src.size(); ++s) {
+        const int se = mp.src[s].entity;
+        float* target = se == dst ? dh_out : t->dS[dcur[se]][se];
+        HIP_TRY(launch_csr_gather_add(target, mt.trows[s], mt.tptr[s], mt.tidx[s], t->dx, DIN, 1, st));
+      }
+    }
+    dcur[dst] = 1 - dcur[dst];
+  }
+  return IGN_OK;
+}
+
+int ign_mse_loss(ign_plan* p, const float* pred, const float* labels, int64_t n, float* dpred, double* loss) {
+  if (!p || !pred || !labels || !dpred) return fail(IGN_ERR_INVALID, "null argument");
+  if (n <= 0) return fail(IGN_ERR_INVALID, "empty prediction vector");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  constexpr int NB = 256;
+  if (!p->d_red) HIP_TRY(hipMalloc(&p->d_red, 1024 * sizeof(double)));
+  HIP_TRY(launch_mse(pred, labels, n, dpred, p->d_red, NB, p->stream));
+  if (loss) {
+    double h[NB];
+    HIP_TRY(hipMemcpyAsync(h, p->d_red, NB * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    double s = 0;
+    for (int i = 0; i < NB; ++i) s += h[i];
+    *loss = s / (double)n;
+  }
+  return IGN_OK;
+}
+
+int ign_l2_loss(ign_plan* p, double* loss) {
+  if (!p || !loss) return fail(IGN_ERR_INVALID, "null argument");
+  if (!p->params_set) return fail(IGN_ERR_INVALID, "parameters not set (ign_plan_set_params)");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  constexpr int NB = 64;
+  if (!p->d_red) HIP_TRY(hipMalloc(&p->d_red, 1024 * sizeof(double)));
+  double total = 0;
+  for (auto& d : p->dense) {
+    if (d.l2 == 0.f) continue;
+    HIP_TRY(launch_sumsq(p->d_params + d.off_w, (int64_t)d.in * d.out, p->d_red, NB, p->stream));
+    double h[NB];
+    HIP_TRY(hipMemcpyAsync(h, p->d_red, NB * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    double s = 0;
+    for (int i = 0; i < NB; ++i) s += h[i];
+    total += (double)d.l2 * s;
+  }
+  *loss = total;
+  return IGN_OK;
+}
+
+int ign_adam_step(ign_plan* p, const float* grads, float* m, float* v, int64_t iteration, float lr, float beta1,
+                  float beta2, float epsilon) {
+  if (!p || !grads || !m || !v) return fail(IGN_ERR_INVALID, "null argument");
+  if (!p->params_set) return fail(IGN_ERR_INVALID, "parameters not set (ign_plan_set_params)");
+  if (iteration < 0) return fail(IGN_ERR_INVALID, "negative iteration");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  const double tstep = (double)iteration + 1.0;
+  const double lr_t = (double)lr * std::sqrt(1.0 - std::pow((double)beta2, tstep)) / (1.0 - std::pow((double)beta1, tstep));
+  HIP_TRY(launch_adam(p->d_params, grads, m, v, p->n_params, (float)lr_t, beta1, beta2, epsilon, p->stream));
+  return repack(p);
+}
+
+int ign_plan_get_params(ign_plan* p, float* host_out) {
+  if (!p || !host_out) return fail(IGN_ERR_INVALID, "null argument");
+  if (!p->params_set) return fail(IGN_ERR_INVALID, "parameters not set (ign_plan_set_params)");
+  int rc = ensure_device(p);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(host_out, p->d_params, p->n_params * sizeof(float), hipMemcpyDeviceToHost, p->stream));
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  return IGN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// train_kernels.h — argument blocks and launchers of the backward / optimizer kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// Backward of the ordered update (reverse-time GRU, AUX:767-796).
+struct SeqBwdArgs {
+  const float* hs;           // [n_steps + n_dst][H]: order position p owns rows step_ptr[p]+p .. +len[p]
+                             // (h_0 = state before the MP, then the state after every step)
+  const float* table;        // the MP's projected table (pre-scaled, as the forward built it)
+  const int32_t* order;
+  const int32_t* len;
+  const int32_t* step_ptr;
+  const uint32_t* step_code;
+  const float* Up;           // forward recurrent fragments (pre-scaled)
+  const float* bias;         // forward combined biases [4][H] (pre-scaled)
+  const float* Ut;           // U^T fragments (unscaled): tiles over H, k over 3H
+  const float* dh_in;        // [rows][H] dLoss/d(state after the MP)
+  float* dh_out;             // [rows][H] dLoss/d(state before the MP), GRU part
+  float* ga;                 // [n_steps][3H]  dLoss/d(x.W + b_in) per step
+  float* gu;                 // [n_steps + n_dst][3H] dLoss/d(h.U + b_rec), rows aligned with hs (pre-zeroed)
+  int64_t n_dst;
+};
+
+// Backward of the sum update (AUX:752-765): one GRU step per destination row.
+struct SumBwdArgs {
+  const float* x;            // [rows][DIN] aggregated messages saved by the forward
+  const float* h;            // [rows][H] state before the MP
+  const float* Wp;           // forward fragments (pre-scaled)
+  const float* Up;
+  const float* bias;
+  const float* Wt;           // W^T fragments (unscaled): tiles over DIN, k over 3H
+  const float* Ut;           // U^T fragments (unscaled): tiles over H, k over 3H
+  const float* dh_in;
+  float* dh_out;
+  float* dx;                 // [rows][DIN] dLoss/dx
+  float* ga;                 // [rows][3H]
+  float* gu;                 // [rows][3H]
+  int64_t n_dst;
+};
+
+hipError_t launch_pack_a(const float* M, int rows, int cols, float* out, hipStream_t st);
+bool bwd_shape_supported(int din, int h);
+hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st);
+hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);
+// out[r][:cols] (+)= sum over k in [ptr[r], ptr[r+1]) of in[idx[k]][:cols]   (cols % 4 == 0)
+hipError_t launch_csr_gather_add(float* out, int64_t n_rows, const int32_t* ptr, const int32_t* idx,
+                                 const float* in, int cols, int accumulate, hipStream_t st);
+// out[r][m] (+)= sum_k in[r][k] * Mat[m][k] (Mat packed by launch_pack_a, K % 16 == 0, M % 16 == 0),
+// then (act >= 0) multiplied by act'(aprev[r][m]) given the activation values aprev.
+bool row_gemm_supported(int K, int M);
+hipError_t launch_row_gemm_t(const float* in, int64_t n, int K, const float* Ap, int M, float* out, int accumulate,
+                             int act, const float* aprev, hipStream_t st);
+// generic VALU version (any K, M): out[r][m] (+)= sum_k in[r][k] * Mat[m][k] (Mat row-major [M][K])
+hipError_t launch_row_gemm_t_generic(const float* in, int64_t n, int K, const float* Mat, int M, float* out,
+                                     int accumulate, int act, const float* aprev, hipStream_t st);
+// dst[r][:width] += src[r][col0 : col0 + width]
+hipError_t launch_split_cols_add(float* dst, int64_t n, int width, const float* src, int src_stride, int col0,
+                                 hipStream_t st);
+// dz[r][c] = da[r][c] * act'(a[r][c])
+hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, float* dz, hipStream_t st);
+// C[M][N] += sum_r A[r][:M]^T B[r][:N]; partial sums per row chunk, reduced in a fixed order
+int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N);
+hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
+                             float* part, float* C, hipStream_t st);
+// C[N] += sum_r B[r][:N]
+hipError_t launch_colsum_add(const float* B, int ldb, int64_t n_rows, int N, float* part, float* C, hipStream_t st);
+// y[i] += alpha * x[i]
+hipError_t launch_axpy(float* y, const float* x, float alpha, int64_t n, hipStream_t st);
+// dpred = 2 (pred - label) / n ; part[b] = partial sums of (pred - label)^2
+hipError_t launch_mse(const float* pred, const float* label, int64_t n, float* dpred, double* part, int nblk,
+                      hipStream_t st);
+// part[b] = partial sums of x^2
+hipError_t launch_sumsq(const float* x, int64_t n, double* part, int nblk, hipStream_t st);
+hipError_t launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float b1, float b2,
+                       float eps, hipStream_t st);

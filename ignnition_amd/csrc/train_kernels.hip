@@ -1,0 +1,626 @@
+// train_kernels.hip — gfx950 kernels of the training step (backward + optimizer).
+//
+// Same MFMA conventions as kernels.hip (transposed formulation D[unit][row], k order
+// k(s, g) = 16(s>>2) + 4g + (s&3), so an accumulator tile is the next contraction's B operand).
+// The backward contractions that run along a row (dh = gu.U^T, dx = ga.W^T, readout dX = dz.W^T)
+// use "A" fragments of the matrix itself (pack_a: tiles over its rows, k over its columns).
+// Weight gradients are contractions over rows (sum_r A[r]^T B[r]): tsgemm_kernel puts the rows
+// on the MFMA k axis and writes one partial tile per row chunk; reduce_add sums the chunks in a
+// fixed order, so every gradient is deterministic.
+//
+// Gate math of the backward (Keras GRUCell v2, reset_after=True; u = h.U + b_rec, a = x.W + b_in):
+//   z = s(a_z + u_z), r = s(a_r + u_r), c = tanh(a_h + r u_h), h' = z h + (1 - z) c
+//   dz = dh' (h - c) z (1 - z);  dc = dh' (1 - z)(1 - c^2);  dr = dc u_h r (1 - r)
+//   da = (dz, dr, dc);  du = (dz, dr, dc r);  dh = dh' z + du.U^T;  dx = da.W^T
+// z, r, c are recomputed exactly as the forward computed them (pre-scaled pre-activations,
+// sig2_/tanh2_), u_h is unscaled from the pre-scaled accumulator.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+#include "train_kernels.h"
+
+namespace {
+
+constexpr float kInv2Log2e = 0.34657359027997264f;   // 1 / (2 log2 e)
+
+__device__ __forceinline__ float act_grad(float a, int act) {
+  // derivative of the activation expressed through its output a
+  switch (act) {
+    case IGN_K_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case IGN_K_ACT_SELU: {
+      const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
+      return a > 0.f ? lam : a + la;
+    }
+    case IGN_K_ACT_SIGMOID: return a * (1.f - a);
+    case IGN_K_ACT_TANH: return 1.f - a * a;
+    default: return 1.f;
+  }
+}
+
+// pack_a: Mat [rows][cols] row-major -> float4-grouped A fragments, tiles over rows, k over cols:
+//   element ((t * KS/4 + s/4) * 64 + lane) * 4 + s%4 = Mat[16t + (lane&15)][k(s, lane>>4)], KS = cols/4
+__global__ void pack_a_kernel(const float* __restrict__ M, int rows, int cols, float* __restrict__ out) {
+  const int64_t total = (int64_t)rows * cols;
+  const int KS = cols / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(i & 3);
+    const int lane = (int)((i >> 2) & 63);
+    const int64_t f = i >> 8;
+    const int s = (int)((f % (KS / 4)) * 4 + q);
+    const int t = (int)(f / (KS / 4));
+    const int k = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
+    out[i] = M[(int64_t)(16 * t + (lane & 15)) * cols + k];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ordered update backward.  One wave = the forward's 16-row tile (same order), steps in reverse.
+// Lanes whose sequence is shorter skip the step (mask): their gradient passes through.
+template <int H>
+__global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
+  constexpr int NT = H / 16, KH = H / 4, K3 = 3 * H / 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = pos < a.n_dst;
+  const int row = valid ? a.order[pos] : 0;
+  const int L = valid ? a.len[pos] : 0;
+  const int64_t sp = valid ? a.step_ptr[pos] : 0;
+  const int64_t hbase = valid ? sp + pos : 0;
+  f4 dh[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dh[t] = valid ? ld4(a.dh_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  int Lmax = L;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  f4 bh[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bh[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+
+  for (int step = Lmax - 1; step >= 0; --step) {
+    const bool act = step < L;
+    const int64_t tt = act ? step : 0;
+    const int64_t i = sp + tt;
+    const int64_t hr = hbase + tt;
+    f4 hp[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
+    const uint32_t code = a.step_code[i];
+    f4 x[3][NT];
+#pragma unroll
+    for (int G = 0; G < 3; ++G)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
+    f4 az[NT], ar[NT], ah[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      az[t] = f4{0, 0, 0, 0};
+      ar[t] = f4{0, 0, 0, 0};
+      ah[t] = bh[t];
+    }
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      const float hb = hp[s >> 2][s & 3];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        az[t] = MFMA(a.Up[frag_idx(0 * NT + t, s, KH, lane)], hb, az[t]);
+        ar[t] = MFMA(a.Up[frag_idx(1 * NT + t, s, KH, lane)], hb, ar[t]);
+        ah[t] = MFMA(a.Up[frag_idx(2 * NT + t, s, KH, lane)], hb, ah[t]);
+      }
+    }
+    f4 gz[NT], gr[NT], gh[NT], guh[NT], acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[t][r] + x[0][t][r]);
+        const float rr = sig2_(ar[t][r] + x[1][t][r]);
+        const float c = tanh2_(x[2][t][r] + rr * ah[t][r]);
+        const float uh = ah[t][r] * kInv2Log2e;
+        const float d = act ? dh[t][r] : 0.f;
+        const float dzp = d * (hp[t][r] - c) * z * (1.f - z);
+        const float dcp = d * (1.f - z) * (1.f - c * c);
+        const float drp = dcp * uh * rr * (1.f - rr);
+        gz[t][r] = dzp;
+        gr[t][r] = drp;
+        gh[t][r] = dcp;
+        guh[t][r] = dcp * rr;
+        acc[t][r] = dh[t][r] * z;
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float* pa = a.ga + i * (3 * H) + 16 * t + 4 * g;
+        st4(pa, gz[t]);
+        st4(pa + H, gr[t]);
+        st4(pa + 2 * H, gh[t]);
+        float* pu = a.gu + hr * (3 * H) + 16 * t + 4 * g;
+        st4(pu, gz[t]);
+        st4(pu + H, gr[t]);
+        st4(pu + 2 * H, guh[t]);
+      }
+    }
+    // dh_prev = dh' z + du . U^T   (k over the 3H gate units, gate-major)
+#pragma unroll
+    for (int s = 0; s < K3; ++s) {
+      const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
+      const float b = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = MFMA(a.Ut[frag_idx(t, s, K3, lane)], b, acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dh[t][r] = act ? acc[t][r] : dh[t][r];
+  }
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.dh_out + (int64_t)row * H + 16 * t + 4 * g, dh[t]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sum update backward: one wave = 16 destination rows (identity order).
+template <int DIN, int H>
+__global__ __launch_bounds__(256) void sum_gru_bwd_kernel(SumBwdArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, KX = DIN / 4, KH = H / 4, K3 = 3 * H / 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = row < a.n_dst;
+  const int64_t rr0 = valid ? row : 0;
+  f4 x[NC], h[NT], dh[NT];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = ld4(a.x + rr0 * DIN + 16 * c + 4 * g);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    h[t] = ld4(a.h + rr0 * H + 16 * t + 4 * g);
+    dh[t] = valid ? ld4(a.dh_in + rr0 * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  }
+  f4 az[NT], ar[NT], ax[NT], ah[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    az[t] = ld4(a.bias + 0 * H + 16 * t + 4 * g);
+    ar[t] = ld4(a.bias + 1 * H + 16 * t + 4 * g);
+    ax[t] = ld4(a.bias + 2 * H + 16 * t + 4 * g);
+    ah[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+  }
+#pragma unroll
+  for (int s = 0; s < KX; ++s) {
+    const float xb = x[s >> 2][s & 3];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      az[t] = MFMA(a.Wp[frag_idx(0 * NT + t, s, KX, lane)], xb, az[t]);
+      ar[t] = MFMA(a.Wp[frag_idx(1 * NT + t, s, KX, lane)], xb, ar[t]);
+      ax[t] = MFMA(a.Wp[frag_idx(2 * NT + t, s, KX, lane)], xb, ax[t]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KH; ++s) {
+    const float hb = h[s >> 2][s & 3];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      az[t] = MFMA(a.Up[frag_idx(0 * NT + t, s, KH, lane)], hb, az[t]);
+      ar[t] = MFMA(a.Up[frag_idx(1 * NT + t, s, KH, lane)], hb, ar[t]);
+      ah[t] = MFMA(a.Up[frag_idx(2 * NT + t, s, KH, lane)], hb, ah[t]);
+    }
+  }
+  f4 gz[NT], gr[NT], gh[NT], guh[NT], acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = sig2_(az[t][r]);
+      const float rr = sig2_(ar[t][r]);
+      const float c = tanh2_(ax[t][r] + rr * ah[t][r]);
+      const float uh = ah[t][r] * kInv2Log2e;
+      const float d = dh[t][r];
+      const float dzp = d * (h[t][r] - c) * z * (1.f - z);
+      const float dcp = d * (1.f - z) * (1.f - c * c);
+      const float drp = dcp * uh * rr * (1.f - rr);
+      gz[t][r] = dzp;
+      gr[t][r] = drp;
+      gh[t][r] = dcp;
+      guh[t][r] = dcp * rr;
+      acc[t][r] = d * z;
+    }
+  }
+  f4 dxa[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) dxa[c] = f4{0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < K3; ++s) {
+    const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
+    const float ba = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : gh[t2][s & 3];
+    const float bu = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dxa[c] = MFMA(a.Wt[frag_idx(c, s, K3, lane)], ba, dxa[c]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = MFMA(a.Ut[frag_idx(t, s, K3, lane)], bu, acc[t]);
+  }
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      st4(a.dh_out + row * H + 16 * t + 4 * g, acc[t]);
+      float* pa = a.ga + row * (3 * H) + 16 * t + 4 * g;
+      st4(pa, gz[t]);
+      st4(pa + H, gr[t]);
+      st4(pa + 2 * H, gh[t]);
+      float* pu = a.gu + row * (3 * H) + 16 * t + 4 * g;
+      st4(pu, gz[t]);
+      st4(pu + H, gr[t]);
+      st4(pu + 2 * H, guh[t]);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) st4(a.dx + row * DIN + 16 * c + 4 * g, dxa[c]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, const int32_t* __restrict__ ptr,
+                                      const int32_t* __restrict__ idx, const float* __restrict__ in, int cols,
+                                      int accumulate) {
+  const int q = cols >> 2;
+  const int64_t total = n_rows * q;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / q;
+    const int c = (int)(e - r * q) * 4;
+    f4 acc = accumulate ? ld4(out + r * cols + c) : f4{0, 0, 0, 0};
+    for (int k = ptr[r]; k < ptr[r + 1]; ++k) acc += ld4(in + (int64_t)idx[k] * cols + c);
+    st4(out + r * cols + c, acc);
+  }
+}
+
+// out[r][m] (+)= sum_k in[r][k] Mat[m][k]; optional *= act'(aprev[r][m]).  One wave = 16 rows.
+template <int K, int M>
+__global__ __launch_bounds__(256) void row_gemm_t_kernel(const float* __restrict__ in, int64_t n,
+                                                         const float* __restrict__ Ap, float* __restrict__ out,
+                                                         int accumulate, int act, const float* __restrict__ aprev) {
+  constexpr int KS = K / 4, NM = M / 16, NCH = K / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t r = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = r < n;
+  const int64_t rr = valid ? r : 0;
+  f4 acc[NM];
+#pragma unroll
+  for (int t = 0; t < NM; ++t) acc[t] = f4{0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const f4 b = valid ? ld4(in + rr * K + 16 * c + 4 * g) : f4{0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s = 4 * c + q;
+#pragma unroll
+      for (int t = 0; t < NM; ++t) acc[t] = MFMA(Ap[frag_idx(t, s, KS, lane)], b[q], acc[t]);
+    }
+  }
+  if (!valid) return;
+#pragma unroll
+  for (int t = 0; t < NM; ++t) {
+    float* po = out + r * M + 16 * t + 4 * g;
+    f4 v = acc[t];
+    if (act >= 0) {
+      const f4 av = ld4(aprev + r * M + 16 * t + 4 * g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= act_grad(av[q], act);
+    }
+    if (accumulate) v += ld4(po);
+    st4(po, v);
+  }
+}
+
+__global__ void row_gemm_t_generic_kernel(const float* __restrict__ in, int64_t n, int K, const float* __restrict__ Mat,
+                                          int M, float* __restrict__ out, int accumulate, int act,
+                                          const float* __restrict__ aprev) {
+  const int64_t total = n * M;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / M;
+    const int m = (int)(e - r * M);
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += in[r * K + k] * Mat[(int64_t)m * K + k];
+    if (act >= 0) s *= act_grad(aprev[e], act);
+    out[e] = accumulate ? out[e] + s : s;
+  }
+}
+
+__global__ void split_cols_add_kernel(float* __restrict__ dst, int64_t n, int width, const float* __restrict__ src,
+                                      int src_stride, int col0) {
+  const int64_t total = n * width;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / width;
+    const int c = (int)(i - r * width);
+    dst[i] += src[r * src_stride + col0 + c];
+  }
+}
+
+__global__ void act_bwd_kernel(const float* __restrict__ da, const float* __restrict__ a, int64_t n, int act,
+                               float* __restrict__ dz) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dz[i] = da[i] * act_grad(a[i], act);
+}
+
+// ---------------------------------------------------------------------------------------------
+// part[chunk][M][N] = sum over the chunk's rows of A[r][m] B[r][n].  Rows are the MFMA k axis:
+// one MFMA consumes 4 rows; a wave owns a 64 x 64 output tile (4 x 4 MFMA blocks).
+constexpr int64_t kTsChunk = 8192;
+
+__global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                     int ldb, int64_t n_rows, int M, int N,
+                                                     float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tiles_m = (M + 63) / 64, tiles_n = (N + 63) / 64;
+  const int tile = blockIdx.y * 4 + wave;
+  if (tile >= tiles_m * tiles_n) return;
+  const int m0 = (tile / tiles_n) * 64, n0 = (tile % tiles_n) * 64;
+  const int64_t r0 = (int64_t)blockIdx.x * kTsChunk;
+  const int64_t r1 = std::min<int64_t>(n_rows, r0 + kTsChunk);
+  const int kk = lane >> 4, c = lane & 15;
+  f4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f4{0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; r += 4) {
+    const int64_t rr = r + kk;
+    const bool ok = rr < r1;
+    float av[4], bv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int m = m0 + 16 * a + c;
+      av[a] = (ok && m < M) ? A[rr * lda + m] : 0.f;
+      const int nn = n0 + 16 * a + c;
+      bv[a] = (ok && nn < N) ? B[rr * ldb + nn] : 0.f;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = MFMA(av[a], bv[b], acc[a][b]);
+  }
+  float* P = part + (int64_t)blockIdx.x * M * N;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int nn = n0 + 16 * b + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m0 + 16 * a + 4 * kk + q;
+        if (m < M && nn < N) P[(int64_t)m * N + nn] = acc[a][b][q];
+      }
+    }
+}
+
+__global__ void colsum_kernel(const float* __restrict__ B, int ldb, int64_t n_rows, int N, float* __restrict__ part) {
+  const int64_t r0 = (int64_t)blockIdx.x * kTsChunk;
+  const int64_t r1 = std::min<int64_t>(n_rows, r0 + kTsChunk);
+  for (int nn = threadIdx.x; nn < N; nn += blockDim.x) {
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += B[r * ldb + nn];
+    part[(int64_t)blockIdx.x * N + nn] = s;
+  }
+}
+
+__global__ void reduce_add_kernel(const float* __restrict__ part, int64_t nblk, int64_t size, float* __restrict__ C) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < size; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t b = 0; b < nblk; ++b) s += part[b * size + i];
+    C[i] += s;
+  }
+}
+
+__global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, float alpha, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] += alpha * x[i];
+}
+
+__global__ void mse_kernel(const float* __restrict__ pred, const float* __restrict__ label, int64_t n,
+                           float* __restrict__ dpred, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  const float sc = 2.0f / (float)n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = pred[i] - label[i];
+    dpred[i] = sc * d;
+    s += (double)d * (double)d;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void sumsq_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    s += (double)x[i] * (double)x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// Keras Adam (training_ops.ApplyAdam): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+// w -= lr_t m / (sqrt(v) + eps), lr_t = lr sqrt(1 - b2^t) / (1 - b1^t) computed by the host
+__global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float lr_t, float b1, float b2, float eps) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    w[i] -= lr_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+int blocks_for(int64_t n, int per = 256, int cap = 16384) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, cap));
+}
+
+}  // namespace
+
+// =============================================================================================
+hipError_t launch_pack_a(const float* M, int rows, int cols, float* out, hipStream_t st) {
+  if (rows % 16 || cols % 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_a_kernel, dim3(blocks_for((int64_t)rows * cols)), dim3(256), 0, st, M, rows, cols, out);
+  return hipGetLastError();
+}
+
+bool bwd_shape_supported(int din, int h) {
+  return (din == 16 || din == 32 || din == 64) && (h == 16 || h == 32 || h == 64) && (h != 64 || din == 64) &&
+         (din != 64 || h == 64);
+}
+
+hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
+  if (a.n_dst == 0) return hipSuccess;
+  dim3 grid((unsigned)((a.n_dst + 63) / 64));
+  if (h == 16) hipLaunchKernelGGL((seq_gru_bwd_kernel<16>), grid, dim3(256), 0, st, a);
+  else if (h == 32) hipLaunchKernelGGL((seq_gru_bwd_kernel<32>), grid, dim3(256), 0, st, a);
+  else if (h == 64) hipLaunchKernelGGL((seq_gru_bwd_kernel<64>), grid, dim3(256), 0, st, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st) {
+  if (a.n_dst == 0) return hipSuccess;
+  dim3 grid((unsigned)((a.n_dst + 63) / 64));
+#define SB_CASE(D, HH)                                                                   \
+  if (din == D && h == HH) {                                                             \
+    hipLaunchKernelGGL((sum_gru_bwd_kernel<D, HH>), grid, dim3(256), 0, st, a);          \
+    return hipGetLastError();                                                            \
+  }
+  SB_CASE(16, 16)
+  SB_CASE(16, 32)
+  SB_CASE(32, 16)
+  SB_CASE(32, 32)
+  SB_CASE(64, 64)
+#undef SB_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_csr_gather_add(float* out, int64_t n_rows, const int32_t* ptr, const int32_t* idx, const float* in,
+                                 int cols, int accumulate, hipStream_t st) {
+  if (n_rows == 0) return hipSuccess;
+  if (cols % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(csr_gather_add_kernel, dim3(blocks_for(n_rows * (cols / 4))), dim3(256), 0, st, out, n_rows, ptr,
+                     idx, in, cols, accumulate);
+  return hipGetLastError();
+}
+
+bool row_gemm_supported(int K, int M) {
+  return (K == 48 || K == 96 || K == 192 || K == 256) && (M == 16 || M == 32 || M == 64 || M == 256);
+}
+
+hipError_t launch_row_gemm_t(const float* in, int64_t n, int K, const float* Ap, int M, float* out, int accumulate,
+                             int act, const float* aprev, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  dim3 grid((unsigned)((n + 63) / 64));
+#define RG_CASE(KK, MM)                                                                                  \
+  if (K == KK && M == MM) {                                                                              \
+    hipLaunchKernelGGL((row_gemm_t_kernel<KK, MM>), grid, dim3(256), 0, st, in, n, Ap, out, accumulate, act, aprev); \
+    return hipGetLastError();                                                                            \
+  }
+  RG_CASE(48, 16)
+  RG_CASE(96, 16)
+  RG_CASE(48, 32)
+  RG_CASE(96, 32)
+  RG_CASE(192, 64)
+  RG_CASE(256, 16)
+  RG_CASE(256, 32)
+  RG_CASE(256, 64)
+  RG_CASE(256, 256)
+#undef RG_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_row_gemm_t_generic(const float* in, int64_t n, int K, const float* Mat, int M, float* out,
+                                     int accumulate, int act, const float* aprev, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(row_gemm_t_generic_kernel, dim3(blocks_for(n * M)), dim3(256), 0, st, in, n, K, Mat, M, out,
+                     accumulate, act, aprev);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_cols_add(float* dst, int64_t n, int width, const float* src, int src_stride, int col0,
+                                 hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_cols_add_kernel, dim3(blocks_for(n * width)), dim3(256), 0, st, dst, n, width, src,
+                     src_stride, col0);
+  return hipGetLastError();
+}
+
+hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, float* dz, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(blocks_for(n)), dim3(256), 0, st, da, a, n, act, dz);
+  return hipGetLastError();
+}
+
+int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N) {
+  const int64_t chunks = std::max<int64_t>(1, (n_rows + kTsChunk - 1) / kTsChunk);
+  return chunks * (int64_t)M * N;
+}
+
+hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
+                             float* part, float* C, hipStream_t st) {
+  if (n_rows == 0) return hipSuccess;
+  const int64_t chunks = (n_rows + kTsChunk - 1) / kTsChunk;
+  const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  dim3 grid((unsigned)chunks, (unsigned)((tiles + 3) / 4));
+  hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, n_rows, M, N, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t size = (int64_t)M * N;
+  hipLaunchKernelGGL(reduce_add_kernel, dim3(blocks_for(size)), dim3(256), 0, st, part, chunks, size, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum_add(const float* B, int ldb, int64_t n_rows, int N, float* part, float* C, hipStream_t st) {
+  if (n_rows == 0) return hipSuccess;
+  const int64_t chunks = (n_rows + kTsChunk - 1) / kTsChunk;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)chunks), dim3(256), 0, st, B, ldb, n_rows, N, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(reduce_add_kernel, dim3(blocks_for(N)), dim3(256), 0, st, part, chunks, (int64_t)N, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_axpy(float* y, const float* x, float alpha, int64_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(axpy_kernel, dim3(blocks_for(n)), dim3(256), 0, st, y, x, alpha, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_mse(const float* pred, const float* label, int64_t n, float* dpred, double* part, int nblk,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(mse_kernel, dim3(nblk), dim3(256), 0, st, pred, label, n, dpred, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_sumsq(const float* x, int64_t n, double* part, int nblk, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, st, x, n, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float b1, float b2,
+                       float eps, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, st, w, g, m, v, n, lr_t, b1, b2, eps);
+  return hipGetLastError();
+}

@@ -164,7 +164,7 @@ class MPPlan:
                                  C.cast(srcs, C.POINTER(_lib.SourceDesc)))
         cells = (_lib.CellDesc * len(self.cells))(*[_lib.CellDesc(din, h) for _, din, h in self.cells])
         ro = (C.c_int32 * len(self.readout_inputs))(*self.readout_inputs)
-        dense = (_lib.DenseDesc * len(self.dense))(*[_lib.DenseDesc(u, a, b) for _, u, a, b, _ in self.dense])
+        dense = (_lib.DenseDesc * len(self.dense))(*[_lib.DenseDesc(u, a, b, l2) for _, u, a, b, l2 in self.dense])
         keep += [ents, mps, cells, ro, dense]
         d = _lib.PlanDesc(self.iterations, len(self.entities), ents, len(self.adj_slots), len(self.il_slots),
                           len(self.mps), mps, len(self.cells), cells, len(self.readout_inputs), ro,
@@ -263,6 +263,27 @@ class Engine:
         """Run on an external HIP stream (e.g. ``torch.cuda.current_stream().cuda_stream``)."""
         check(lib.ign_plan_set_stream(self.handle, C.c_void_p(hip_stream)))
 
+    # ---- training (SURVEY §8f; ignnition_amd.training drives these) --------------------------
+    def get_params(self) -> dict:
+        flat = np.empty(self.n_params, np.float32)
+        check(lib.ign_plan_get_params(self.handle, flat.ctypes.data_as(C.c_void_p)))
+        return {name: flat[off:off + int(np.prod(shape))].reshape(shape).copy() for name, shape, off in self.layout}
+
+    def mse_loss(self, pred, labels, dpred) -> float:
+        """Device tensors or addresses: pred/labels/dpred [n] fp32 (n = labels.numel()).  Returns the
+        loss; writes dLoss/dpred."""
+        out = C.c_double()
+        check(lib.ign_mse_loss(self.handle, _ptr(pred), _ptr(labels), labels.numel(), _ptr(dpred), C.byref(out)))
+        return out.value
+
+    def l2_loss(self) -> float:
+        out = C.c_double()
+        check(lib.ign_l2_loss(self.handle, C.byref(out)))
+        return out.value
+
+    def adam_step(self, grads, m, v, iteration: int, lr: float, beta1=0.9, beta2=0.999, epsilon=1e-7):
+        check(lib.ign_adam_step(self.handle, _ptr(grads), _ptr(m), _ptr(v), int(iteration), lr, beta1, beta2, epsilon))
+
     def gather_rows(self, src, idx, dst):
         """dst[i] = src[idx[i]] (device tensors: src [R, C] fp32, idx [n] int32, dst [n, C])."""
         n = idx.numel()
@@ -278,6 +299,11 @@ class Engine:
 
     def __del__(self):
         self.close()
+
+
+def _ptr(x) -> C.c_void_p:
+    """Device pointer of a torch tensor, or a raw integer address."""
+    return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
 
 
 def _i64(a):
@@ -384,6 +410,25 @@ class Batch:
         check(lib.ign_batch_bind_state(self.engine.handle, self.handle, e, C.c_void_p(buf0.data_ptr()),
                                        C.c_void_p(buf1.data_ptr()), cap))
         self._bound[entity] = (buf0, buf1)
+
+    # ---- training -------------------------------------------------------------------------
+    def enable_training(self):
+        check(lib.ign_batch_enable_training(self.engine.handle, self.handle))
+
+    def forward_train(self, to_host: bool = True):
+        out = np.empty((self.predictions, self.output_units), np.float32) if to_host else None
+        check(lib.ign_forward_train(self.engine.handle, self.handle,
+                                    out.ctypes.data_as(C.c_void_p) if to_host else None))
+        return out
+
+    def predictions_ptr(self) -> int:
+        p = C.c_void_p()
+        check(lib.ign_batch_predictions(self.handle, C.byref(p)))
+        return p.value
+
+    def backward(self, dpred, grads):
+        """dpred, grads: device tensors ([predictions * units], [n_params])."""
+        check(lib.ign_backward(self.engine.handle, self.handle, _ptr(dpred), _ptr(grads)))
 
     def state_slot(self, entity: str) -> int:
         s = C.c_int32()

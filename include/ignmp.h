@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 2
+#define IGN_ABI_VERSION 3
 
 enum ign_status {
   IGN_OK = 0,
@@ -101,6 +101,7 @@ typedef struct {
   int32_t units;
   int32_t activation;              /* enum ign_activation */
   int32_t use_bias;
+  float l2;                        /* kernel_regularizer coefficient c: loss += c * sum(W^2) (AUX:833-834) */
 } ign_dense_desc;
 
 typedef struct {
@@ -212,6 +213,27 @@ int  ign_batch_state_slot(const ign_batch* batch, int32_t entity, int32_t* slot)
 /* dst[i][:] = src[idx[i]][:] on the plan stream (halo pack); cols % 4 == 0, device pointers. */
 int  ign_gather_rows(ign_plan* plan, const float* src, int64_t ld, const int32_t* idx, int64_t n, int32_t cols,
                      float* dst);
+
+/* ---- Training step (model_fn's TRAIN branch, GM:697-830) -------------------------
+ * ign_batch_enable_training allocates what the backward keeps (every hidden-state version, the
+ * per-step states of ordered updates, the aggregated messages of sum updates, the readout
+ * activations) and the transposed index tables.  Device pointers throughout; gradients come in
+ * the flat parameter layout of ign_plan_param_tensor and include the Dense l2 terms. */
+int  ign_batch_enable_training(ign_plan* plan, ign_batch* batch);
+/* forward of ComnetModel.call keeping the activations; pred_out: host or NULL (see ign_forward) */
+int  ign_forward_train(ign_plan* plan, ign_batch* batch, float* pred_out);
+/* grads[n_params] = dLoss/dparams for dLoss/dpredictions = dpred[predictions * output_units] */
+int  ign_backward(ign_plan* plan, ign_batch* batch, const float* dpred, float* grads);
+/* MeanSquaredError: loss = mean((pred - labels)^2) (host, may be NULL), dpred = 2 (pred - labels) / n */
+int  ign_mse_loss(ign_plan* plan, const float* pred, const float* labels, int64_t n, float* dpred, double* loss);
+/* sum over Dense layers of l2 * sum(W^2) for the current parameters (the regularization loss) */
+int  ign_l2_loss(ign_plan* plan, double* loss);
+/* Keras Adam on the plan's parameters (in place) with lr = the schedule at `iteration`:
+ * lr_t = lr sqrt(1 - beta2^(it+1)) / (1 - beta1^(it+1)); m, v: caller-owned device state. */
+int  ign_adam_step(ign_plan* plan, const float* grads, float* m, float* v, int64_t iteration, float lr,
+                   float beta1, float beta2, float epsilon);
+/* Copy the current parameters (flat layout) to host. */
+int  ign_plan_get_params(ign_plan* plan, float* host_out);
 
 #ifdef __cplusplus
 }

@@ -187,7 +187,7 @@ class TorchOracle:
         reg = self.regularization()
         (loss + reg).backward()
         grads = {k: v.grad.detach().numpy().copy() if v.grad is not None else np.zeros(v.shape) for k, v in self.p.items()}
-        return float(loss), float(reg), grads, pred.detach().numpy()
+        return float(loss.detach()), float(reg.detach()), grads, pred.detach().numpy()
 
 
 # -------------------------------------------------------------------- optimizer (GM:797-818)

@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_functions():
     src = open(os.path.join(REPO, "include", "ignmp.h")).read()
-    return sorted(set(re.findall(r"\b(ign_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(ign_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_every_header_symbol_exported():
@@ -27,7 +27,7 @@ def test_every_header_symbol_exported():
 
 
 def test_abi_version_and_error_string():
-    assert _lib.lib.ign_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.lib.ign_abi_version() == _lib.ABI_VERSION == 3
     rc = _lib.lib.ign_plan_create(None, 0, None)
     assert rc == -1
     assert b"null" in _lib.lib.ign_last_error()
