@@ -25,6 +25,7 @@ def normalization_queue_size(feature, feature_name):
 def main():
     model = ignnition.create_model()
     ignnition.debug(model)
+    ignnition.train_and_evaluate(model)
     return ignnition.predict(model)
 
 

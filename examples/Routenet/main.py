@@ -29,7 +29,7 @@ def exp(feature, feature_name):
 def main():
     model = ignnition.create_model()
     ignnition.debug(model)
-    # ignnition.train_and_evaluate(model)  # backward pass: next round
+    ignnition.train_and_evaluate(model)
     return ignnition.predict(model)
 
 

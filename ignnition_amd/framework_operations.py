@@ -143,8 +143,103 @@ def debug(model_description, out_dir: str = "../debug_model/"):
     return dump
 
 
-def train_and_evaluate(model):
-    """FO:108-166.  Training (backward through the packed GRU, MSE + L2, Adam) is the next
-    row of the build and is not lowered yet."""
-    raise NotImplementedError("train_and_evaluate: the backward pass is not implemented in this round "
-                              "(forward / predict are)")
+def _shard(stream, rank: int, world: int):
+    """Data parallel: rank r keeps batches r, r + world, ... of the shared stream."""
+    for k, item in enumerate(stream):
+        if k % world == rank:
+            yield item
+
+
+def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
+    """FO:108-166 on the HIP engine.
+
+    The same INI options drive it:
+    - ``[PATHS]`` train_dataset, eval_dataset, model_dir (an ``experiment_<datetime>`` subdirectory
+      is created, FO:124), warm_start_path (``kernel`` / ``recurrent_kernel`` / ``bias`` tensors,
+      FO:126-131);
+    - ``[TRAINING_OPTIONS]`` batch_size, train_steps, eval_samples, shuffle_train_samples,
+      shuffle_eval_samples, save_checkpoints_secs, keep_checkpoint_max, throttle_secs.
+
+    The Estimator's checkpoint/evaluate cycle becomes:
+    - a safetensors checkpoint every ``save_checkpoints_secs`` and at the end;
+    - an evaluation of ``eval_samples`` one-graph batches after each checkpoint, at most every
+      ``throttle_secs``;
+    - metrics appended to ``<model_dir>/metrics.jsonl``.
+
+    ``execute_gpu`` is ignored: in the reference, ``True`` *hides* the GPU (FO:134-145); here
+    every step runs on the HIP engine. With ``dist`` (torch.distributed, initialised),
+    each rank takes every world-th batch and gradients are averaged by all-reduce."""
+    import time
+
+    from .checkpoint import load_params, save_params
+    from .training import Trainer
+
+    log.warning("IGNNITION: Starting the training and evaluation process...")
+    gm.set_model_info(model)
+    opts = CONFIG["TRAINING_OPTIONS"]
+    paths = CONFIG["PATHS"]
+    batch_size = int(opts.get("batch_size", "1"))
+    train_steps = int(opts["train_steps"])
+    eval_samples = int(opts.get("eval_samples", "100"))
+    save_secs = float(opts.get("save_checkpoints_secs", "600"))
+    keep = int(opts.get("keep_checkpoint_max", "5"))
+    throttle = float(opts.get("throttle_secs", "600"))
+    rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    model_dir = os.path.join(paths["model_dir"], "experiment_" + str(datetime.datetime.now()).replace(" ", "_"))
+    if rank == 0:
+        os.makedirs(model_dir, exist_ok=True)
+    params = None
+    if paths.get("warm_start_path", None):
+        warm = load_params(paths["warm_start_path"])
+        params = {k: v for k, v in warm.items()
+                  if k.endswith("kernel") or k.endswith("recurrent_kernel") or k.endswith("bias")}
+    trainer = Trainer(model, params=params, device=device, dist=dist)
+    if params is not None and set(params) != set(trainer.params()):
+        full = trainer.params()
+        full.update(params)
+        trainer.set_params(full)
+    train_stream = gm.input_fn(paths["train_dataset"], shuffle=str_to_bool(opts.get("shuffle_train_samples", "False")),
+                               batch_size=batch_size)
+    if world > 1:
+        train_stream = _shard(train_stream, rank, world)
+
+    def eval_batches():
+        it = gm.input_fn(paths["eval_dataset"], shuffle=str_to_bool(opts.get("shuffle_eval_samples", "False")),
+                         batch_size=1)
+        for _ in range(eval_samples):
+            yield next(it)
+
+    ckpts, history = [], []
+    last_save = last_eval = time.time()
+    metrics = None
+
+    def checkpoint_and_eval(step, force=False):
+        nonlocal last_save, last_eval, metrics
+        if rank != 0:
+            return
+        path = os.path.join(model_dir, "ckpt-%d.safetensors" % step)
+        save_params(trainer.params(), path, {"step": str(step)})
+        ckpts.append(path)
+        while len(ckpts) > keep:
+            os.remove(ckpts.pop(0))
+        last_save = time.time()
+        if force or time.time() - last_eval >= throttle:
+            metrics = dict(trainer.evaluate(eval_batches()), step=step)
+            history.append(metrics)
+            with open(os.path.join(model_dir, "metrics.jsonl"), "a") as fh:
+                fh.write(json.dumps(metrics) + "\n")
+            log.warning("IGNNITION: eval at step %d: %s", step, metrics)
+            last_eval = time.time()
+
+    for step in range(1, train_steps + 1):
+        features, labels = next(train_stream)
+        out = trainer.train_step(features, labels)
+        if rank == 0 and (step % log_every == 0 or step == 1):
+            log.warning("IGNNITION: step %d  Loss %.6g  Regularization loss %.6g  Total loss %.6g", step,
+                        out["loss"], out["regularization_loss"], out["total_loss"])
+        if time.time() - last_save >= save_secs:
+            checkpoint_and_eval(step)
+    checkpoint_and_eval(train_steps, force=True)
+    return {"model_dir": model_dir, "final_metrics": metrics, "history": history, "checkpoints": list(ckpts),
+            "trainer": trainer}

@@ -1,0 +1,156 @@
+"""Training on the HIP engine: model_fn's TRAIN / EVAL branches (code/utils/generate_model.py:697-830,
+"GM") and the loop of train_and_evaluate (code/utils/framework_operations.py:108-166, "FO").
+
+* loss: ``learning_options.loss`` (MeanSquaredError, GM:745-753) over the batch's concatenated
+  flat predictions, plus the Dense l2 kernel regularizers (AUX:833-834).  The engine computes
+  it (``ign_mse_loss``, ``ign_l2_loss``).
+* gradients: ``ign_backward``, the HIP backward of the whole forward (tf.gradients, GM:790).
+* optimizer: ``learning_options.optimizer`` (GM:797-818).  Only Adam is lowered (``ign_adam_step``,
+  Keras semantics); the learning rate is a float or an ExponentialDecay schedule evaluated at
+  ``iterations`` (the global step, GM:816).
+* data parallel: with torch.distributed initialised, every rank trains on its own batches and
+  the gradient is averaged with one all-reduce (RCCL on GPUs) before the update.
+* eval metrics (GM:755-785): label/prediction mean, MAE, MRE and the batch-mean r-squared
+  (GM:201-216), after denormalisation, plus the mean loss.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .engine import UnsupportedModel
+from .generate_model import ComnetModel, _resolve
+
+SUPPORTED_LOSSES = ("MeanSquaredError",)
+
+
+class LearningRate:
+    """``optimizer.learning_rate`` or ``optimizer.schedule`` (Keras ExponentialDecay)."""
+
+    def __init__(self, opt: dict):
+        sched = opt.get("schedule")
+        self.kind = "constant"
+        self.lr0 = float(opt.get("learning_rate", 0.001))
+        if sched is not None:
+            sched = dict(sched)
+            kind = sched.pop("type")
+            if kind != "ExponentialDecay":
+                raise UnsupportedModel("learning-rate schedule %r is not lowered (ExponentialDecay only)" % kind)
+            self.kind = kind
+            self.lr0 = float(sched["initial_learning_rate"])
+            self.decay_steps = float(sched["decay_steps"])
+            self.decay_rate = float(sched["decay_rate"])
+            # Keras tests `if self.staircase:`; a JSON string such as "True" (QSJ:204) or even
+            # "False" is truthy there
+            self.staircase = bool(sched.get("staircase", False))
+
+    def __call__(self, step: int) -> float:
+        if self.kind == "constant":
+            return self.lr0
+        p = step / self.decay_steps
+        if self.staircase:
+            p = math.floor(p)
+        return self.lr0 * self.decay_rate ** p
+
+
+class Trainer:
+    def __init__(self, model_info, params: dict | None = None, device: int = 0, seed: int = 0, dist=None):
+        import torch
+        self.torch = torch
+        loss = model_info.get_loss()
+        if loss not in SUPPORTED_LOSSES:
+            raise UnsupportedModel("loss %r is not lowered (%s)" % (loss, ", ".join(SUPPORTED_LOSSES)))
+        opt = dict(model_info.get_optimizer())
+        if opt.get("type") != "Adam":
+            raise UnsupportedModel("optimizer %r is not lowered (Adam only)" % opt.get("type"))
+        self.lr = LearningRate(opt)
+        self.beta1 = float(opt.get("beta_1", 0.9))
+        self.beta2 = float(opt.get("beta_2", 0.999))
+        self.epsilon = float(opt.get("epsilon", 1e-7))
+        self.model_info = model_info
+        torch.cuda.set_device(device)
+        self.model = ComnetModel(model_info, device=device, params=params, seed=seed)
+        eng = self.model.engine
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)   # torch copies / RCCL stream-ordered
+        dev = torch.device("cuda", device)
+        self.grads = torch.zeros(eng.n_params, dtype=torch.float32, device=dev)
+        self.m = torch.zeros_like(self.grads)
+        self.v = torch.zeros_like(self.grads)
+        self.dpred = None
+        self.device = dev
+        self.dist = dist
+        self.iterations = 0
+        self.output_name, _, self.output_denorm = model_info.get_output_info()
+
+    @property
+    def engine(self):
+        return self.model.engine
+
+    def _labels(self, labels):
+        y = np.concatenate([np.asarray(l, np.float32).reshape(-1) for l in labels])
+        return self.torch.from_numpy(y).to(self.device)
+
+    def train_step(self, features: list, labels: list) -> dict:
+        """One optimizer step on a batch of graphs (model_fn TRAIN, GM:712-830)."""
+        b = self.model.batch(features)
+        try:
+            b.enable_training()
+            b.forward_train(to_host=False)
+            y = self._labels(labels)
+            if y.numel() != b.predictions * b.output_units:
+                raise ValueError("labels hold %d values for %d predictions" % (y.numel(), b.predictions * b.output_units))
+            dpred = self.torch.empty_like(y)
+            loss = self.engine.mse_loss(b.predictions_ptr(), y, dpred)
+            b.backward(dpred, self.grads)
+            if self.dist is not None and self.dist.is_initialized() and self.dist.get_world_size() > 1:
+                self.dist.all_reduce(self.grads)
+                self.grads /= self.dist.get_world_size()
+            lr = self.lr(self.iterations)
+            self.engine.adam_step(self.grads, self.m, self.v, self.iterations, lr, self.beta1, self.beta2, self.epsilon)
+            self.iterations += 1
+        finally:
+            b.close()
+        reg = self.engine.l2_loss()
+        return {"loss": loss, "regularization_loss": reg, "total_loss": loss + reg, "learning_rate": lr,
+                "step": self.iterations}
+
+    def _denorm(self, v):
+        if self.output_denorm is None or str(self.output_denorm) == "None":
+            return v
+        try:
+            return _resolve(self.output_denorm)(v, self.output_name)
+        except KeyError:
+            return v
+
+    def evaluate(self, batches) -> dict:
+        """model_fn EVAL (GM:755-785) over an iterable of (features, labels) batches."""
+        labels_all, preds_all, losses, r2 = [], [], [], []
+        for features, labels in batches:
+            b = self.model.batch(features)
+            try:
+                p = b.forward().reshape(-1).astype(np.float64)
+            finally:
+                b.close()
+            y = np.concatenate([np.asarray(l, np.float64).reshape(-1) for l in labels])
+            losses.append(float(np.mean((y - p) ** 2)))
+            yd = np.asarray(self._denorm(y), np.float64)
+            pd = np.asarray(self._denorm(p), np.float64)
+            labels_all.append(yd)
+            preds_all.append(pd)
+            tot = np.sum((yd - yd.mean()) ** 2)
+            r2.append(1.0 - np.sum((yd - pd) ** 2) / tot if tot > 0 else float("nan"))
+        y = np.concatenate(labels_all)
+        p = np.concatenate(preds_all)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rel = np.where(y != 0, np.abs(y - p) / np.abs(y), 0.0)   # div_no_nan
+        return {"loss": float(np.mean(losses)), "label/mean": float(y.mean()), "prediction/mean": float(p.mean()),
+                "mae": float(np.mean(np.abs(y - p))), "mre": float(rel.mean()), "r-squared": float(np.nanmean(r2)),
+                "samples": int(len(losses))}
+
+    def params(self) -> dict:
+        return self.engine.get_params()
+
+    def set_params(self, params: dict):
+        self.model.set_params(params)

@@ -54,3 +54,45 @@ def test_predict_end_to_end(example_dir):
     ref = DenseOracle(desc, fo.find_dataset_dimensions(fo.CONFIG["PATHS"]["train_dataset"]), prm).forward(graphs)
     got = np.concatenate(preds)   # no label_denormalization in RNJ -> normalised outputs
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_train_and_evaluate_end_to_end(example_dir):
+    """FO:108-166: steps, checkpoints, eval metrics, warm start."""
+    from ignnition_amd.checkpoint import load_params
+    mi = fo.create_model()
+    fo.CONFIG["TRAINING_OPTIONS"]["train_steps"] = "25"
+    fo.CONFIG["TRAINING_OPTIONS"]["batch_size"] = "3"
+    fo.CONFIG["TRAINING_OPTIONS"]["eval_samples"] = "3"
+    fo.CONFIG["TRAINING_OPTIONS"]["keep_checkpoint_max"] = "2"
+    res = fo.train_and_evaluate(mi, log_every=5)
+    m = res["final_metrics"]
+    assert m["step"] == 25 and m["samples"] == 3
+    assert np.isfinite(m["loss"]) and np.isfinite(m["mae"]) and np.isfinite(m["r-squared"])
+    assert res["trainer"].iterations == 25
+    assert 1 <= len(res["checkpoints"]) <= 2 and all(os.path.exists(c) for c in res["checkpoints"])
+    assert os.path.exists(os.path.join(res["model_dir"], "metrics.jsonl"))
+    saved = load_params(res["checkpoints"][-1])
+    now = res["trainer"].params()
+    for k in now:
+        np.testing.assert_array_equal(saved[k], now[k])
+    # warm start from the checkpoint continues from those parameters
+    fo.CONFIG["PATHS"]["warm_start_path"] = res["checkpoints"][-1]
+    fo.CONFIG["TRAINING_OPTIONS"]["train_steps"] = "1"
+    res2 = fo.train_and_evaluate(mi)
+    assert res2["trainer"].iterations == 1
+    del fo.CONFIG["PATHS"]["warm_start_path"]
+
+
+@pytest.mark.gpu
+def test_training_learns_on_repeated_batch(example_dir):
+    from ignnition_amd.training import Trainer
+    mi = fo.create_model()
+    gm.set_model_info(mi)
+    xs, ys = next(gm.input_fn(fo.CONFIG["PATHS"]["train_dataset"], batch_size=3))
+    tr = Trainer(mi, seed=1)
+    tr.lr.lr0 = 0.003
+    first = tr.train_step(xs, ys)["loss"]
+    for _ in range(40):
+        last = tr.train_step(xs, ys)["loss"]
+    assert last < 0.5 * first
