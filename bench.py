@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--model", default="routenet", choices=["routenet", "qsize", "synthetic"],
                     help="synthetic = the 1M-node / 10M-edge graph of BASELINE configs[4] (one graph per rank)")
     ap.add_argument("--nodes", type=int, default=1_000_000, help="synthetic graph size")
+    ap.add_argument("--train", action="store_true",
+                    help="time the training step (forward keeping activations, MSE, backward, gradient "
+                         "all-reduce over ranks, Adam) instead of the forward")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -122,11 +125,12 @@ def main():
         # one graph edge-cut across the ranks (strong scaling): every rank generates the same seeded
         # graph, keeps its node range and in-edges, and exchanges halo rows over RCCL (partition.py)
         args.graphs, args.topology = 1, "1m" if args.nodes == 1_000_000 else str(args.nodes)
-        desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=args.nodes)
+        desc, dims, mi, graphs, labels = workloads.make_synthetic_inputs(n_nodes=args.nodes)
     else:
         # per-rank shard: graphs [rank*G, (rank+1)*G) -> weak scaling, no forward collective
         ids = workloads.shard_graph_ids(rank, world, args.graphs)
-        desc, dims, mi, graphs, _ = workloads.make_batch_inputs(args.model, args.topology, len(ids), first_id=ids[0])
+        desc, dims, mi, graphs, labels = workloads.make_batch_inputs(args.model, args.topology, len(ids),
+                                                                     first_id=ids[0])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(seed=0, bias_scale=0.05)
     eng = Engine(plan, device if world > 1 else 0)
@@ -153,6 +157,25 @@ def main():
         step = lambda: batch.forward(to_host=False)
         edges = batch.edges_per_forward
         gru_steps = batch.gru_steps_per_forward
+        if args.train:
+            import torch
+            torch.cuda.set_device(device if world > 1 else 0)
+            eng.set_stream(torch.cuda.current_stream().cuda_stream)
+            batch.enable_training()
+            y = torch.from_numpy(np.concatenate([np.asarray(l, np.float32).reshape(-1) for l in labels])).cuda()
+            dpred = torch.empty_like(y)
+            grads = torch.zeros(eng.n_params, dtype=torch.float32, device=y.device)
+            m_state, v_state = torch.zeros_like(grads), torch.zeros_like(grads)
+            it_box = [0]
+
+            def step():   # model_fn TRAIN (GM:712-818): one optimizer step on the rank's batch
+                batch.forward_train(to_host=False)
+                eng.mse_loss(batch.predictions_ptr(), y, dpred, want_loss=False)
+                batch.backward(dpred, grads)
+                if dist is not None:
+                    dist.all_reduce(grads)
+                eng.adam_step(grads, m_state, v_state, it_box[0], 1e-3)
+                it_box[0] += 1
     t_build = time.perf_counter() - t_build
 
     # Warm-up with every launch timed (per-kind breakdown, picks the dominant kernel); the timed
@@ -183,9 +206,9 @@ def main():
         dist.destroy_process_group()
         return
 
-    workload = "%s_%s_x%d" % (args.model, args.topology, args.graphs)
+    workload = "%s_%s_x%d%s" % (args.model, args.topology, args.graphs, "_train" if args.train else "")
     roof = None
-    if not args.no_timing and stats[dom]["ms"] > 0:
+    if not args.no_timing and not args.train and stats[dom]["ms"] > 0:
         s = stats[dom]
         launches = max(s["launches"], 1)
         avg_s = s["ms"] / launches / 1e3
@@ -210,7 +233,7 @@ def main():
                                        "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
                                    for k, v in warm.items() if v["launches"]}}
     cpu = None
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and not args.train:
         if synthetic:
             # bounded sample: a 25k-node graph from the same generator (same degree law and locality)
             sd, sdims, _, sg, _ = workloads.make_synthetic_inputs(n_nodes=25_000)

@@ -118,11 +118,8 @@ int ign::repack(ign_plan* p) {
       HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
     }
   }
-  if (p->fused_readout) {
-    for (int l = 0; l < 2; ++l)
-      HIP_TRY(launch_pack_dense(p->d_params + p->dense[l].off_w, p->d_packed + p->dense[l].pk_w, p->dense[l].in,
-                                p->dense[l].out, p->stream));
-  }
+  for (auto& dp : p->dense)
+    if (dp.pk_w >= 0) HIP_TRY(launch_pack_dense(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in, dp.out, p->stream));
   for (auto& dp : p->dense)
     if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
   return IGN_OK;
@@ -275,9 +272,12 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.pk_u = pk; pk = align(pk + 3LL * cp.H * cp.H);
     cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
   }
-  if (p->fused_readout) {
-    p->dense[0].pk_w = pk; pk = align(pk + (int64_t)p->dense[0].in * p->dense[0].out);
-    p->dense[1].pk_w = pk; pk = align(pk + (int64_t)p->dense[1].in * p->dense[1].out);
+  for (size_t l = 0; l < p->dense.size(); ++l) {
+    DenseP& dp = p->dense[l];
+    if ((p->fused_readout && l < 2) || dense_fwd_supported(dp.in, dp.out)) {
+      dp.pk_w = pk;
+      pk = align(pk + (int64_t)dp.in * dp.out);
+    }
   }
   // backward fragments (training): W^T / U^T per cell, W^T per Dense layer where the MFMA
   // row GEMM is instantiated

@@ -43,7 +43,7 @@ struct CellP {
 struct DenseP {
   int in, out, act, use_bias;
   float l2 = 0.f;
-  int64_t off_w, off_b, pk_w;
+  int64_t off_w, off_b, pk_w = -1;   // pk_w: forward fragments (fused readout, training readout)
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
 };
 

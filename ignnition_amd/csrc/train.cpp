@@ -313,8 +313,8 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
   for (size_t l = 0; l < p->dense.size(); ++l) {
     const DenseP& d = p->dense[l];
     float* o = l + 1 == p->dense.size() ? b->d_pred : t->act[l];
-    HIP_TRY(launch_dense_generic(in, P, d.in, in_stride, p->d_params + d.off_w, d.use_bias ? p->d_params + d.off_b : nullptr,
-                                 d.out, d.act, o, st));
+    HIP_TRY(launch_dense_fwd(in, P, d.in, in_stride, d.pk_w >= 0 ? p->d_packed + d.pk_w : nullptr,
+                             p->d_params + d.off_w, d.use_bias ? p->d_params + d.off_b : nullptr, d.out, d.act, o, st));
     in = o;
     in_stride = d.out;
   }
@@ -348,8 +348,8 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
   for (int l = L - 1; l >= 0; --l) {
     const DenseP& d = p->dense[l];
     const float* A = l == 0 ? X : t->act[l - 1];
-    HIP_TRY(launch_tsgemm_add(A, d.in, t->dz[zi], d.out, P, d.in, d.out, t->part, grads + d.off_w, st));
-    if (d.use_bias) HIP_TRY(launch_colsum_add(t->dz[zi], d.out, P, d.out, t->part, grads + d.off_b, st));
+    HIP_TRY(launch_tsgemm_add(A, d.in, t->dz[zi], d.out, P, d.in, d.out, t->part, grads + d.off_w,
+                              d.use_bias ? grads + d.off_b : nullptr, st));
     if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)d.in * d.out, st));
     float* out;
     int act = -1, acc = 0;
@@ -396,18 +396,16 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     float* gb = grads + cp.off_b;
     if (mp.sorted) {
       if ((rc = build_table(p, mp, mb, cp, srcs))) return rc;
-      HIP_TRY(hipMemsetAsync(t->gu, 0, mt.hs_rows * H3 * sizeof(float), st));
       SeqBwdArgs a{mt.hs[rec.it], mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
                    t->ga, t->gu, mb.n_dst};
       HIP_TRY(launch_seq_gru_bwd(a, H, st));
-      HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, st));
-      HIP_TRY(launch_colsum_add(t->gu, H3, mt.hs_rows, H3, t->part, gb + H3, st));
+      HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, gb + H3, st));
       HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, gb, st));
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const int se = mp.src[s].entity;
         HIP_TRY(launch_csr_gather_add(t->dtab, mt.trows[s], mt.tptr[s], mt.tidx[s], t->ga, H3, 0, st));
-        HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, st));
+        HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, nullptr, st));
         float* target = se == dst ? dh_out : t->dS[dcur[se]][se];
         HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, 1, -1, nullptr, st));
       }
@@ -416,10 +414,8 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       SumBwdArgs a{mt.xs[rec.it], hin, p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b,
                    p->d_packed + cp.pk_wt, p->d_packed + cp.pk_ut, dh_in, dh_out, t->dx, t->ga, t->gu, mb.n_dst};
       HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
-      HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, st));
-      HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, st));
-      HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_dst, H3, t->part, gb, st));
-      HIP_TRY(launch_colsum_add(t->gu, H3, mb.n_dst, H3, t->part, gb + H3, st));
+      HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, gb, st));
+      HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, gb + H3, st));
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const int se = mp.src[s].entity;
         float* target = se == dst ? dh_out : t->dS[dcur[se]][se];

@@ -18,7 +18,8 @@ struct SeqBwdArgs {
   const float* dh_in;        // [rows][H] dLoss/d(state after the MP)
   float* dh_out;             // [rows][H] dLoss/d(state before the MP), GRU part
   float* ga;                 // [n_steps][3H]  dLoss/d(x.W + b_in) per step
-  float* gu;                 // [n_steps + n_dst][3H] dLoss/d(h.U + b_rec), rows aligned with hs (pre-zeroed)
+  float* gu;                 // [n_steps + n_dst][3H] dLoss/d(h.U + b_rec), rows aligned with hs
+                             // (the kernel zeroes each sequence's final-state row)
   int64_t n_dst;
 };
 
@@ -59,10 +60,15 @@ hipError_t launch_split_cols_add(float* dst, int64_t n, int width, const float* 
                                  hipStream_t st);
 // dz[r][c] = da[r][c] * act'(a[r][c])
 hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, float* dz, hipStream_t st);
-// C[M][N] += sum_r A[r][:M]^T B[r][:N]; partial sums per row chunk, reduced in a fixed order
+// C[M][N] += sum_r A[r][:M]^T B[r][:N] and, if Cb, Cb[N] += sum_r B[r][:N] (a virtual ones column);
+// partial sums per row chunk, reduced in a fixed order (deterministic)
 int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N);
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
-                             float* part, float* C, hipStream_t st);
+                             float* part, float* C, float* Cb, hipStream_t st);
+// forward Dense layer for the training readout: y = act(x W + b), MFMA when packed fragments exist
+bool dense_fwd_supported(int K, int M);
+hipError_t launch_dense_fwd(const float* x, int64_t n, int K, int x_stride, const float* Wp, const float* W,
+                            const float* bias, int M, int act, float* y, hipStream_t st);
 // C[N] += sum_r B[r][:N]
 hipError_t launch_colsum_add(const float* B, int ldb, int64_t n_rows, int N, float* part, float* C, hipStream_t st);
 // y[i] += alpha * x[i]

@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "kernels.h"
 #include "train_kernels.h"
 
 namespace {
@@ -162,6 +163,10 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   if (valid) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) st4(a.dh_out + (int64_t)row * H + 16 * t + 4 * g, dh[t]);
+    // the final state's row of gu has no step (no memset of the whole buffer needed)
+    float* pz = a.gu + (hbase + L) * (3 * H) + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 3 * NT; ++t) st4(pz + 16 * t, f4{0, 0, 0, 0});
   }
 }
 
@@ -349,73 +354,161 @@ __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __rest
 }
 
 // ---------------------------------------------------------------------------------------------
-// part[chunk][M][N] = sum over the chunk's rows of A[r][m] B[r][n].  Rows are the MFMA k axis:
-// one MFMA consumes 4 rows; a wave owns a 64 x 64 output tile (4 x 4 MFMA blocks).
-constexpr int64_t kTsChunk = 8192;
+// Row contractions C[M][N] = sum_r A[r][:M]^T B[r][:N] (weight gradients), optionally with a
+// virtual all-ones column appended to A: C row M = sum_r B[r] (the bias gradient).  Rows are the
+// MFMA k axis (4 per MFMA); a wave owns a 64 x 64 output tile and a chunk of rows, 16 rows per
+// iteration (32 loads in flight), and writes its partial tile.  Chunks are sized so the grid
+// holds ~8k waves; two reduction passes (segments, then final) sum the partials in a fixed order.
+constexpr int kTsWaves = 8192;
+constexpr int kTsSegs = 64;
+
+struct TsPlan {
+  int Mx, tiles;
+  int64_t chunks, chunk;
+};
+
+TsPlan ts_plan(int64_t n_rows, int M, int N, int ones) {
+  TsPlan p;
+  p.Mx = M + ones;
+  p.tiles = ((p.Mx + 63) / 64) * ((N + 63) / 64);
+  const int64_t max_chunks = std::max<int64_t>(1, (n_rows + 255) / 256);
+  p.chunks = std::max<int64_t>(1, std::min<int64_t>((kTsWaves + p.tiles - 1) / p.tiles, max_chunks));
+  p.chunk = ((n_rows + p.chunks - 1) / p.chunks + 15) / 16 * 16;
+  p.chunks = std::max<int64_t>(1, (n_rows + p.chunk - 1) / p.chunk);
+  return p;
+}
 
 __global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
-                                                     int ldb, int64_t n_rows, int M, int N,
+                                                     int ldb, int64_t n_rows, int M, int N, int ones, int64_t chunk,
                                                      float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int tiles_m = (M + 63) / 64, tiles_n = (N + 63) / 64;
+  const int Mx = M + ones;
+  const int tiles_m = (Mx + 63) / 64, tiles_n = (N + 63) / 64;
   const int tile = blockIdx.y * 4 + wave;
   if (tile >= tiles_m * tiles_n) return;
   const int m0 = (tile / tiles_n) * 64, n0 = (tile % tiles_n) * 64;
-  const int64_t r0 = (int64_t)blockIdx.x * kTsChunk;
-  const int64_t r1 = std::min<int64_t>(n_rows, r0 + kTsChunk);
+  const int na = min(4, (Mx - m0 + 15) / 16), nb = min(4, (N - n0 + 15) / 16);
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  const int64_t r1 = std::min<int64_t>(n_rows, r0 + chunk);
   const int kk = lane >> 4, c = lane & 15;
   f4 acc[4][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f4{0, 0, 0, 0};
-  for (int64_t r = r0; r < r1; r += 4) {
-    const int64_t rr = r + kk;
-    const bool ok = rr < r1;
-    float av[4], bv[4];
+    for (int y = 0; y < 4; ++y) acc[x][y] = f4{0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; r += 16) {
+    float av[4][4], bv[4][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int m = m0 + 16 * a + c;
-      av[a] = (ok && m < M) ? A[rr * lda + m] : 0.f;
-      const int nn = n0 + 16 * a + c;
-      bv[a] = (ok && nn < N) ? B[rr * ldb + nn] : 0.f;
+    for (int q = 0; q < 4; ++q) {
+      const int64_t rr = r + 4 * q + kk;
+      const bool ok = rr < r1;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int m = m0 + 16 * x + c;
+        float v = 0.f;
+        if (x < na && ok) v = m < M ? A[rr * lda + m] : (m == M && ones ? 1.f : 0.f);
+        av[q][x] = v;
+        const int n = n0 + 16 * x + c;
+        bv[q][x] = (x < nb && ok && n < N) ? B[rr * ldb + n] : 0.f;
+      }
     }
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = MFMA(av[a], bv[b], acc[a][b]);
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+          if (x < na && y < nb) acc[x][y] = MFMA(av[q][x], bv[q][y], acc[x][y]);
   }
-  float* P = part + (int64_t)blockIdx.x * M * N;
+  float* P = part + (int64_t)blockIdx.x * Mx * N;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int nn = n0 + 16 * b + c;
+    for (int y = 0; y < 4; ++y) {
+      const int n = n0 + 16 * y + c;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int m = m0 + 16 * a + 4 * kk + q;
-        if (m < M && nn < N) P[(int64_t)m * N + nn] = acc[a][b][q];
+        const int m = m0 + 16 * x + 4 * kk + q;
+        if (x < na && y < nb && m < Mx && n < N) P[(int64_t)m * N + n] = acc[x][y][q];
       }
     }
 }
 
-__global__ void colsum_kernel(const float* __restrict__ B, int ldb, int64_t n_rows, int N, float* __restrict__ part) {
-  const int64_t r0 = (int64_t)blockIdx.x * kTsChunk;
-  const int64_t r1 = std::min<int64_t>(n_rows, r0 + kTsChunk);
-  for (int nn = threadIdx.x; nn < N; nn += blockDim.x) {
-    float s = 0.f;
-    for (int64_t r = r0; r < r1; ++r) s += B[r * ldb + nn];
-    part[(int64_t)blockIdx.x * N + nn] = s;
+// pass 1: seg[s][i] = sum of part[c][i] over chunks c = s, s + S, ...   (grid: elements x S)
+__global__ void reduce_seg_kernel(const float* __restrict__ part, int64_t nchunks, int64_t size, int S,
+                                  float* __restrict__ seg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.y;
+  if (i >= size) return;
+  float acc = 0.f;
+  for (int64_t c = s; c < nchunks; c += S) acc += part[c * size + i];
+  seg[(int64_t)s * size + i] = acc;
+}
+
+// pass 2: C[m][n] += sum_s seg[s][m][n] for m < M; row M (ones column) goes to Cb[n]
+__global__ void reduce_final_kernel(const float* __restrict__ seg, int S, int M, int N, int ones,
+                                    float* __restrict__ C, float* __restrict__ Cb) {
+  const int64_t size = (int64_t)(M + ones) * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < size; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += seg[(int64_t)s * size + i];
+    if (i < (int64_t)M * N) C[i] += acc;
+    else Cb[i - (int64_t)M * N] += acc;
   }
 }
 
-__global__ void reduce_add_kernel(const float* __restrict__ part, int64_t nblk, int64_t size, float* __restrict__ C) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < size; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int64_t b = 0; b < nblk; ++b) s += part[b * size + i];
-    C[i] += s;
+// y[r][m] = act(sum_k x[r][k] W[k][m] + b[m]); W given as pack_dense fragments (A[m][k] = W[k][m]).
+template <int K, int M>
+__global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict__ x, int64_t n, int x_stride,
+                                                        const float* __restrict__ Wp, const float* __restrict__ bias,
+                                                        int act, float* __restrict__ y) {
+  constexpr int KS = K / 4, NM = M / 16, NCH = K / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t r = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
+  const bool valid = r < n;
+  const int64_t rr = valid ? r : 0;
+  f4 acc[NM];
+#pragma unroll
+  for (int t = 0; t < NM; ++t) acc[t] = bias ? ld4(bias + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const f4 b = ld4(x + rr * x_stride + 16 * c + 4 * g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s = 4 * c + q;
+#pragma unroll
+      for (int t = 0; t < NM; ++t) acc[t] = MFMA(Wp[frag_idx(t, s, KS, lane)], b[q], acc[t]);
+    }
   }
+  if (!valid) return;
+#pragma unroll
+  for (int t = 0; t < NM; ++t) {
+    f4 v = acc[t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = act_apply(v[q], act);
+    st4(y + r * M + 16 * t + 4 * g, v);
+  }
+}
+
+// y[r] = act(x[r] . w + b) for a 1-unit layer: 16 lanes per row, float4 loads, shuffle reduce
+__global__ void dense_dot_kernel(const float* __restrict__ x, int64_t n, int K, int x_stride,
+                                 const float* __restrict__ w, const float* __restrict__ bias, int act,
+                                 float* __restrict__ y) {
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int l = threadIdx.x & 15;
+  float s = 0.f;
+  if (r < n)
+    for (int k = 4 * l; k < K; k += 64) {
+      const f4 a = ld4(x + r * x_stride + k);
+      const f4 b = ld4(w + k);
+      s += a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+    }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 16);
+  if (r < n && l == 0) y[r] = act_apply(s + (bias ? bias[0] : 0.f), act);
 }
 
 __global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, float alpha, int64_t n) {
@@ -573,32 +666,57 @@ hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, f
 }
 
 int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N) {
-  const int64_t chunks = std::max<int64_t>(1, (n_rows + kTsChunk - 1) / kTsChunk);
-  return chunks * (int64_t)M * N;
+  const TsPlan p = ts_plan(n_rows, M, N, 1);
+  return (p.chunks + kTsSegs) * (int64_t)p.Mx * N;
 }
 
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
-                             float* part, float* C, hipStream_t st) {
+                             float* part, float* C, float* Cb, hipStream_t st) {
   if (n_rows == 0) return hipSuccess;
-  const int64_t chunks = (n_rows + kTsChunk - 1) / kTsChunk;
-  const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
-  dim3 grid((unsigned)chunks, (unsigned)((tiles + 3) / 4));
-  hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, n_rows, M, N, part);
+  const int ones = Cb != nullptr;
+  const TsPlan p = ts_plan(n_rows, M, N, ones);
+  dim3 grid((unsigned)p.chunks, (unsigned)((p.tiles + 3) / 4));
+  hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int64_t size = (int64_t)M * N;
-  hipLaunchKernelGGL(reduce_add_kernel, dim3(blocks_for(size)), dim3(256), 0, st, part, chunks, size, C);
+  const int64_t size = (int64_t)p.Mx * N;
+  float* seg = part + p.chunks * size;
+  const int S = (int)std::min<int64_t>(kTsSegs, p.chunks);
+  hipLaunchKernelGGL(reduce_seg_kernel, dim3((unsigned)((size + 255) / 256), (unsigned)S), dim3(256), 0, st, part,
+                     p.chunks, size, S, seg);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(reduce_final_kernel, dim3(blocks_for(size)), dim3(256), 0, st, seg, S, M, N, ones, C, Cb);
   return hipGetLastError();
 }
 
 hipError_t launch_colsum_add(const float* B, int ldb, int64_t n_rows, int N, float* part, float* C, hipStream_t st) {
-  if (n_rows == 0) return hipSuccess;
-  const int64_t chunks = (n_rows + kTsChunk - 1) / kTsChunk;
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)chunks), dim3(256), 0, st, B, ldb, n_rows, N, part);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(reduce_add_kernel, dim3(blocks_for(N)), dim3(256), 0, st, part, chunks, (int64_t)N, C);
-  return hipGetLastError();
+  return launch_tsgemm_add(nullptr, 0, B, ldb, n_rows, 0, N, part, nullptr, C, st);
+}
+
+bool dense_fwd_supported(int K, int M) {
+  return (K == 16 || K == 32 || K == 64 || K == 256) && M == 256;
+}
+
+hipError_t launch_dense_fwd(const float* x, int64_t n, int K, int x_stride, const float* Wp, const float* W,
+                            const float* bias, int M, int act, float* y, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (M == 1 && K % 4 == 0 && x_stride % 4 == 0) {
+    hipLaunchKernelGGL(dense_dot_kernel, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, st, x, n, K, x_stride,
+                       W, bias, act, y);
+    return hipGetLastError();
+  }
+  dim3 grid((unsigned)((n + 63) / 64));
+#define DF_CASE(KK, MM)                                                                                        \
+  if (K == KK && M == MM && Wp) {                                                                              \
+    hipLaunchKernelGGL((dense_fwd_kernel<KK, MM>), grid, dim3(256), 0, st, x, n, x_stride, Wp, bias, act, y);  \
+    return hipGetLastError();                                                                                  \
+  }
+  DF_CASE(16, 256)
+  DF_CASE(32, 256)
+  DF_CASE(64, 256)
+  DF_CASE(256, 256)
+#undef DF_CASE
+  return launch_dense_generic(x, n, K, x_stride, W, bias, M, act, y, st);
 }
 
 hipError_t launch_axpy(float* y, const float* x, float alpha, int64_t n, hipStream_t st) {

@@ -269,12 +269,13 @@ class Engine:
         check(lib.ign_plan_get_params(self.handle, flat.ctypes.data_as(C.c_void_p)))
         return {name: flat[off:off + int(np.prod(shape))].reshape(shape).copy() for name, shape, off in self.layout}
 
-    def mse_loss(self, pred, labels, dpred) -> float:
+    def mse_loss(self, pred, labels, dpred, want_loss: bool = True) -> float:
         """Device tensors or addresses: pred/labels/dpred [n] fp32 (n = labels.numel()).  Returns the
         loss; writes dLoss/dpred."""
         out = C.c_double()
-        check(lib.ign_mse_loss(self.handle, _ptr(pred), _ptr(labels), labels.numel(), _ptr(dpred), C.byref(out)))
-        return out.value
+        check(lib.ign_mse_loss(self.handle, _ptr(pred), _ptr(labels), labels.numel(), _ptr(dpred),
+                               C.byref(out) if want_loss else None))
+        return out.value if want_loss else None
 
     def l2_loss(self) -> float:
         out = C.c_double()
