@@ -381,6 +381,8 @@ TsPlan ts_plan(int64_t n_rows, int M, int N, int ones) {
 __global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                      int ldb, int64_t n_rows, int M, int N, int ones, int64_t chunk,
                                                      float* __restrict__ part) {
+  // The ones column (bias gradient) is not an MFMA row: the tile whose m range would hold it
+  // accumulates plain column sums of B on the VALU (lanes of one kk own 4 rows each).
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int Mx = M + ones;
@@ -388,11 +390,13 @@ __global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A
   const int tile = blockIdx.y * 4 + wave;
   if (tile >= tiles_m * tiles_n) return;
   const int m0 = (tile / tiles_n) * 64, n0 = (tile % tiles_n) * 64;
-  const int na = min(4, (Mx - m0 + 15) / 16), nb = min(4, (N - n0 + 15) / 16);
+  const int na = max(0, min(4, (M - m0 + 15) / 16)), nb = min(4, (N - n0 + 15) / 16);
+  const bool has_ones = ones && M >= m0 && M < m0 + 64;
   const int64_t r0 = (int64_t)blockIdx.x * chunk;
   const int64_t r1 = std::min<int64_t>(n_rows, r0 + chunk);
   const int kk = lane >> 4, c = lane & 15;
   f4 acc[4][4];
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -406,20 +410,21 @@ __global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const int m = m0 + 16 * x + c;
-        float v = 0.f;
-        if (x < na && ok) v = m < M ? A[rr * lda + m] : (m == M && ones ? 1.f : 0.f);
-        av[q][x] = v;
+        av[q][x] = (x < na && ok && m < M) ? A[rr * lda + m] : 0.f;
         const int n = n0 + 16 * x + c;
         bv[q][x] = (x < nb && ok && n < N) ? B[rr * ldb + n] : 0.f;
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y) csum[y] += bv[q][y];
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y)
           if (x < na && y < nb) acc[x][y] = MFMA(av[q][x], bv[q][y], acc[x][y]);
+    }
   }
   float* P = part + (int64_t)blockIdx.x * Mx * N;
 #pragma unroll
@@ -430,9 +435,19 @@ __global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = m0 + 16 * x + 4 * kk + q;
-        if (x < na && y < nb && m < Mx && n < N) P[(int64_t)m * N + n] = acc[x][y][q];
+        if (x < na && y < nb && m < M && n < N) P[(int64_t)m * N + n] = acc[x][y][q];
       }
     }
+  if (has_ones) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {      // sum over the 4 row phases kk (lanes c, c+16, c+32, c+48)
+      float s = csum[y];
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      const int n = n0 + 16 * y + c;
+      if (kk == 0 && n < N) P[(int64_t)M * N + n] = s;
+    }
+  }
 }
 
 // pass 1: seg[s][i] = sum of part[c][i] over chunks c = s, s + S, ...   (grid: elements x S)
