@@ -54,6 +54,14 @@ class BatchDesc(C.Structure):
                 ("halo_rows", C.POINTER(i64))]
 
 
+class DatasetDesc(C.Structure):
+    _fields_ = [("num_features", i32), ("features", C.POINTER(C.c_char_p)), ("output_name", C.c_char_p),
+                ("num_adjacencies", i32), ("adj_name", C.POINTER(C.c_char_p)), ("adj_src", C.POINTER(C.c_char_p)),
+                ("adj_dst", C.POINTER(C.c_char_p)), ("adj_params", C.POINTER(i32)),
+                ("num_interleave", i32), ("il_name", C.POINTER(C.c_char_p)), ("il_dst", C.POINTER(C.c_char_p)),
+                ("num_additional", i32), ("additional", C.POINTER(C.c_char_p))]
+
+
 class BatchInfo(C.Structure):
     _fields_ = [("num_graphs", i64), ("predictions", i64), ("output_units", i64), ("edges_per_forward", i64),
                 ("gru_steps_per_forward", i64), ("rows", i64 * 8)]
@@ -77,7 +85,8 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_forward_begin", "ign_forward_mp", "ign_forward_end", "ign_batch_mp_split", "ign_batch_bind_state",
            "ign_batch_state_slot", "ign_gather_rows", "ign_plan_set_timing_kinds",
            "ign_batch_enable_training", "ign_forward_train", "ign_backward", "ign_mse_loss", "ign_l2_loss",
-           "ign_adam_step", "ign_plan_get_params"]
+           "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
+           "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get"]
 
 ABI_VERSION = 3
 PART = {"all": 0, "interior": 1, "boundary": 2}
@@ -131,6 +140,12 @@ def _load():
         "ign_l2_loss": (C.c_int, [VP, P(C.c_double)]),
         "ign_adam_step": (C.c_int, [VP, VP, VP, VP, i64, f32, f32, f32, f32]),
         "ign_plan_get_params": (C.c_int, [VP, VP]),
+        "ign_dataset_open": (C.c_int, [C.c_char_p, P(DatasetDesc), i32, P(VP)]),
+        "ign_dataset_close": (None, [VP]),
+        "ign_dataset_size": (C.c_int, [VP, P(i64), P(i32)]),
+        "ign_dataset_error": (C.c_char_p, [VP, i32]),
+        "ign_dataset_gather": (C.c_int, [VP, P(i64), i32]),
+        "ign_dataset_get": (C.c_int, [VP, C.c_char_p, P(i32), P(VP), P(i64), P(P(i64))]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

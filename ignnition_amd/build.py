@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libignmp.so")
-SOURCES = ["engine.cpp", "train.cpp", "kernels.hip", "train_kernels.hip"]
+SOURCES = ["engine.cpp", "train.cpp", "dataset.cpp", "kernels.hip", "train_kernels.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
          "-Wno-unused-value"]
 
@@ -27,7 +27,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = OUT + ".tmp"
-    cmd = [hipcc] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
+    cmd = [hipcc] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp, "-lz", "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,110 @@
+"""Native dataset reader: the generator of code/utils/generator_std_to_framework.py
+(GEN:53-230) in C++ (``ign_dataset_*`` in libignmp.so), multi-threaded over the tar.gz files.
+
+``NativeDataset`` reads a dataset directory once, with the model's feature / adjacency /
+interleave names.  ``batch(ids)`` returns a ``BatchedGraphs`` (graph-concatenated arrays that
+``engine.Batch`` consumes without per-graph Python work) plus the batch's labels.
+Normalisation (GM:46-86) is applied by name to each feature's concatenated array.  That equals
+the reference's per-sample call for elementwise functions, which is what the examples use
+(RNM:26-38, QSM:27-39).  The per-sample index arrays are bit-identical to ``generator.py``'s
+(tests/test_dataset.py).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import logging
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .engine import BatchedGraphs
+
+log = logging.getLogger("ignnition_amd")
+
+
+def _strs(items):
+    arr = (C.c_char_p * max(len(items), 1))(*[s.encode() for s in items])
+    return arr
+
+
+class NativeDataset:
+    def __init__(self, data_dir: str, feature_names, output_name, adj_names, interleave_names,
+                 additional_input=(), training: bool = True, threads: int = 16):
+        self._keep = []
+        feats = _strs(list(feature_names))
+        adj = [[str(x) for x in a] for a in adj_names]
+        an, asrc, adst = _strs([a[0] for a in adj]), _strs([a[1] for a in adj]), _strs([a[2] for a in adj])
+        aprm = (C.c_int32 * max(len(adj), 1))(*[1 if a[3] == "True" else 0 for a in adj])
+        iln, ild = _strs([i[0] for i in interleave_names]), _strs([i[1] for i in interleave_names])
+        add = _strs(list(additional_input))
+        self._keep += [feats, an, asrc, adst, aprm, iln, ild, add]
+        desc = _lib.DatasetDesc(len(feature_names), feats, output_name.encode() if training else None,
+                                len(adj), an, asrc, adst, aprm, len(interleave_names), iln, ild,
+                                len(additional_input), add)
+        h = C.c_void_p()
+        check(lib.ign_dataset_open(str(data_dir).encode(), C.byref(desc), threads, C.byref(h)))
+        self.handle = h
+        n, ne = C.c_int64(), C.c_int32()
+        check(lib.ign_dataset_size(h, C.byref(n), C.byref(ne)))
+        self.n_samples = n.value
+        self.errors = [lib.ign_dataset_error(h, i).decode(errors="replace") for i in range(ne.value)]
+        for e in self.errors:           # GEN:229-230 logs the exception and abandons that file
+            log.error(e)
+        self.training = training
+
+    @classmethod
+    def for_model(cls, data_dir: str, model_info, training: bool = True, threads: int = 16):
+        feature_list = model_info.get_all_features()
+        names = [f.name for f in feature_list]
+        output_name, _, _ = model_info.get_output_info()
+        additional = [a for a in model_info.get_additional_input_names() if a not in names]
+        return cls(data_dir, names, output_name, model_info.get_adjecency_info(),
+                   model_info.get_interleave_tensors(), additional, training, threads)
+
+    def __len__(self):
+        return self.n_samples
+
+    def gather(self, ids):
+        ids = np.ascontiguousarray(np.asarray(ids, np.int64))
+        check(lib.ign_dataset_gather(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), len(ids)))
+        self._ids = ids
+
+    def get(self, key: str):
+        """(graph-concatenated array, per-graph lengths) of one generator key for the gathered batch."""
+        dt, ptr, total, lens = C.c_int32(), C.c_void_p(), C.c_int64(), C.POINTER(C.c_int64)()
+        check(lib.ign_dataset_get(self.handle, key.encode(), C.byref(dt), C.byref(ptr), C.byref(total), C.byref(lens)))
+        G = len(self._ids)
+        ctype, np_t = (C.c_float, np.float32) if dt.value == 0 else (C.c_int64, np.int64)
+        vals = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(max(total.value, 1),))[:total.value].copy()
+        glen = np.ctypeslib.as_array(lens, shape=(max(G, 1),))[:G].copy()
+        return vals.astype(np_t, copy=False), glen
+
+    def batch(self, ids, keys):
+        """BatchedGraphs holding ``keys`` for samples ``ids``, and the labels (or None)."""
+        self.gather(ids)
+        arrays = {k: self.get(k) for k in keys}
+        labels = self.get("__label__") if self.training else None
+        return BatchedGraphs(arrays, len(ids)), labels
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h:
+            lib.ign_dataset_close(h)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+def plan_keys(plan) -> list:
+    """The generator keys an engine plan reads."""
+    keys = []
+    for e, name in enumerate(plan.entities):
+        keys.append("num_" + name)
+        keys += [f for f, _ in plan.features[e]]
+    for slot in plan.adj_slots:
+        keys += list(slot.keys)
+    keys += list(plan.il_slots)
+    return list(dict.fromkeys(keys))

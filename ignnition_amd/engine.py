@@ -311,52 +311,83 @@ def _i64(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.int64).reshape(-1))
 
 
+class BatchedGraphs:
+    """A batch of graphs as graph-concatenated arrays: key -> (values, per-graph lengths), the
+    keys of the input_fn dict (GM:127-158).  ``num_<entity>`` holds one value per graph."""
+
+    def __init__(self, arrays: dict, num_graphs: int):
+        self.arrays = arrays
+        self.num_graphs = num_graphs
+
+    @classmethod
+    def from_dicts(cls, graphs: list) -> "BatchedGraphs":
+        keys = {}
+        for x in graphs:
+            for k in x:
+                keys.setdefault(k, None)
+        arrays = {}
+        for k in keys:
+            if not all(k in x for x in graphs):
+                continue
+            parts = [np.asarray(x[k]).reshape(-1) for x in graphs]
+            arrays[k] = (np.concatenate(parts) if parts else np.zeros(0), np.array([len(v) for v in parts], np.int64))
+        return cls(arrays, len(graphs))
+
+    def get(self, key):
+        if key not in self.arrays:
+            raise KeyError("batch has no array %r" % key)
+        return self.arrays[key]
+
+    def __contains__(self, key):
+        return key in self.arrays
+
+
 class Batch:
     """A disjoint-union batch of graphs on the device (``ign_batch``).
 
     ``graphs``: list of feature dicts with the input_fn keys (GM:127-158), features already
     normalised.  Graph-local indices are kept; the engine offsets them per graph."""
 
-    def __init__(self, engine: Engine, graphs: list, halo_rows: dict = None):
-        """``halo_rows``: {entity: extra rows} for one edge-cut partition (see partition.py)."""
+    def __init__(self, engine: Engine, graphs, halo_rows: dict = None):
+        """``graphs``: a list of feature dicts, or a ``BatchedGraphs`` (graph-concatenated arrays,
+        e.g. from the native dataset reader).  ``halo_rows``: {entity: extra rows} for one
+        edge-cut partition (see partition.py)."""
         p = engine.plan
         self.engine = engine
-        G = len(graphs)
+        bg = graphs if isinstance(graphs, BatchedGraphs) else BatchedGraphs.from_dicts(graphs)
+        G = bg.num_graphs
         E = len(p.entities)
         num = np.zeros((G, E), np.int64)
-        for g, x in enumerate(graphs):
-            for e, name in enumerate(p.entities):
-                num[g, e] = int(np.asarray(x["num_" + name]).reshape(()))
+        for e, name in enumerate(p.entities):
+            v, _ = bg.get("num_" + name)
+            num[:, e] = np.asarray(v, np.int64).reshape(G)
         feats = []
         for e, name in enumerate(p.entities):
             cols = []
             for fname, size in p.features[e]:
-                parts = [np.asarray(x[fname], np.float32).reshape(int(num[g, e]), size) for g, x in enumerate(graphs)]
-                cols.append(np.concatenate(parts, 0) if parts else np.zeros((0, size), np.float32))
+                v, lens = bg.get(fname)
+                if not np.array_equal(np.asarray(lens, np.int64), num[:, e] * size):
+                    raise ValueError("feature %s: %s values per graph for %s nodes of size %d"
+                                     % (fname, list(lens), list(num[:, e]), size))
+                cols.append(np.asarray(v, np.float32).reshape(-1, size))
             feats.append(np.ascontiguousarray(np.concatenate(cols, 1)) if cols else None)
         A = len(p.adj_slots)
         cnt = np.zeros((G, A), np.int64)
         srcs, dsts, seqs = [], [], []
         for a, slot in enumerate(p.adj_slots):
             ks, kd, kq = slot.keys
-            s_parts, d_parts, q_parts = [], [], []
-            for g, x in enumerate(graphs):
-                s, d, q = _i64(x[ks]), _i64(x[kd]), _i64(x[kq])
-                if not (len(s) == len(d) == len(q)):
-                    raise ValueError("graph %d: %s/%s/%s have different lengths" % (g, ks, kd, kq))
-                cnt[g, a] = len(s)
-                s_parts.append(s), d_parts.append(d), q_parts.append(q)
-            srcs.append(np.concatenate(s_parts)), dsts.append(np.concatenate(d_parts)), seqs.append(np.concatenate(q_parts))
+            (s, ls), (d, ld), (q, lq) = bg.get(ks), bg.get(kd), bg.get(kq)
+            if not (np.array_equal(ls, ld) and np.array_equal(ls, lq)):
+                raise ValueError("%s/%s/%s have different lengths" % (ks, kd, kq))
+            cnt[:, a] = ls
+            srcs.append(_i64(s)), dsts.append(_i64(d)), seqs.append(_i64(q))
         I = len(p.il_slots)
         il_len = np.zeros((G, max(I, 1)), np.int64)
         ils = []
         for i, key in enumerate(p.il_slots):
-            parts = []
-            for g, x in enumerate(graphs):
-                v = _i64(x[key])
-                il_len[g, i] = len(v)
-                parts.append(v)
-            ils.append(np.concatenate(parts))
+            v, lens = bg.get(key)
+            il_len[:, i] = lens
+            ils.append(_i64(v))
         self._arrays = (num, feats, cnt, srcs, dsts, seqs, il_len, ils)
         fp = C.POINTER(C.c_float)
         lp = C.POINTER(C.c_int64)

@@ -158,7 +158,8 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
       is created, FO:124), warm_start_path (``kernel`` / ``recurrent_kernel`` / ``bias`` tensors,
       FO:126-131);
     - ``[TRAINING_OPTIONS]`` batch_size, train_steps, eval_samples, shuffle_train_samples,
-      shuffle_eval_samples, save_checkpoints_secs, keep_checkpoint_max, throttle_secs.
+      shuffle_eval_samples, save_checkpoints_secs, keep_checkpoint_max, throttle_secs, and
+      ``native_reader`` (default True: the C++ dataset reader; False: the Python generator).
 
     The Estimator's checkpoint/evaluate cycle becomes:
     - a safetensors checkpoint every ``save_checkpoints_secs`` and at the end;
@@ -199,14 +200,16 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
         full = trainer.params()
         full.update(params)
         trainer.set_params(full)
-    train_stream = gm.input_fn(paths["train_dataset"], shuffle=str_to_bool(opts.get("shuffle_train_samples", "False")),
-                               batch_size=batch_size)
+    native = str_to_bool(opts.get("native_reader", "True"))   # C++ reader
+    make_input = gm.input_fn_native if native else gm.input_fn
+    train_stream = make_input(paths["train_dataset"], shuffle=str_to_bool(opts.get("shuffle_train_samples", "False")),
+                              batch_size=batch_size)
     if world > 1:
         train_stream = _shard(train_stream, rank, world)
 
     def eval_batches():
-        it = gm.input_fn(paths["eval_dataset"], shuffle=str_to_bool(opts.get("shuffle_eval_samples", "False")),
-                         batch_size=1)
+        it = make_input(paths["eval_dataset"], shuffle=str_to_bool(opts.get("shuffle_eval_samples", "False")),
+                        batch_size=1)
         for _ in range(eval_samples):
             yield next(it)
 

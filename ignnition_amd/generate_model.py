@@ -109,6 +109,48 @@ def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True):
             yield batch
 
 
+def input_fn_native(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, threads=16, seed=None):
+    """input_fn on the native reader (ignnition_amd.dataset): yields ``BatchedGraphs`` (and the
+    batch's label array when training).  Normalisation functions are applied by name to each
+    feature's graph-concatenated array and to the labels: the same values as the per-sample
+    call for elementwise functions (those of the examples)."""
+    from .dataset import NativeDataset, plan_keys
+    mi = model_info
+    ds = NativeDataset.for_model(data_dir, mi, training=training, threads=threads)
+    plan = MPPlan.from_model_info(mi)
+    keys = plan_keys(plan)
+    feature_list = mi.get_all_features()
+    output_name, output_normalization, _ = mi.get_output_info()
+    rng = np.random.default_rng(seed)
+    n = len(ds)
+    if n == 0:
+        return
+    while True:
+        order = rng.permutation(n) if shuffle else np.arange(n)
+        for b0 in range(0, n, batch_size):
+            ids = order[b0:b0 + batch_size]
+            bg, labels = ds.batch(ids, keys)
+            for f in feature_list:
+                if str(f.normalization) != "None" and f.name in bg:
+                    v, lens = bg.get(f.name)
+                    try:
+                        fn = _resolve(f.normalization)
+                    except KeyError:
+                        log.error("IGNNITION: The normalization function " + str(f.normalization) +
+                                  " is not defined in the main file.")
+                        sys.exit(1)
+                    bg.arrays[f.name] = (np.asarray(fn(v, f.name), np.float32), lens)
+            if training:
+                y = labels[0]
+                if str(output_normalization) != "None":
+                    y = np.asarray(_resolve(output_normalization)(y, output_name), np.float32)
+                yield bg, [y]
+            else:
+                yield bg
+        if not repeat:
+            return
+
+
 def r_squared(labels, predictions):
     """GM:201-216 (value of the streaming mean for one batch)."""
     labels = np.asarray(labels, np.float64)
@@ -151,7 +193,8 @@ class ComnetModel:
                 out.append(l2 * float((w * w).sum()))
         return out
 
-    def batch(self, graphs: list) -> Batch:
+    def batch(self, graphs) -> Batch:
+        """``graphs``: a list of feature dicts or a ``BatchedGraphs`` (native reader)."""
         return Batch(self.engine, graphs)
 
     def predict_batch(self, graphs: list) -> np.ndarray:

@@ -235,6 +235,39 @@ int  ign_adam_step(ign_plan* plan, const float* grads, float* m, float* v, int64
 /* Copy the current parameters (flat layout) to host. */
 int  ign_plan_get_params(ign_plan* plan, float* host_out);
 
+/* ---- Native dataset reader (GEN:32-230 = the reference's generator) -----
+ * Reads every <dir>/*.tar.gz (sorted by name; data.json inside, a list of samples) on `threads`
+ * host threads and builds the generator's index contract per sample.  A sample that fails
+ * abandons the rest of its file and is reported through ign_dataset_error (GEN:229-230); a file
+ * without data.json fails the open.  Batches are gathered by sample id; ign_dataset_get returns
+ * the batch's graph-concatenated array of one generator key (feature names, src_/dst_<adj>,
+ * seq_<src>_<dst>, params_<adj>, num_<entity>, indices_<src>_to_<dst>, or "__label__") with its
+ * per-graph lengths; pointers stay valid until the next gather. */
+typedef struct ign_dataset ign_dataset;
+typedef struct {
+  int32_t num_features;
+  const char* const* features;      /* feature names (model order) */
+  const char* output_name;          /* label key; NULL when reading without labels (predict) */
+  int32_t num_adjacencies;          /* model_info.get_adjecency_info() order (GEN:134) */
+  const char* const* adj_name;
+  const char* const* adj_src;       /* source entity type */
+  const char* const* adj_dst;       /* destination entity type */
+  const int32_t* adj_params;        /* 1: keep [node, params] parameters ("True") */
+  int32_t num_interleave;           /* get_interleave_tensors(): (definition key, destination) */
+  const char* const* il_name;
+  const char* const* il_dst;
+  int32_t num_additional;
+  const char* const* additional;
+} ign_dataset_desc;
+int  ign_dataset_open(const char* dir, const ign_dataset_desc* desc, int32_t threads, ign_dataset** out);
+void ign_dataset_close(ign_dataset* ds);
+int  ign_dataset_size(const ign_dataset* ds, int64_t* n_samples, int32_t* n_errors);
+const char* ign_dataset_error(const ign_dataset* ds, int32_t i);
+int  ign_dataset_gather(ign_dataset* ds, const int64_t* ids, int32_t count);
+/* dtype: 0 float32, 1 int64 */
+int  ign_dataset_get(ign_dataset* ds, const char* key, int32_t* dtype, const void** ptr, int64_t* total,
+                     const int64_t** per_graph);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,114 @@
+"""Native dataset reader (libignmp.so ign_dataset_*) vs the reference generator's own outputs
+(tests/golden/gen_fixtures.json, bit-exact) and vs ignnition_amd.generator on synthetic
+datasets.  CPU only: the reader is host code."""
+import json
+import time
+
+import numpy as np
+import pytest
+
+from ignnition_amd import generator as G
+from ignnition_amd import synthetic, workloads
+from ignnition_amd.dataset import NativeDataset, plan_keys
+from ignnition_amd.engine import BatchedGraphs, MPPlan
+
+
+def _flat(v):
+    return np.asarray(v, dtype=np.float64).reshape(-1)
+
+
+@pytest.mark.parametrize("idx", range(8))
+def test_native_reader_matches_reference_fixtures(gen_fixtures, idx, tmp_path):
+    case = gen_fixtures[idx]
+    synthetic.write_tar_dataset(case["samples"], str(tmp_path), per_file=len(case["samples"]))
+    ds = NativeDataset(str(tmp_path), case["feature_names"], case["output_name"], case["adj_names"],
+                       case["interleave_names"], [], case["training"], threads=2)
+    assert len(ds) == len(case["expected"]), case["name"]
+    for sid, exp in enumerate(case["expected"]):
+        ds.gather([sid])
+        for k, v in exp["data"].items():
+            got, lens = ds.get(k)
+            if got.dtype == np.int64:
+                assert got.tolist() == np.asarray(v).reshape(-1).tolist(), (case["name"], k)
+            else:
+                np.testing.assert_array_equal(got, _flat(v).astype(np.float32), err_msg="%s %s" % (case["name"], k))
+            assert lens.tolist() == [got.size]
+        if case["training"]:
+            lab, _ = ds.get("__label__")
+            np.testing.assert_array_equal(lab, _flat(exp["output"]).astype(np.float32))
+    ds.close()
+
+
+def _compare_with_python(tmp_path, kind, topology, n):
+    samples = synthetic.dataset(topology, n, qsize=(kind == "qsize"), first_id=3)
+    synthetic.write_tar_dataset(samples, str(tmp_path), per_file=3)
+    desc, dims, mi = workloads.model(kind)
+    names = [f.name for f in mi.get_all_features()]
+    out, _, _ = mi.get_output_info()
+    py = list(G.generator(str(tmp_path), names, out, mi.get_adjecency_info(), mi.get_interleave_tensors(), [], True))
+    ds = NativeDataset.for_model(str(tmp_path), mi, threads=4)
+    assert len(ds) == len(py) == n
+    plan = MPPlan.from_model_info(mi)
+    keys = plan_keys(plan)
+    bg, labels = ds.batch(list(range(n)), keys)
+    ref = BatchedGraphs.from_dicts([x for x, _ in py])
+    for k in keys:
+        got, glen = bg.get(k)
+        exp, elen = ref.get(k)
+        assert glen.tolist() == elen.tolist(), k
+        if got.dtype == np.int64:
+            assert got.tolist() == np.asarray(exp, np.int64).tolist(), k
+        else:
+            np.testing.assert_array_equal(got, np.asarray(exp, np.float32), err_msg=k)
+    np.testing.assert_array_equal(labels[0], np.concatenate([np.asarray(y, np.float32) for _, y in py]))
+    # a shuffled subset keeps per-sample contents
+    sub = [5, 0, 2]
+    bg2, _ = ds.batch(sub, keys)
+    one = BatchedGraphs.from_dicts([py[i][0] for i in sub])
+    for k in keys:
+        assert np.array_equal(bg2.get(k)[0], np.asarray(one.get(k)[0], bg2.get(k)[0].dtype)), k
+    return ds
+
+
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_native_reader_matches_python_generator(tmp_path, kind):
+    _compare_with_python(tmp_path, kind, "nsfnet", 7).close()
+
+
+def test_native_reader_errors_abandon_file(tmp_path):
+    good = synthetic.routenet_sample("nsfnet", 0)
+    bad = dict(good)
+    del bad["traffic"]
+    synthetic.write_tar_dataset([good, bad, good], str(tmp_path), per_file=3)
+    desc, dims, mi = workloads.model("routenet")
+    ds = NativeDataset.for_model(str(tmp_path), mi)
+    assert len(ds) == 1           # the first sample is kept, the rest of the file is abandoned
+    assert ds.errors and "traffic" in ds.errors[0]
+
+
+def test_native_reader_missing_data_json_is_fatal(tmp_path):
+    import tarfile
+    with tarfile.open(str(tmp_path / "x.tar.gz"), "w:gz") as tar:
+        p = tmp_path / "other.json"
+        p.write_text("[]")
+        tar.add(str(p), arcname="other.json")
+    desc, dims, mi = workloads.model("routenet")
+    with pytest.raises(Exception, match="data.json"):
+        NativeDataset.for_model(str(tmp_path), mi)
+
+
+def test_native_reader_is_faster(tmp_path):
+    samples = synthetic.dataset("geant2", 24, qsize=False, first_id=0)
+    synthetic.write_tar_dataset(samples, str(tmp_path), per_file=4)
+    desc, dims, mi = workloads.model("routenet")
+    names = [f.name for f in mi.get_all_features()]
+    out, _, _ = mi.get_output_info()
+    t0 = time.perf_counter()
+    py = list(G.generator(str(tmp_path), names, out, mi.get_adjecency_info(), mi.get_interleave_tensors(), [], True))
+    t_py = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ds = NativeDataset.for_model(str(tmp_path), mi, threads=4)
+    ds.batch(list(range(len(ds))), plan_keys(MPPlan.from_model_info(mi)))
+    t_native = time.perf_counter() - t0
+    assert len(ds) == len(py)
+    assert t_native < t_py
