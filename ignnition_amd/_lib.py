@@ -27,7 +27,7 @@ class SourceDesc(C.Structure):
 
 class MPDesc(C.Structure):
     _fields_ = [("dst_entity", i32), ("aggregation", i32), ("concat_axis", i32), ("cell", i32),
-                ("num_sources", i32), ("sources", C.POINTER(SourceDesc))]
+                ("num_sources", i32), ("sources", C.POINTER(SourceDesc)), ("activation", i32)]
 
 
 class CellDesc(C.Structure):
@@ -88,7 +88,7 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get"]
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 

@@ -118,6 +118,11 @@ int ign::repack(ign_plan* p) {
       HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
     }
   }
+  if (p->pk_conv >= 0)
+    HIP_TRY(launch_pack_dense(p->d_params + p->off_conv, p->d_packed + p->pk_conv, p->conv_F, p->conv_F, p->stream));
+  if (p->pk_w12 >= 0)
+    HIP_TRY(launch_attn_vectors(p->d_params + p->off_k1, p->d_params + p->off_k2, p->d_params + p->off_att, p->attn_F,
+                                p->d_packed + p->pk_w12, p->stream));
   for (auto& dp : p->dense)
     if (dp.pk_w >= 0) HIP_TRY(launch_pack_dense(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in, dp.out, p->stream));
   for (auto& dp : p->dense)
@@ -195,8 +200,15 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
           return fail(IGN_ERR_UNSUPPORTED, "mp %d: concat aggregation on axis %d is not lowered yet", m, mp.concat_axis);
         mp.sorted = true;
         break;
+      case IGN_AGGR_ATTENTION:
+      case IGN_AGGR_CONVOLUTION:
+        mp.sorted = false;
+        mp.act = md.activation;
+        if (mp.aggr == IGN_AGGR_CONVOLUTION && !act_ok(mp.act))
+          return fail(IGN_ERR_UNSUPPORTED, "mp %d: convolution activation %d", m, mp.act);
+        break;
       default:
-        return fail(IGN_ERR_UNSUPPORTED, "mp %d: aggregation %d (attention/convolution) is not lowered yet", m, mp.aggr);
+        return fail(IGN_ERR_UNSUPPORTED, "mp %d: aggregation %d is not lowered", m, mp.aggr);
     }
     int din = -1;
     for (auto& s : mp.src) {
@@ -219,6 +231,20 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (!gru_shape_supported(din, cp.H))
       return fail(IGN_ERR_UNSUPPORTED, "mp %d: GRU shape (input %d, units %d) not instantiated (16/32, 64/64)", m,
                   din, cp.H);
+    if (mp.aggr == IGN_AGGR_ATTENTION || mp.aggr == IGN_AGGR_CONVOLUTION) {
+      const int F = p->ents[mp.dst].hidden_dim;
+      // AUX:311-319 / GM:293-298: the messages and the destination states must have one width
+      if (din != F)
+        return fail(IGN_ERR_INVALID, "mp %d: %s needs message dim %d == destination dim %d", m,
+                    mp.aggr == IGN_AGGR_ATTENTION ? "attention" : "convolution", din, F);
+      if (F != 16 && F != 32)
+        return fail(IGN_ERR_UNSUPPORTED, "mp %d: attention / convolution lowered for 16 or 32 units", m);
+      int& pf = mp.aggr == IGN_AGGR_ATTENTION ? p->attn_F : p->conv_F;
+      if (pf && pf != F)
+        return fail(IGN_ERR_INVALID, "mp %d: the shared %s weights have width %d, this MP needs %d (GM:288-300)", m,
+                    mp.aggr == IGN_AGGR_ATTENTION ? "attention" : "convolution", pf, F);
+      pf = F;
+    }
     cp.used = true;
     p->mps.push_back(mp);
   }
@@ -259,6 +285,16 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.off_rk = off; p->tensors.push_back({1, (int)c, off, cp.H, g3}); off = align(off + (int64_t)cp.H * g3);
     cp.off_b = off; p->tensors.push_back({2, (int)c, off, 2, g3}); off = align(off + 2LL * g3);
   }
+  if (p->conv_F) {
+    const int F = p->conv_F;
+    p->off_conv = off; p->tensors.push_back({5, -1, off, F, F}); off = align(off + (int64_t)F * F);
+  }
+  if (p->attn_F) {
+    const int F = p->attn_F;
+    p->off_k1 = off; p->tensors.push_back({6, -1, off, F, F}); off = align(off + (int64_t)F * F);
+    p->off_k2 = off; p->tensors.push_back({7, -1, off, F, F}); off = align(off + (int64_t)F * F);
+    p->off_att = off; p->tensors.push_back({8, -1, off, 2 * F, 1}); off = align(off + 2LL * F);
+  }
   for (size_t l = 0; l < p->dense.size(); ++l) {
     DenseP& dp = p->dense[l];
     dp.off_w = off; p->tensors.push_back({3, (int)l, off, dp.in, dp.out}); off = align(off + (int64_t)dp.in * dp.out);
@@ -290,6 +326,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (!row_gemm_supported(dp.out, dp.in)) continue;
     dp.pk_wt = pk; pk = align(pk + (int64_t)dp.in * dp.out);
   }
+  if (p->conv_F) { p->pk_conv = pk; pk = align(pk + (int64_t)p->conv_F * p->conv_F); }
+  if (p->attn_F) { p->pk_w12 = pk; pk = align(pk + 2LL * p->attn_F); }
   p->n_packed = pk;
 
   // Device resources are allocated on first use (ensure_device), so plan validation and the
@@ -502,6 +540,15 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         const int64_t e0 = eoff[a][g], e1 = eoff[a][g + 1];
         const int64_t nsrc = b->row_off[se][g + 1] - b->row_off[se][g] + b->halo[se];   // halo: G == 1
         const int64_t ndst = b->row_off[dst][g + 1] - b->row_off[dst][g];
+        // attention: comb_seq of source s > 0 is seq + that source's own in-degree (GM:539-540)
+        std::vector<int64_t> lens_s;
+        if (mp.aggr == IGN_AGGR_ATTENTION && s > 0) {
+          lens_s.assign(ndst, 0);
+          for (int64_t k = e0; k < e1; ++k) {
+            const int64_t di = d->adj_dst[a][k];
+            if (di >= 0 && di < ndst) lens_s[di]++;
+          }
+        }
         for (int64_t k = e0; k < e1; ++k) {
           int64_t si = d->adj_src[a][k], di = d->adj_dst[a][k], sq = d->adj_seq[a][k];
           if (si < 0 || si >= nsrc) return fail(IGN_ERR_INVALID, "graph %d: src index %lld out of range [0,%lld)", g, (long long)si, (long long)nsrc);
@@ -513,6 +560,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
               return fail(IGN_ERR_INVALID, "graph %d: interleave index %lld outside [0,%lld) (scatter_nd, AUX:435)",
                           g, (long long)pos, (long long)total_slots);
           }
+          if (mp.aggr == IGN_AGGR_ATTENTION) pos = sq + (s > 0 ? lens_s[di] : 0);
           int64_t drow = b->row_off[dst][g] + di;
           mdst.push_back(drow);
           mpos.push_back(pos);
@@ -644,9 +692,59 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       for (size_t k = 0; k < mdst.size(); ++k) ptr[where[mdst[k]] + 1]++;
       for (int64_t i = 0; i < ND; ++i) ptr[i + 1] += ptr[i];
       std::vector<uint32_t> msrc(mdst.size());
+      std::vector<int32_t> csr_pos(mdst.size());
       {
         std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
-        for (size_t k = 0; k < mdst.size(); ++k) msrc[fill[where[mdst[k]]]++] = mcode[k];
+        for (size_t k = 0; k < mdst.size(); ++k) {
+          csr_pos[k] = fill[where[mdst[k]]]++;
+          msrc[csr_pos[k]] = mcode[k];
+        }
+      }
+      if (mp.aggr == IGN_AGGR_ATTENTION) {
+        // dense (destination, position) cells of the scatter_nd (AUX:327-331); duplicates share one
+        // cell.  Groups = (graph, position): the softmax runs over a graph's destinations (AUX:336)
+        std::vector<int> gof(ND);
+        for (int g = 0; g < G; ++g)
+          for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r) gof[r] = g;
+        std::vector<int64_t> key(mdst.size());
+        std::vector<int64_t> gmax(G, 0);
+        for (size_t k = 0; k < mdst.size(); ++k) gmax[gof[mdst[k]]] = std::max(gmax[gof[mdst[k]]], mpos[k] + 1);
+        std::vector<int64_t> gbase(G + 1, 0);   // group index base per graph
+        for (int g = 0; g < G; ++g) gbase[g + 1] = gbase[g] + gmax[g];
+        std::vector<size_t> ord(mdst.size());
+        std::iota(ord.begin(), ord.end(), 0);
+        std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) {
+          const int64_t gx = gbase[gof[mdst[x]]] + mpos[x], gy = gbase[gof[mdst[y]]] + mpos[y];
+          return gx != gy ? gx < gy : mdst[x] < mdst[y];
+        });
+        std::vector<int32_t> group_ptr(gbase[G] + 1, 0), group_empty(gbase[G], 0), cell_dst, cell_ptr(1, 0), cell_msgs;
+        for (size_t q = 0; q < ord.size();) {
+          const size_t k = ord[q];
+          const int64_t grp = gbase[gof[mdst[k]]] + mpos[k];
+          size_t q2 = q;
+          while (q2 < ord.size() && mdst[ord[q2]] == mdst[k] && mpos[ord[q2]] == mpos[k]) cell_msgs.push_back(csr_pos[ord[q2++]]);
+          cell_dst.push_back((int32_t)mdst[k]);
+          cell_ptr.push_back((int32_t)cell_msgs.size());
+          group_ptr[grp + 1]++;
+          q = q2;
+        }
+        for (int64_t q = 0; q < gbase[G]; ++q) group_ptr[q + 1] += group_ptr[q];
+        for (int g = 0; g < G; ++g)
+          for (int64_t pq = 0; pq < gmax[g]; ++pq) {
+            const int64_t grp = gbase[g] + pq;
+            group_empty[grp] = (int32_t)((b->row_off[dst][g + 1] - b->row_off[dst][g]) - (group_ptr[grp + 1] - group_ptr[grp]));
+          }
+        mb.n_groups = gbase[G];
+        mb.n_cells = (int64_t)cell_dst.size();
+        if ((rc = dev_upload(b.get(), &mb.d_group_ptr, group_ptr)) || (rc = dev_upload(b.get(), &mb.d_group_empty, group_empty)) ||
+            (rc = dev_upload(b.get(), &mb.d_cell_dst, cell_dst)) || (rc = dev_upload(b.get(), &mb.d_cell_ptr, cell_ptr)) ||
+            (rc = dev_upload(b.get(), &mb.d_cell_msgs, cell_msgs)))
+          return rc;
+        if ((rc = dev_alloc(b.get(), &mb.d_msg_w, (int64_t)mdst.size())) || (rc = dev_alloc(b.get(), &mb.d_ecell, mb.n_cells)) ||
+            (rc = dev_alloc(b.get(), &mb.d_s_dst, ND)))
+          return rc;
+        for (int s = 0; s < S; ++s)
+          if ((rc = dev_alloc(b.get(), &mb.d_s_src[s], b->rows[mp.src[s].entity] + b->halo[mp.src[s].entity]))) return rc;
       }
       mb.n_msgs = (int64_t)msrc.size();
       if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
@@ -816,9 +914,30 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     const int64_t first = part == IGN_PART_BOUNDARY ? mb.n_interior : 0;
     const int64_t count = part == IGN_PART_INTERIOR ? mb.n_interior
                         : part == IGN_PART_BOUNDARY ? mb.n_dst - mb.n_interior : mb.n_dst;
+    if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343: scores, then the axis-0 softmax weights
+      const float* w12 = p->d_packed + p->pk_w12;
+      tm.begin(K_OTHER, 0, 0);
+      for (size_t s = 0; s < mp.src.size(); ++s) {
+        const int se = mp.src[s].entity;
+        HIP_TRY(launch_dense_fwd(sbases.base[s], b->rows[se] + b->halo[se], mp.din, mp.din, nullptr, w12, nullptr, 1,
+                                 IGN_ACT_LINEAR, mb.d_s_src[s], st));
+      }
+      HIP_TRY(launch_dense_fwd(hin, mb.n_dst, cp.H, cp.H, nullptr, w12 + p->attn_F, nullptr, 1, IGN_ACT_LINEAR,
+                               mb.d_s_dst, st));
+      AttnArgs aa{mb.d_group_ptr, mb.d_group_empty, mb.d_cell_dst, mb.d_cell_ptr, mb.d_cell_msgs, mb.d_msg_src,
+                  {mb.d_s_src[0], mb.d_s_src[1], mb.d_s_src[2], mb.d_s_src[3]}, mb.d_s_dst, mb.d_ecell, mb.d_msg_w,
+                  mb.n_groups};
+      HIP_TRY(launch_attn_softmax(aa, st));
+      tm.end();
+    }
     if (count > 0) {
       SumGruArgs a{hin, hout, sbases, mb.d_order + first, mb.d_msg_ptr + first, mb.d_msg_src,
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count, p->xcd_remap};
+      if (mp.aggr == IGN_AGGR_ATTENTION) a.msg_w = mb.d_msg_w;
+      if (mp.aggr == IGN_AGGR_CONVOLUTION) {
+        a.conv_kp = p->d_packed + p->pk_conv;
+        a.conv_act = mp.act;
+      }
       const double frac = mb.n_dst ? (double)count / mb.n_dst : 0.0;
       tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac);
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));

@@ -52,6 +52,7 @@ struct MPP {
   std::vector<ign_source_desc> src;
   bool sorted;                    // sorted (sequence) update vs single-step update
   int din;
+  int act = 0;                    // convolution activation (AUX:370-374)
 };
 
 
@@ -71,6 +72,18 @@ struct MPB {
   int64_t n_interior = 0;         // sum MPs: order[0, n_interior) reads no halo row
   int32_t* d_multi_ptr = nullptr;
   uint32_t* d_multi_rows = nullptr;
+  // attention (AUX:264-343): per-message softmax weights over dense (destination, position)
+  // cells, grouped per (graph, position) for the axis-0 softmax
+  int64_t n_cells = 0, n_groups = 0;
+  float* d_msg_w = nullptr;       // [n_msgs] in CSR order
+  int32_t* d_group_ptr = nullptr; // [n_groups + 1] cell ranges
+  int32_t* d_group_empty = nullptr;
+  int32_t* d_cell_dst = nullptr;
+  int32_t* d_cell_ptr = nullptr;  // [n_cells + 1] ranges of d_cell_msgs
+  int32_t* d_cell_msgs = nullptr; // CSR message positions
+  float* d_ecell = nullptr;
+  float* d_s_src[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  float* d_s_dst = nullptr;
   double flops = 0, bytes = 0;    // algorithmic, per launch
   // host copies of the index tables (the training path builds their transposes)
   std::vector<int32_t> h_order, h_len, h_step_ptr, h_msg_ptr, h_multi_ptr;
@@ -94,6 +107,10 @@ struct ign_plan {
   std::vector<CellP> cells;
   std::vector<int> ro_in;
   std::vector<DenseP> dense;
+  // one convolution / attention weight set per plan (GM:288-300: the last MP's weights serve all)
+  int conv_F = 0, attn_F = 0;
+  int64_t off_conv = -1, off_k1 = -1, off_k2 = -1, off_att = -1;
+  int64_t pk_conv = -1, pk_w12 = -1;
   std::vector<Tensor> tensors;
   int64_t n_params = 0, n_packed = 0;
   float* d_params = nullptr;

@@ -45,6 +45,25 @@ struct SumGruArgs {
   int64_t n_dst;
   int xcd_remap;
   float* x_save = nullptr;   // training: [rows][DIN] aggregated messages, by destination row
+  const float* msg_w = nullptr;    // attention: per-message weight (CSR order), x = sum w_m h_src
+  const float* conv_kp = nullptr;  // convolution: packed kernel; x = act((sum h_src . K + h) / deg)
+  int conv_act = 0;
+};
+
+// Attention weights (AUX:287-343): per (graph, position) group of dense cells, the axis-0 softmax
+// of e = LeakyReLU_0.2(s_src + s_dst) summed per cell, written to every message of the cell.
+struct AttnArgs {
+  const int32_t* group_ptr;
+  const int32_t* group_empty;      // empty cells of the group (they score 0 in the softmax)
+  const int32_t* cell_dst;
+  const int32_t* cell_ptr;
+  const int32_t* cell_msgs;        // CSR message positions
+  const uint32_t* msg_src;         // message codes (slot << 29 | row)
+  const float* s_src[IGN_MAX_SLOTS];   // h_src . (K1 a1) per source row
+  const float* s_dst;              // h_dst . (K2 a2) per destination row
+  float* ecell;
+  float* msg_w;
+  int64_t n_groups;
 };
 
 struct Readout3Args {
@@ -77,3 +96,6 @@ hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, c
                               hipStream_t st);
 hipError_t launch_gather_rows(const float* src, int64_t ld, const int32_t* idx, int64_t n, int cols, float* dst,
                               hipStream_t st);
+hipError_t launch_attn_softmax(const AttnArgs& a, hipStream_t st);
+// w12[0:F] = K1 . a[0:F], w12[F:2F] = K2 . a[F:2F]  (attention score vectors)
+hipError_t launch_attn_vectors(const float* K1, const float* K2, const float* a, int F, float* w12, hipStream_t st);

@@ -464,7 +464,10 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
-template <int DIN, int H>
+// MODE 0 sum (AUX:261); 1 attention: messages weighted by their softmax coefficient (AUX:339-342);
+// 2 convolution: x = act((sum_m h_src . K + h) / deg) (AUX:384-401; K.sum = sum.K, exact
+// reassociation).  Then one GRU step (AUX:764).
+template <int DIN, int H, int MODE>
 __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
   constexpr int NC = DIN / 16, NT = H / 16;
   __shared__ float sbias[4 * H];
@@ -489,32 +492,58 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
     int64_t m = m0;
-    for (; m + 4 <= m1; m += 4) {
-      uint32_t c0 = a.msg_src[m], c1 = a.msg_src[m + 1], c2 = a.msg_src[m + 2], c3 = a.msg_src[m + 3];
-      const float* p0 = src_ptr(a.src, c0, DIN);
-      const float* p1 = src_ptr(a.src, c1, DIN);
-      const float* p2 = src_ptr(a.src, c2, DIN);
-      const float* p3 = src_ptr(a.src, c3, DIN);
-      f4 v0[NC], v1[NC], v2[NC], v3[NC];
+    if constexpr (MODE == 1) {
+      for (; m < m1; ++m) {
+        const float w = a.msg_w[m];
+        const float* p = src_ptr(a.src, a.msg_src[m], DIN);
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        v0[c] = ld4(p0 + 16 * c + 4 * g);
-        v1[c] = ld4(p1 + 16 * c + 4 * g);
-        v2[c] = ld4(p2 + 16 * c + 4 * g);
-        v3[c] = ld4(p3 + 16 * c + 4 * g);
+        for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g) * w;
       }
+    } else {
+      for (; m + 4 <= m1; m += 4) {
+        uint32_t c0 = a.msg_src[m], c1 = a.msg_src[m + 1], c2 = a.msg_src[m + 2], c3 = a.msg_src[m + 3];
+        const float* p0 = src_ptr(a.src, c0, DIN);
+        const float* p1 = src_ptr(a.src, c1, DIN);
+        const float* p2 = src_ptr(a.src, c2, DIN);
+        const float* p3 = src_ptr(a.src, c3, DIN);
+        f4 v0[NC], v1[NC], v2[NC], v3[NC];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] = (((x[c] + v0[c]) + v1[c]) + v2[c]) + v3[c];
-    }
-    for (; m < m1; ++m) {
-      const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+        for (int c = 0; c < NC; ++c) {
+          v0[c] = ld4(p0 + 16 * c + 4 * g);
+          v1[c] = ld4(p1 + 16 * c + 4 * g);
+          v2[c] = ld4(p2 + 16 * c + 4 * g);
+          v3[c] = ld4(p3 + 16 * c + 4 * g);
+        }
 #pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+        for (int c = 0; c < NC; ++c) x[c] = (((x[c] + v0[c]) + v1[c]) + v2[c]) + v3[c];
+      }
+      for (; m < m1; ++m) {
+        const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+      }
     }
 
     f4 h[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    if constexpr (MODE == 2) {
+      static_assert(MODE != 2 || DIN == H, "convolution needs message dim == destination dim");
+      f4 y[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) y[c] = f4{0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < DIN / 4; ++s) {
+        const float xb = x[s >> 2][s & 3];
+#pragma unroll
+        for (int t = 0; t < NC; ++t) y[t] = MFMA(a.conv_kp[frag_idx(t, s, DIN / 4, lane)], xb, y[t]);
+      }
+      const float deg = (float)(m1 - m0);   // no neighbour: 0/0 or h/0, as the reference divides
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[c][r] = act_apply((y[c][r] + h[c][r]) / deg, a.conv_act);
+    }
     if (a.x_save && valid) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
@@ -525,6 +554,51 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
     }
   }
+}
+
+// Attention softmax weights: one wave per (graph, position) group.
+__global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t grp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (grp >= a.n_groups) return;
+  const int c0 = a.group_ptr[grp], c1 = a.group_ptr[grp + 1];
+  if (c0 == c1) return;   // only empty cells: no message reads this group
+  float mx = a.group_empty[grp] > 0 ? 0.f : -INFINITY;
+  for (int c = c0 + lane; c < c1; c += 64) {
+    const float sd = a.s_dst[a.cell_dst[c]];
+    float e = 0.f;
+    for (int q = a.cell_ptr[c]; q < a.cell_ptr[c + 1]; ++q) {
+      const uint32_t code = a.msg_src[a.cell_msgs[q]];
+      const float v = a.s_src[code >> IGN_SLOT_SHIFT][code & IGN_ROW_MASK] + sd;
+      e += v > 0.f ? v : 0.2f * v;                       // LeakyReLU(alpha=0.2), scatter_nd adds
+    }
+    a.ecell[c] = e;
+    mx = fmaxf(mx, e);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float z = 0.f;
+  for (int c = c0 + lane; c < c1; c += 64) z += __expf(a.ecell[c] - mx);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) z += __shfl_xor(z, o);
+  z += (float)a.group_empty[grp] * __expf(-mx);         // empty cells hold 0
+  const float inv = 1.0f / z;
+  for (int c = c0 + lane; c < c1; c += 64) {
+    const float w = __expf(a.ecell[c] - mx) * inv;
+    for (int q = a.cell_ptr[c]; q < a.cell_ptr[c + 1]; ++q) a.msg_w[a.cell_msgs[q]] = w;
+  }
+}
+
+__global__ void attn_vectors_kernel(const float* __restrict__ K1, const float* __restrict__ K2,
+                                    const float* __restrict__ av, int F, float* __restrict__ w12) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * F) return;
+  const float* K = i < F ? K1 : K2;
+  const int r = i < F ? i : i - F;
+  const float* aa = i < F ? av : av + F;
+  float s = 0.f;
+  for (int jj = 0; jj < F; ++jj) s += K[r * F + jj] * aa[jj];
+  w12[i] = s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1279,9 +1353,13 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
   // one tile per wave: measured faster than a persistent grid for this latency-bound gather
   // (0.109 vs 0.141 ms on 512 x synth50): more independent waves queue behind the resident ones
   dim3 grid(grid_for(args.n_dst, 64));
+  const int mode = args.conv_kp ? 2 : args.msg_w ? 1 : 0;
 #define SUM_CASE(D, HH)                                                                    \
   if (din == D && h == HH) {                                                               \
-    hipLaunchKernelGGL((sum_gru_kernel<D, HH>), grid, dim3(256), 0, st, args);             \
+    if (mode == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 1>), grid, dim3(256), 0, st, args); \
+    else if (mode == 2 && D == HH) hipLaunchKernelGGL((sum_gru_kernel<D, (D == HH ? HH : D), (D == HH ? 2 : 0)>), grid, dim3(256), 0, st, args); \
+    else if (mode == 2) return hipErrorInvalidValue;                                       \
+    else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args);    \
     return hipGetLastError();                                                              \
   }
   SUM_CASE(32, 32)
@@ -1290,6 +1368,7 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
   SUM_CASE(32, 16)
 #undef SUM_CASE
   if (din == 64 && h == 64) {
+    if (mode != 0) return hipErrorInvalidValue;
     if (variant == 5) {
       constexpr int WV = 12;
       auto kern = sum_gru_pf_kernel<64, 64, WV, 4, 16>;
@@ -1361,5 +1440,16 @@ hipError_t launch_gather_rows(const float* src, int64_t ld, const int32_t* idx, 
   const int64_t total = n * (cols / 4);
   int blocks = (int)std::min<int64_t>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, st, src, ld, idx, n, cols, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_softmax(const AttnArgs& a, hipStream_t st) {
+  if (a.n_groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)((a.n_groups + 3) / 4)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_vectors(const float* K1, const float* K2, const float* a, int F, float* w12, hipStream_t st) {
+  hipLaunchKernelGGL(attn_vectors_kernel, dim3((2 * F + 63) / 64), dim3(64), 0, st, K1, K2, a, F, w12);
   return hipGetLastError();
 }

@@ -70,6 +70,8 @@ class MPPlan:
     dense: list = field(default_factory=list)          # [(name, units, act, use_bias, l2)]
     iterations: int = 0
     readout_label: str = ""
+    convolution_dim: int = 0                           # F of convolution/kernel [F, F] (0: none)
+    attention_dim: int = 0                             # F of the attention weights (0: none)
 
     @classmethod
     def from_model_info(cls, mi) -> "MPPlan":
@@ -99,8 +101,14 @@ class MPPlan:
                 if extra:
                     raise UnsupportedModel("GRU options %s are not lowered (Keras defaults only)" % sorted(extra))
                 aggr = mp.aggregation.type
-                if aggr not in ("sum", "ordered", "interleave", "concat"):
+                if aggr not in ("sum", "ordered", "interleave", "concat", "attention", "convolution"):
                     raise UnsupportedModel("aggregation %r is not lowered yet" % aggr)
+                act = 0
+                if aggr == "convolution":       # AUX:370-374: activation_function, default relu
+                    fn = getattr(mp.aggregation, "activation_function", "relu")
+                    if fn not in _lib.ACT:
+                        raise UnsupportedModel("convolution activation %r is not lowered" % fn)
+                    act = _lib.ACT[fn]
                 if aggr == "concat" and mp.aggregation.concat_axis != 1:
                     raise UnsupportedModel("concat aggregation on axis 2 is not lowered yet")
                 srcs = []
@@ -124,7 +132,11 @@ class MPPlan:
                     cell_of[dst] = len(p.cells)
                     p.cells.append((dst, din, p.hidden[eidx[dst]]))
                 p.mps.append({"dst": eidx[dst], "aggr": aggr, "axis": getattr(mp.aggregation, "concat_axis", 0),
-                              "cell": cell_of[dst], "sources": srcs, "stage": stage_name})
+                              "cell": cell_of[dst], "sources": srcs, "stage": stage_name, "act": act})
+                if aggr in ("attention", "convolution"):
+                    # one weight set per model: the reference overwrites self.kernel1 / conv_kernel per
+                    # MP and every MP uses the last one (GM:288-300)
+                    setattr(p, aggr + "_dim", p.hidden[eidx[dst]])
         preds = [op for op in mi.get_readout_operations() if op.type == "predict"]
         others = [op for op in mi.get_readout_operations() if op.type != "predict"]
         if others:
@@ -161,7 +173,7 @@ class MPPlan:
             srcs = (_lib.SourceDesc * len(m["sources"]))(*[_lib.SourceDesc(*s) for s in m["sources"]])
             keep.append(srcs)
             mps[i] = _lib.MPDesc(m["dst"], _lib.AGGR[m["aggr"]], int(m["axis"] or 0), m["cell"], len(m["sources"]),
-                                 C.cast(srcs, C.POINTER(_lib.SourceDesc)))
+                                 C.cast(srcs, C.POINTER(_lib.SourceDesc)), int(m.get("act", 0)))
         cells = (_lib.CellDesc * len(self.cells))(*[_lib.CellDesc(din, h) for _, din, h in self.cells])
         ro = (C.c_int32 * len(self.readout_inputs))(*self.readout_inputs)
         dense = (_lib.DenseDesc * len(self.dense))(*[_lib.DenseDesc(u, a, b, l2) for _, u, a, b, l2 in self.dense])
@@ -178,6 +190,12 @@ class MPPlan:
         for dst, din, h in self.cells:
             specs += [(dst + "_update/kernel", (din, 3 * h)), (dst + "_update/recurrent_kernel", (h, 3 * h)),
                       (dst + "_update/bias", (2, 3 * h))]
+        if self.convolution_dim:
+            F = self.convolution_dim
+            specs.append(("convolution/kernel", (F, F)))
+        if self.attention_dim:
+            F = self.attention_dim
+            specs += [("attention/kernel1", (F, F)), ("attention/kernel2", (F, F)), ("attention/attn_kernel", (2 * F, 1))]
         width = sum(self.hidden[e] for e in self.readout_inputs)
         fan_in = width
         for li, (name, units, _, use_bias, _) in enumerate(self.dense):
@@ -198,7 +216,7 @@ class MPPlan:
                 q, r = np.linalg.qr(a)
                 q = q * np.sign(np.diag(r))
                 out[name] = q.T.astype(np.float32)
-            elif name.endswith("kernel"):
+            elif name.endswith("kernel") or name.endswith("kernel1") or name.endswith("kernel2"):
                 lim = np.sqrt(6.0 / (shape[0] + shape[1]))
                 out[name] = rng.uniform(-lim, lim, shape).astype(np.float32)
             else:

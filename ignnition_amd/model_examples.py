@@ -32,6 +32,24 @@ def _gru_update():
     return {"type": "recurrent_neural_network", "nn_name": "recurrent1"}
 
 
+def routenet_aggregation(aggregation: dict, hidden: int = 32, iterations: int = 8) -> dict:
+    """RouteNet with the path -> link stage aggregated by ``aggregation`` (e.g. {"type":
+    "attention"} or {"type": "convolution", "activation_function": "relu"}): schema-legal
+    aggregations outside the example configs (AUX:264-401)."""
+    d = routenet(hidden, iterations)
+    d["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = dict(aggregation)
+    return d
+
+
+def qsize_aggregation(aggregation: dict, iterations: int = 8) -> dict:
+    """Q-size with the {link, node} -> path stage aggregated by ``aggregation`` instead of
+    interleave: a two-source attention / convolution (AUX:264-401 with GM:523-541)."""
+    d = qsize(iterations=iterations)
+    mp = d["message_passing"]["stages"][0]["stage_mp"][0]
+    mp["aggregation"] = dict(aggregation)
+    return d
+
+
 def routenet(hidden: int = 32, iterations: int = 8) -> dict:
     """RNJ:1-165."""
     layer_names = ["1st_dense_layer", "2nd_dense_layer", "Output_layer"]

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 3
+#define IGN_ABI_VERSION 4
 
 enum ign_status {
   IGN_OK = 0,
@@ -90,6 +90,7 @@ typedef struct {
   int32_t cell;                    /* GRU cell index (one per destination entity name, GM:313) */
   int32_t num_sources;
   const ign_source_desc* sources;  /* in model_description order (GM:423) */
+  int32_t activation;              /* IGN_AGGR_CONVOLUTION: activation_function (AUX:370-374) */
 } ign_mp_desc;
 
 typedef struct {
@@ -166,7 +167,10 @@ void ign_plan_destroy(ign_plan* plan);
 int  ign_plan_num_params(const ign_plan* plan, int64_t* n_floats);
 int  ign_plan_num_param_tensors(const ign_plan* plan, int32_t* n);
 /* tensor i: kind 0 gru kernel [in,3H], 1 gru recurrent_kernel [H,3H], 2 gru bias [2,3H],
- *           3 dense kernel [in,out], 4 dense bias [1,out]; owner = cell or dense index */
+ *           3 dense kernel [in,out], 4 dense bias [1,out]; owner = cell or dense index;
+ *           5 convolution kernel [F,F], 6 attention kernel1 [F,F], 7 attention kernel2 [F,F],
+ *           8 attention attn_kernel [2F,1] (one set per plan, GM:288-300; owner -1).
+ * Order: cells, convolution, attention, Dense layers. */
 int  ign_plan_param_tensor(const ign_plan* plan, int32_t i, int32_t* kind, int32_t* owner,
                            int64_t* offset, int32_t* rows, int32_t* cols);
 int  ign_plan_set_params(ign_plan* plan, const float* params, int32_t on_device);

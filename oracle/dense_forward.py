@@ -172,8 +172,13 @@ class DenseOracle:
             else:                                                         # GM:523-543
                 if first:
                     src_input, final_len, first = s, lens, False
+                    comb_src, comb_dst, comb_seq = msgs, dst_idx, seq      # GM:528
                 else:
                     src_input = np.concatenate([src_input, s], axis=1)
+                    comb_src = np.concatenate([comb_src, msgs], axis=0)   # GM:533-541
+                    comb_dst = np.concatenate([comb_dst, dst_idx], axis=0)
+                    # quirk: the offset is this source's own lens (GM:539-540)
+                    comb_seq = np.concatenate([comb_seq, seq + lens[dst_idx]], axis=0)
                     final_len = final_len + lens
 
         if aggr == "sum":                                                 # AUX:261
@@ -188,8 +193,27 @@ class DenseOracle:
             out = np.zeros_like(t)
             np.add.at(out, flat, t)
             src_input = np.transpose(out, (1, 0, 2))
-        elif aggr in ("attention", "convolution"):
-            raise OracleError("aggregation %s not restated" % aggr)
+        elif aggr == "attention":                                         # AUX:287-343
+            K1, K2, A = (self.p["attention/kernel1"], self.p["attention/kernel2"], self.p["attention/attn_kernel"])
+            t_src = comb_src @ K1
+            t_dst = dst_states[comb_dst] @ K2
+            ai = np.concatenate([t_src, t_dst], axis=1) @ A               # [E, 1]
+            ai = np.where(ai > 0, ai, 0.2 * ai)                           # LeakyReLU(alpha=0.2)
+            max_len = int(comb_seq.max()) + 1
+            aux = _scatter_nd(comb_dst, comb_seq, ai, (num_dst, max_len, 1))
+            aux = aux - aux.max(axis=0, keepdims=True)                    # softmax over axis 0 (AUX:336)
+            coef = np.exp(aux) / np.exp(aux).sum(axis=0, keepdims=True)
+            fc = coef[comb_dst, comb_seq]                                 # gather_nd, [E, 1]
+            src_input = np.zeros((num_dst, comb_src.shape[1]), dt)
+            np.add.at(src_input, comb_dst, comb_src * fc)                 # unsorted_segment_sum
+        elif aggr == "convolution":                                       # AUX:384-401
+            Kc = self.p["convolution/kernel"]
+            ns = np.zeros((num_dst, Kc.shape[1]), dt)
+            np.add.at(ns, comb_dst, comb_src @ Kc)
+            deg = np.bincount(comb_dst, minlength=num_dst)[:num_dst].astype(dt)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                src_input = (ns + dst_states) / deg[:, None]
+            src_input = _act(src_input, mp["aggregation"].get("activation_function", "relu"))
 
         upd = mp["update"]
         if upd["type"] != "recurrent_neural_network":

@@ -245,3 +245,32 @@ def test_timing_kinds_mask():
     st = eng.stats()
     assert st["seq_gru"]["launches"] == plan.iterations and st["seq_gru"]["ms"] > 0
     assert st["readout"]["launches"] == 0 and st["sum_gru"]["launches"] == 0
+
+
+# ---------------------------------------------------------------------------------------------
+# schema-legal aggregations outside the example configs (AUX:264-401)
+def _variant_inputs(desc, kind, n, seed0=0):
+    _, dims, _ = workloads.model(kind)
+    mi = Model_information(copy.deepcopy(desc), dims)
+    samples = [synthetic.routenet_sample("nsfnet", seed0 + g, qsize=(kind == "qsize")) for g in range(n)]
+    graphs, _ = workloads.graph_inputs(mi, samples)
+    return dims, graphs
+
+
+@pytest.mark.parametrize("aggr", [{"type": "attention"}, {"type": "convolution"},
+                                  {"type": "convolution", "activation_function": "tanh"}])
+@pytest.mark.parametrize("n", [1, 3])
+def test_routenet_attention_convolution(aggr, n):
+    desc = model_examples.routenet_aggregation(aggr, hidden=32, iterations=3)
+    dims, graphs = _variant_inputs(desc, "routenet", n)
+    out, ref, _, _ = _run(desc, dims, graphs, seed=5, bias=0.1)
+    _close(out, ref)
+
+
+@pytest.mark.parametrize("aggr", [{"type": "attention"}, {"type": "convolution"}])
+def test_two_source_attention_convolution(aggr):
+    """{link, node} -> path: the combined edge list and the attention position quirk (GM:539-541)."""
+    desc = model_examples.qsize_aggregation(aggr, iterations=3)
+    dims, graphs = _variant_inputs(desc, "qsize", 2)
+    out, ref, _, _ = _run(desc, dims, graphs, seed=6, bias=0.1)
+    _close(out, ref)
