@@ -127,10 +127,27 @@ def test_lowering_qsize():
 
 def test_lowering_rejects_unsupported():
     d = model_examples.routenet()
-    d["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = {"type": "attention"}
+    d["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = {"type": "concat", "concat_axis": 2}
+    with pytest.raises(UnsupportedModel):
+        MPPlan.from_model_info(Model_information(d, DIMS))
+    d = model_examples.routenet()
+    d["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = {"type": "convolution",
+                                                                       "activation_function": "softplus"}
     with pytest.raises(UnsupportedModel):
         MPPlan.from_model_info(Model_information(d, DIMS))
     d = model_examples.routenet()
     d["neural_networks"][1]["recurrent_type"] = "LSTM"
     with pytest.raises(UnsupportedModel):
         MPPlan.from_model_info(Model_information(d, DIMS))
+
+
+def test_attention_convolution_lowering():
+    """AUX:264-401: one shared weight set each (GM:288-300), names and shapes in the layout."""
+    d = model_examples.routenet_aggregation({"type": "attention"})
+    plan = MPPlan.from_model_info(Model_information(d, DIMS))
+    names = dict(plan.param_specs())
+    assert names["attention/kernel1"] == (32, 32) and names["attention/attn_kernel"] == (64, 1)
+    d = model_examples.routenet_aggregation({"type": "convolution", "activation_function": "tanh"})
+    plan = MPPlan.from_model_info(Model_information(d, DIMS))
+    assert dict(plan.param_specs())["convolution/kernel"] == (32, 32)
+    assert plan.mps[1]["act"] == 4
