@@ -118,6 +118,14 @@ int ign::repack(ign_plan* p) {
       HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
     }
   }
+  for (auto& mp : p->mps)
+    if (mp.feature_concat) {
+      const CellP& cp = p->cells[mp.cell];
+      for (size_t s = 0; s < mp.src.size(); ++s)
+        HIP_TRY(launch_pack_gru(p->d_params + cp.off_k + (int64_t)mp.slice_off[s] * 3 * cp.H, nullptr, nullptr,
+                                p->d_packed + mp.pk_slice[s], nullptr, nullptr, p->ents[mp.src[s].entity].hidden_dim,
+                                cp.H, p->stream));
+    }
   if (p->pk_conv >= 0)
     HIP_TRY(launch_pack_dense(p->d_params + p->off_conv, p->d_packed + p->pk_conv, p->conv_F, p->conv_F, p->stream));
   if (p->pk_w12 >= 0)
@@ -196,9 +204,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
           return fail(IGN_ERR_UNSUPPORTED, "mp %d: interleave aggregation supports exactly 2 sources (GM:518)", m);
         break;
       case IGN_AGGR_CONCAT:
-        if (mp.concat_axis != 1)
-          return fail(IGN_ERR_UNSUPPORTED, "mp %d: concat aggregation on axis %d is not lowered yet", m, mp.concat_axis);
+        if (mp.concat_axis != 1 && mp.concat_axis != 2)
+          return fail(IGN_ERR_INVALID, "mp %d: concat_axis must be 1 or 2", m);
         mp.sorted = true;
+        mp.feature_concat = mp.concat_axis == 2;
         break;
       case IGN_AGGR_ATTENTION:
       case IGN_AGGR_CONVOLUTION:
@@ -217,6 +226,11 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
       if (mp.aggr == IGN_AGGR_INTERLEAVE && (s.interleave < 0 || s.interleave >= p->n_il))
         return fail(IGN_ERR_INVALID, "mp %d: interleave slot missing", m);
       int dm = p->ents[s.entity].hidden_dim;   // direct_assignation: message = source state
+      if (mp.feature_concat) {                 // axis 2: the step input is the sources' concatenation
+        mp.slice_off.push_back(din < 0 ? 0 : din);
+        din = (din < 0 ? 0 : din) + dm;
+        continue;
+      }
       if (din >= 0 && dm != din)
         return fail(IGN_ERR_INVALID, "mp %d: sources have different message dimensions (%d vs %d)", m, din, dm);
       din = dm;
@@ -228,9 +242,15 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
       return fail(IGN_ERR_INVALID, "mp %d: cell units %d != destination hidden dim %d", m, cp.H, p->ents[mp.dst].hidden_dim);
     if (cp.din != din)
       return fail(IGN_ERR_INVALID, "mp %d: cell input_dim %d != message dim %d", m, cp.din, din);
-    if (!gru_shape_supported(din, cp.H))
+    if (mp.feature_concat) {   // x.W is hoisted per source slice: the shapes that matter are (slice, H)
+      for (auto& s : mp.src)
+        if (!gru_shape_supported(p->ents[s.entity].hidden_dim, cp.H))
+          return fail(IGN_ERR_UNSUPPORTED, "mp %d: concat slice (input %d, units %d) not instantiated", m,
+                      p->ents[s.entity].hidden_dim, cp.H);
+    } else if (!gru_shape_supported(din, cp.H)) {
       return fail(IGN_ERR_UNSUPPORTED, "mp %d: GRU shape (input %d, units %d) not instantiated (16/32, 64/64)", m,
                   din, cp.H);
+    }
     if (mp.aggr == IGN_AGGR_ATTENTION || mp.aggr == IGN_AGGR_CONVOLUTION) {
       const int F = p->ents[mp.dst].hidden_dim;
       // AUX:311-319 / GM:293-298: the messages and the destination states must have one width
@@ -326,6 +346,12 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (!row_gemm_supported(dp.out, dp.in)) continue;
     dp.pk_wt = pk; pk = align(pk + (int64_t)dp.in * dp.out);
   }
+  for (auto& mp : p->mps)
+    if (mp.feature_concat)
+      for (auto& s : mp.src) {
+        mp.pk_slice.push_back(pk);
+        pk = align(pk + 3LL * p->ents[s.entity].hidden_dim * p->cells[mp.cell].H);
+      }
   if (p->conv_F) { p->pk_conv = pk; pk = align(pk + (int64_t)p->conv_F * p->conv_F); }
   if (p->attn_F) { p->pk_w12 = pk; pk = align(pk + 2LL * p->attn_F); }
   p->n_packed = pk;
@@ -531,6 +557,13 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         lmax[s] = mx + 1;
         total_slots += lmax[s];
       }
+      if (mp.feature_concat) {   // tf.concat on axis 2 needs every source's [N, Lmax] to match
+        for (int s = 1; s < S; ++s)
+          if (lmax[s] != lmax[0])
+            return fail(IGN_ERR_INVALID, "graph %d: concat on axis 2 of sequences of length %lld and %lld "
+                        "(ConcatOp dimension mismatch, GM:503)", g, (long long)lmax[0], (long long)lmax[s]);
+        total_slots = lmax[0];
+      }
       if (mp.aggr == IGN_AGGR_INTERLEAVE && (int64_t)ilflat.size() != total_slots)
         return fail(IGN_ERR_INVALID, "graph %d: interleave indices cover %lld slots but the messages need %lld"
                     " (scatter_nd shape mismatch, AUX:435)", g, (long long)ilflat.size(), (long long)total_slots);
@@ -561,11 +594,14 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
                           g, (long long)pos, (long long)total_slots);
           }
           if (mp.aggr == IGN_AGGR_ATTENTION) pos = sq + (s > 0 ? lens_s[di] : 0);
+          if (mp.feature_concat) pos = sq;   // all sources share the positions (axis-2 concat)
           int64_t drow = b->row_off[dst][g] + di;
           mdst.push_back(drow);
           mpos.push_back(pos);
           mcode.push_back(((uint32_t)s << IGN_SLOT_SHIFT) | (uint32_t)(b->row_off[se][g] + si));
-          flen[drow] += 1;   // final_len = sum of lens over sources (GM:505/519/543)
+          // final_len = sum of lens over sources (GM:505/519/543); axis-2 concat keeps the first
+          // source's lens (GM:503-505)
+          if (!mp.feature_concat || s == 0) flen[drow] += 1;
         }
         slot_off += lmax[s];
       }
@@ -890,9 +926,10 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     for (size_t s = 0; s < mp.src.size(); ++s) {
       const int64_t rs = mb.src_rows[s];
       tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3));
-      HIP_TRY(launch_project(sbases.base[s], rs, p->d_packed + cp.pk_w, p->d_packed + cp.pk_b,
-                             mb.d_table + mb.src_off[s] * W3, s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr,
-                             mp.din, cp.H, st));
+      const int sdin = mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : mp.din;
+      const float* wp = mp.feature_concat ? p->d_packed + mp.pk_slice[s] : p->d_packed + cp.pk_w;
+      HIP_TRY(launch_project(sbases.base[s], rs, wp, p->d_packed + cp.pk_b, mb.d_table + mb.src_off[s] * W3,
+                             s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr, sdin, cp.H, st));
       tm.end();
     }
     if (mb.n_multi) {

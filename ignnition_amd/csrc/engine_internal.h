@@ -53,6 +53,9 @@ struct MPP {
   bool sorted;                    // sorted (sequence) update vs single-step update
   int din;
   int act = 0;                    // convolution activation (AUX:370-374)
+  bool feature_concat = false;    // concat on axis 2 (AUX:443-456): step input = [src_1 | src_2 | ...]
+  std::vector<int> slice_off;     // feature_concat: first kernel row of each source's slice
+  std::vector<int64_t> pk_slice;  // feature_concat: packed W-slice fragments per source
 };
 
 

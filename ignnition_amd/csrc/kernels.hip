@@ -49,7 +49,8 @@ __global__ void pack_gru_kernel(const float* __restrict__ W, const float* __rest
   int64_t nU = 3LL * NT * (H / 4) * 64;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e = i; e < nW + nU + 4LL * H; e += stride) {
+  const int64_t total = Up ? nW + nU + 4LL * H : nW;   // Up == nullptr: W only (a concat slice)
+  for (int64_t e = i; e < total; e += stride) {
     if (e < nW + nU) {
       // float4-grouped fragments: idx = (((gate*NT + t)*KS/4 + s/4)*64 + lane)*4 + s%4, so one
       // 16-B read per lane yields 4 consecutive k-steps (global dwordx4, ds_read_b128, LDS copy)

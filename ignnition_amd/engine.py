@@ -109,8 +109,7 @@ class MPPlan:
                     if fn not in _lib.ACT:
                         raise UnsupportedModel("convolution activation %r is not lowered" % fn)
                     act = _lib.ACT[fn]
-                if aggr == "concat" and mp.aggregation.concat_axis != 1:
-                    raise UnsupportedModel("concat aggregation on axis 2 is not lowered yet")
+                feature_concat = aggr == "concat" and mp.aggregation.concat_axis == 2
                 srcs = []
                 din = None
                 for s in mp.source_entities:
@@ -127,7 +126,8 @@ class MPPlan:
                             p.il_slots.append(key)
                         il = p.il_slots.index(key)
                     srcs.append((eidx[s.name], p.adj_slots.index(slot), il))
-                    din = p.hidden[eidx[s.name]]
+                    # axis-2 concat feeds the GRU the sources' concatenated messages (AUX:443-456)
+                    din = (din or 0) + p.hidden[eidx[s.name]] if feature_concat else p.hidden[eidx[s.name]]
                 if dst not in cell_of:
                     cell_of[dst] = len(p.cells)
                     p.cells.append((dst, din, p.hidden[eidx[dst]]))

@@ -47,6 +47,8 @@ def qsize_aggregation(aggregation: dict, iterations: int = 8) -> dict:
     d = qsize(iterations=iterations)
     mp = d["message_passing"]["stages"][0]["stage_mp"][0]
     mp["aggregation"] = dict(aggregation)
+    if aggregation.get("type") == "concat":
+        d["message_passing"]["stages"][0]["stage_mp"][0].pop("interleave_definition", None)
     return d
 
 

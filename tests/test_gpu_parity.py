@@ -274,3 +274,13 @@ def test_two_source_attention_convolution(aggr):
     dims, graphs = _variant_inputs(desc, "qsize", 2)
     out, ref, _, _ = _run(desc, dims, graphs, seed=6, bias=0.1)
     _close(out, ref)
+
+
+@pytest.mark.parametrize("axis", [1, 2])
+def test_two_source_concat(axis):
+    """{link, node} -> path concatenated on axis 1 (slots) or 2 (features, AUX:443-456): the
+    axis-2 step input is [link message | node message], final_len the first source's lens."""
+    desc = model_examples.qsize_aggregation({"type": "concat", "concat_axis": axis}, iterations=3)
+    dims, graphs = _variant_inputs(desc, "qsize", 2)
+    out, ref, _, _ = _run(desc, dims, graphs, seed=7, bias=0.1)
+    _close(out, ref)

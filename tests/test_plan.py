@@ -127,9 +127,6 @@ def test_lowering_qsize():
 
 def test_lowering_rejects_unsupported():
     d = model_examples.routenet()
-    d["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = {"type": "concat", "concat_axis": 2}
-    with pytest.raises(UnsupportedModel):
-        MPPlan.from_model_info(Model_information(d, DIMS))
     d = model_examples.routenet()
     d["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = {"type": "convolution",
                                                                        "activation_function": "softplus"}
