@@ -21,8 +21,14 @@ class EntityDesc(C.Structure):
     _fields_ = [("hidden_dim", i32), ("feature_total", i32)]
 
 
+class DenseDesc(C.Structure):
+    _fields_ = [("units", i32), ("activation", i32), ("use_bias", i32), ("l2", f32)]
+
+
 class SourceDesc(C.Structure):
-    _fields_ = [("entity", i32), ("adjacency", i32), ("interleave", i32)]
+    _fields_ = [("entity", i32), ("adjacency", i32), ("interleave", i32), ("msg_num_inputs", i32),
+                ("msg_inputs", C.POINTER(i32)), ("msg_param_dim", i32), ("msg_num_layers", i32),
+                ("msg_layers", C.POINTER(DenseDesc))]
 
 
 class MPDesc(C.Structure):
@@ -32,10 +38,6 @@ class MPDesc(C.Structure):
 
 class CellDesc(C.Structure):
     _fields_ = [("input_dim", i32), ("units", i32)]
-
-
-class DenseDesc(C.Structure):
-    _fields_ = [("units", i32), ("activation", i32), ("use_bias", i32), ("l2", f32)]
 
 
 class PlanDesc(C.Structure):
@@ -51,7 +53,7 @@ class BatchDesc(C.Structure):
                 ("adj_edges", C.POINTER(i64)), ("adj_src", C.POINTER(C.POINTER(i64))),
                 ("adj_dst", C.POINTER(C.POINTER(i64))), ("adj_seq", C.POINTER(C.POINTER(i64))),
                 ("interleave_len", C.POINTER(i64)), ("interleave_idx", C.POINTER(C.POINTER(i64))),
-                ("halo_rows", C.POINTER(i64))]
+                ("halo_rows", C.POINTER(i64)), ("adj_params", C.POINTER(C.POINTER(f32)))]
 
 
 class DatasetDesc(C.Structure):
@@ -74,6 +76,7 @@ class Stats(C.Structure):
 
 KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "project", "other"]
 
+MSG_INPUT = {"hs_source": 0, "hs_dest": 1, "edge_params": 2}
 AGGR = {"sum": 0, "ordered": 1, "interleave": 2, "concat": 3, "attention": 4, "convolution": 5}
 ACT = {None: 0, "None": 0, "linear": 0, "relu": 1, "selu": 2, "sigmoid": 3, "tanh": 4}
 
@@ -88,7 +91,7 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get"]
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 

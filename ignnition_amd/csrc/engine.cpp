@@ -126,6 +126,14 @@ int ign::repack(ign_plan* p) {
                                 p->d_packed + mp.pk_slice[s], nullptr, nullptr, p->ents[mp.src[s].entity].hidden_dim,
                                 cp.H, p->stream));
     }
+  for (auto& mp : p->mps)
+    for (auto& nn : mp.nn)
+      for (size_t l = 0; l < nn.layers.size(); ++l) {
+        const DenseP& dp = nn.layers[l];
+        if (dp.pk_w >= 0)
+          HIP_TRY(launch_pack_dense_pad(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in,
+                                        l == 0 ? nn.din_pad : dp.in, dp.out, p->stream));
+      }
   if (p->pk_conv >= 0)
     HIP_TRY(launch_pack_dense(p->d_params + p->off_conv, p->d_packed + p->pk_conv, p->conv_F, p->conv_F, p->stream));
   if (p->pk_w12 >= 0)
@@ -226,6 +234,39 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
       if (mp.aggr == IGN_AGGR_INTERLEAVE && (s.interleave < 0 || s.interleave >= p->n_il))
         return fail(IGN_ERR_INVALID, "mp %d: interleave slot missing", m);
       int dm = p->ents[s.entity].hidden_dim;   // direct_assignation: message = source state
+      MsgNN nn;
+      if (s.msg_num_layers > 0) {               // message-creation network (GM:440-475)
+        nn.param_dim = s.msg_param_dim;
+        for (int q = 0; q < s.msg_num_inputs; ++q) {
+          const int kind = s.msg_inputs[q];
+          nn.inputs.push_back(kind);
+          int w = 0;
+          if (kind == IGN_MSG_HS_SOURCE) w = p->ents[s.entity].hidden_dim;
+          else if (kind == IGN_MSG_HS_DEST) w = p->ents[mp.dst].hidden_dim;
+          else if (kind == IGN_MSG_EDGE_PARAMS) w = s.msg_param_dim;
+          else return fail(IGN_ERR_UNSUPPORTED, "mp %d: message input %d is not lowered", m, kind);
+          if (w <= 0) return fail(IGN_ERR_INVALID, "mp %d: message input %d has no width", m, kind);
+          if (q >= 4) return fail(IGN_ERR_UNSUPPORTED, "mp %d: more than 4 message inputs", m);
+          nn.widths.push_back(w);
+          nn.din += w;
+        }
+        if (nn.din <= 0) return fail(IGN_ERR_INVALID, "mp %d: empty message-network input", m);
+        nn.din_pad = (nn.din + 15) / 16 * 16;
+        int in = nn.din;
+        for (int l = 0; l < s.msg_num_layers; ++l) {
+          DenseP dp;
+          dp.in = in;
+          dp.out = s.msg_layers[l].units;
+          dp.act = s.msg_layers[l].activation;
+          dp.use_bias = s.msg_layers[l].use_bias;
+          if (dp.out <= 0) return fail(IGN_ERR_INVALID, "mp %d: message layer %d units", m, l);
+          if (!act_ok(dp.act)) return fail(IGN_ERR_UNSUPPORTED, "mp %d: message layer activation %d", m, dp.act);
+          nn.layers.push_back(dp);
+          in = dp.out;
+        }
+        dm = nn.dout();
+      }
+      mp.nn.push_back(nn);
       if (mp.feature_concat) {                 // axis 2: the step input is the sources' concatenation
         mp.slice_off.push_back(din < 0 ? 0 : din);
         din = (din < 0 ? 0 : din) + dm;
@@ -305,6 +346,13 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.off_rk = off; p->tensors.push_back({1, (int)c, off, cp.H, g3}); off = align(off + (int64_t)cp.H * g3);
     cp.off_b = off; p->tensors.push_back({2, (int)c, off, 2, g3}); off = align(off + 2LL * g3);
   }
+  for (size_t mi = 0; mi < p->mps.size(); ++mi)
+    for (size_t s = 0; s < p->mps[mi].nn.size(); ++s)
+      for (auto& dp : p->mps[mi].nn[s].layers) {
+        const int owner = (int)(mi * IGN_MAX_SLOTS + s);
+        dp.off_w = off; p->tensors.push_back({9, owner, off, dp.in, dp.out}); off = align(off + (int64_t)dp.in * dp.out);
+        if (dp.use_bias) { dp.off_b = off; p->tensors.push_back({10, owner, off, 1, dp.out}); off = align(off + dp.out); }
+      }
   if (p->conv_F) {
     const int F = p->conv_F;
     p->off_conv = off; p->tensors.push_back({5, -1, off, F, F}); off = align(off + (int64_t)F * F);
@@ -346,6 +394,13 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (!row_gemm_supported(dp.out, dp.in)) continue;
     dp.pk_wt = pk; pk = align(pk + (int64_t)dp.in * dp.out);
   }
+  for (auto& mp : p->mps)
+    for (auto& nn : mp.nn)
+      for (size_t l = 0; l < nn.layers.size(); ++l) {
+        DenseP& dp = nn.layers[l];
+        const int kin = l == 0 ? nn.din_pad : dp.in;
+        if (dense_fwd_supported(kin, dp.out)) { dp.pk_w = pk; pk = align(pk + (int64_t)kin * dp.out); }
+      }
   for (auto& mp : p->mps)
     if (mp.feature_concat)
       for (auto& s : mp.src) {
@@ -466,6 +521,9 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   }
   b->halo.assign(E, 0);
   if (d->halo_rows) {
+    for (auto& mp : p->mps)
+      for (auto& nn : mp.nn)
+        if (!nn.layers.empty()) return fail(IGN_ERR_UNSUPPORTED, "edge-cut partitions with message networks");
     for (int e = 0; e < E; ++e) {
       if (d->halo_rows[e] < 0) return fail(IGN_ERR_INVALID, "entity %d: negative halo_rows", e);
       b->halo[e] = d->halo_rows[e];
@@ -598,7 +656,9 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
           int64_t drow = b->row_off[dst][g] + di;
           mdst.push_back(drow);
           mpos.push_back(pos);
-          mcode.push_back(((uint32_t)s << IGN_SLOT_SHIFT) | (uint32_t)(b->row_off[se][g] + si));
+          // a message network's messages live per edge: the code addresses the edge (GM:440-475)
+          const int64_t mrow = mp.nn[s].layers.empty() ? b->row_off[se][g] + si : k;
+          mcode.push_back(((uint32_t)s << IGN_SLOT_SHIFT) | (uint32_t)mrow);
           // final_len = sum of lens over sources (GM:505/519/543); axis-2 concat keeps the first
           // source's lens (GM:503-505)
           if (!mp.feature_concat || s == 0) flen[drow] += 1;
@@ -612,6 +672,34 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
             return fail(IGN_ERR_INVALID, "graph %d: destination row %lld has final_len %lld > %lld padded slots"
                         " (gather_nd out of range, AUX:793-795)", g, (long long)(r - b->row_off[dst][g]),
                         (long long)flen[r], (long long)total_slots);
+      }
+    }
+    for (int s = 0; s < S; ++s) {   // message networks: per-edge rows and parameters (GM:440-475)
+      const MsgNN& nn = mp.nn[s];
+      if (nn.layers.empty()) continue;
+      const int a = mp.src[s].adjacency, se = mp.src[s].entity;
+      const int64_t ne = eoff[a][G];
+      if (ne >= (int64_t)IGN_ROW_MASK) return fail(IGN_ERR_UNSUPPORTED, "too many edges for a message network");
+      std::vector<int32_t> es(ne), ed(ne);
+      for (int g = 0; g < G; ++g)
+        for (int64_t k = eoff[a][g]; k < eoff[a][g + 1]; ++k) {
+          es[k] = (int32_t)(b->row_off[se][g] + d->adj_src[a][k]);
+          ed[k] = (int32_t)(b->row_off[dst][g] + d->adj_dst[a][k]);
+        }
+      mb.n_edges[s] = ne;
+      if ((rc = dev_upload(b.get(), &mb.d_edge_src[s], es)) || (rc = dev_upload(b.get(), &mb.d_edge_dst[s], ed))) return rc;
+      if (std::find(nn.inputs.begin(), nn.inputs.end(), (int)IGN_MSG_EDGE_PARAMS) != nn.inputs.end()) {
+        if (!d->adj_params || !d->adj_params[a])
+          return fail(IGN_ERR_INVALID, "message network of mp %zu reads edge_params but params_<adj> is missing", mi);
+        std::vector<float> prm(d->adj_params[a], d->adj_params[a] + ne * nn.param_dim);
+        if ((rc = dev_upload(b.get(), &mb.d_edge_params[s], prm))) return rc;
+      }
+      if ((rc = dev_alloc(b.get(), &mb.d_msg_in[s], ne * nn.din_pad))) return rc;
+      HIP_TRY(hipMemset(mb.d_msg_in[s], 0, ne * nn.din_pad * sizeof(float)));   // zero padding columns
+      for (auto& dp : nn.layers) {
+        float* f = nullptr;
+        if ((rc = dev_alloc(b.get(), &f, ne * dp.out))) return rc;
+        mb.d_msg_layer[s].push_back(f);
       }
     }
     mb.edges = tot;
@@ -641,8 +729,9 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       for (int s = 0; s < S; ++s) {
         mb.src_off.push_back(trow);
         const int se = mp.src[s].entity;
-        mb.src_rows.push_back(b->rows[se] + b->halo[se]);
-        trow += b->rows[se] + b->halo[se];
+        const int64_t rows_s = mp.nn[s].layers.empty() ? b->rows[se] + b->halo[se] : eoff[mp.src[s].adjacency][G];
+        mb.src_rows.push_back(rows_s);
+        trow += rows_s;
       }
       mb.zero_row = trow;
       auto table_row = [&](uint32_t code) -> int64_t {
@@ -779,8 +868,11 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if ((rc = dev_alloc(b.get(), &mb.d_msg_w, (int64_t)mdst.size())) || (rc = dev_alloc(b.get(), &mb.d_ecell, mb.n_cells)) ||
             (rc = dev_alloc(b.get(), &mb.d_s_dst, ND)))
           return rc;
-        for (int s = 0; s < S; ++s)
-          if ((rc = dev_alloc(b.get(), &mb.d_s_src[s], b->rows[mp.src[s].entity] + b->halo[mp.src[s].entity]))) return rc;
+        for (int s = 0; s < S; ++s) {
+          const int se = mp.src[s].entity;
+          const int64_t rows_s = mp.nn[s].layers.empty() ? b->rows[se] + b->halo[se] : eoff[mp.src[s].adjacency][G];
+          if ((rc = dev_alloc(b.get(), &mb.d_s_src[s], rows_s))) return rc;
+        }
       }
       mb.n_msgs = (int64_t)msrc.size();
       if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
@@ -878,6 +970,40 @@ struct Timer {
   }
 };
 
+// message network of one source: per-edge [inputs...] then the Dense stack into d_msg_layer[s]
+int run_message_net(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
+                    const float* dst_state, hipStream_t st) {
+  MsgGatherArgs g{};
+  g.out = mb.d_msg_in[s];
+  g.n = mb.n_edges[s];
+  g.ld = nn.din_pad;
+  g.nparts = (int)nn.inputs.size();
+  int col = 0;
+  for (int q = 0; q < g.nparts; ++q) {
+    const int kind = nn.inputs[q];
+    g.col[q] = col;
+    g.width[q] = nn.widths[q];
+    if (kind == IGN_MSG_HS_SOURCE) { g.base[q] = src_state; g.rows[q] = mb.d_edge_src[s]; }
+    else if (kind == IGN_MSG_HS_DEST) { g.base[q] = dst_state; g.rows[q] = mb.d_edge_dst[s]; }
+    else { g.base[q] = mb.d_edge_params[s]; g.rows[q] = nullptr; }
+    col += g.width[q];
+  }
+  HIP_TRY(launch_msg_gather(g, st));
+  const float* in = mb.d_msg_in[s];
+  int stride = nn.din_pad;
+  for (size_t l = 0; l < nn.layers.size(); ++l) {
+    const DenseP& dp = nn.layers[l];
+    const bool mfma = dp.pk_w >= 0;
+    const int K = l == 0 ? (mfma ? nn.din_pad : nn.din) : dp.in;
+    HIP_TRY(launch_dense_fwd(in, mb.n_edges[s], K, stride, mfma ? p->d_packed + dp.pk_w : nullptr,
+                             p->d_params + dp.off_w, dp.use_bias ? p->d_params + dp.off_b : nullptr, dp.out, dp.act,
+                             mb.d_msg_layer[s][l], st));
+    in = mb.d_msg_layer[s][l];
+    stride = dp.out;
+  }
+  return IGN_OK;
+}
+
 int check_pb(ign_plan* p, ign_batch* b) {
   if (!p || !b) return fail(IGN_ERR_INVALID, "null argument");
   if (b->plan != p) return fail(IGN_ERR_INVALID, "batch was created for another plan");
@@ -920,6 +1046,14 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   const int dst = mp.dst;
   const float* hin = b->d_state[b->cur[dst]][dst];
   float* hout = b->d_state[1 - b->cur[dst]][dst];
+  if (part != IGN_PART_BOUNDARY)
+    for (size_t s = 0; s < mp.src.size(); ++s) {   // message-creation networks (GM:440-475)
+      const MsgNN& nn = mp.nn[s];
+      if (nn.layers.empty()) continue;
+      if ((rc = run_message_net(p, nn, mb, (int)s, sbases.base[s], hin, st))) return rc;
+    }
+  for (size_t s = 0; s < mp.src.size(); ++s)
+    if (!mp.nn[s].layers.empty()) sbases.base[s] = mb.d_msg_layer[s].back();
   if (mp.sorted) {
     if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split is for sum MPs only");
     const int W3 = 3 * cp.H;
@@ -956,8 +1090,9 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       tm.begin(K_OTHER, 0, 0);
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const int se = mp.src[s].entity;
-        HIP_TRY(launch_dense_fwd(sbases.base[s], b->rows[se] + b->halo[se], mp.din, mp.din, nullptr, w12, nullptr, 1,
-                                 IGN_ACT_LINEAR, mb.d_s_src[s], st));
+        const int64_t rows_s = mp.nn[s].layers.empty() ? b->rows[se] + b->halo[se] : mb.n_edges[s];
+        HIP_TRY(launch_dense_fwd(sbases.base[s], rows_s, mp.din, mp.din, nullptr, w12, nullptr, 1, IGN_ACT_LINEAR,
+                                 mb.d_s_src[s], st));
       }
       HIP_TRY(launch_dense_fwd(hin, mb.n_dst, cp.H, cp.H, nullptr, w12 + p->attn_F, nullptr, 1, IGN_ACT_LINEAR,
                                mb.d_s_dst, st));

@@ -47,6 +47,15 @@ struct DenseP {
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
 };
 
+struct MsgNN {                    // message-creation network of one MP source (GM:440-475)
+  std::vector<int> inputs;        // enum ign_message_input, in order
+  std::vector<int> widths;        // floats per edge of each input part
+  int param_dim = 0;
+  int din = 0, din_pad = 0;       // concatenated input width, padded to 16 for the MFMA layers
+  std::vector<DenseP> layers;
+  int dout() const { return layers.empty() ? 0 : layers.back().out; }
+};
+
 struct MPP {
   int dst, aggr, concat_axis, cell;
   std::vector<ign_source_desc> src;
@@ -56,6 +65,7 @@ struct MPP {
   bool feature_concat = false;    // concat on axis 2 (AUX:443-456): step input = [src_1 | src_2 | ...]
   std::vector<int> slice_off;     // feature_concat: first kernel row of each source's slice
   std::vector<int64_t> pk_slice;  // feature_concat: packed W-slice fragments per source
+  std::vector<MsgNN> nn;          // per source; no layers = direct_assignation
 };
 
 
@@ -87,6 +97,13 @@ struct MPB {
   float* d_ecell = nullptr;
   float* d_s_src[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
   float* d_s_dst = nullptr;
+  // message networks: per source, the per-edge input, the layer outputs (last = the messages)
+  int64_t n_edges[IGN_MAX_SLOTS] = {0, 0, 0, 0};
+  int32_t* d_edge_src[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  int32_t* d_edge_dst[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  float* d_edge_params[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  float* d_msg_in[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<float*> d_msg_layer[IGN_MAX_SLOTS];
   double flops = 0, bytes = 0;    // algorithmic, per launch
   // host copies of the index tables (the training path builds their transposes)
   std::vector<int32_t> h_order, h_len, h_step_ptr, h_msg_ptr, h_multi_ptr;

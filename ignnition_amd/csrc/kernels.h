@@ -99,3 +99,17 @@ hipError_t launch_gather_rows(const float* src, int64_t ld, const int32_t* idx, 
 hipError_t launch_attn_softmax(const AttnArgs& a, hipStream_t st);
 // w12[0:F] = K1 . a[0:F], w12[F:2F] = K2 . a[F:2F]  (attention score vectors)
 hipError_t launch_attn_vectors(const float* K1, const float* K2, const float* a, int F, float* w12, hipStream_t st);
+
+// Message-network input (GM:446-462): out[e][col_q .. col_q + width_q) = part q of edge e, where a
+// part is a state row (rows[q][e]) or the edge's parameters (rows[q] == nullptr: row e).
+struct MsgGatherArgs {
+  float* out;
+  int64_t n;
+  int ld;
+  int nparts;
+  int col[4], width[4];
+  const float* base[4];
+  const int32_t* rows[4];
+};
+hipError_t launch_msg_gather(const MsgGatherArgs& a, hipStream_t st);
+hipError_t launch_pack_dense_pad(const float* W, float* Wp, int IN, int IN_pad, int OUT, hipStream_t st);

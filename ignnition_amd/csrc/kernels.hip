@@ -85,8 +85,9 @@ __global__ void pack_gru_kernel(const float* __restrict__ W, const float* __rest
 }
 
 // Dense kernel [IN][OUT] -> float4-grouped A fragments: ((u * (IN/16) + c) * 64 + lane) * 4 + q
-//   -> W[16c + 4*(lane>>4) + q][16u + (lane&15)]
-__global__ void pack_dense_kernel(const float* __restrict__ W, float* __restrict__ Wp, int IN, int OUT) {
+//   -> W[16c + 4*(lane>>4) + q][16u + (lane&15)]; rows k >= IN_real (input padding) are zero
+__global__ void pack_dense_kernel(const float* __restrict__ W, float* __restrict__ Wp, int IN, int OUT,
+                                  int IN_real) {
   int64_t total = (int64_t)IN * OUT;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -98,7 +99,7 @@ __global__ void pack_dense_kernel(const float* __restrict__ W, float* __restrict
     int u = (int)(f / C);
     int k = 16 * c + 4 * (lane >> 4) + q;
     int col = 16 * u + (lane & 15);
-    Wp[i] = W[(int64_t)k * OUT + col];
+    Wp[i] = k < IN_real ? W[(int64_t)k * OUT + col] : 0.f;
   }
 }
 
@@ -1274,7 +1275,13 @@ hipError_t launch_pack_gru(const float* W, const float* U, const float* bias, fl
 }
 
 hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStream_t st) {
-  hipLaunchKernelGGL(pack_dense_kernel, dim3(256), dim3(256), 0, st, W, Wp, IN, OUT);
+  return launch_pack_dense_pad(W, Wp, IN, IN, OUT, st);
+}
+
+hipError_t launch_pack_dense_pad(const float* W, float* Wp, int IN, int IN_pad, int OUT, hipStream_t st) {
+  const int64_t total = (int64_t)IN_pad * OUT;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
+  hipLaunchKernelGGL(pack_dense_kernel, dim3(blocks), dim3(256), 0, st, W, Wp, IN_pad, OUT, IN);
   return hipGetLastError();
 }
 
@@ -1452,5 +1459,28 @@ hipError_t launch_attn_softmax(const AttnArgs& a, hipStream_t st) {
 
 hipError_t launch_attn_vectors(const float* K1, const float* K2, const float* a, int F, float* w12, hipStream_t st) {
   hipLaunchKernelGGL(attn_vectors_kernel, dim3((2 * F + 63) / 64), dim3(64), 0, st, K1, K2, a, F, w12);
+  return hipGetLastError();
+}
+
+__global__ void msg_gather_kernel(MsgGatherArgs a) {
+  const int64_t total = a.n * a.ld;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i / a.ld;
+    const int c = (int)(i - e * a.ld);
+    float v = 0.f;
+    for (int q = 0; q < a.nparts; ++q)
+      if (c >= a.col[q] && c < a.col[q] + a.width[q]) {
+        const int64_t r = a.rows[q] ? a.rows[q][e] : e;
+        v = a.base[q][r * a.width[q] + (c - a.col[q])];
+      }
+    a.out[i] = v;
+  }
+}
+
+hipError_t launch_msg_gather(const MsgGatherArgs& a, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  const int64_t total = a.n * a.ld;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 65536));
+  hipLaunchKernelGGL(msg_gather_kernel, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }

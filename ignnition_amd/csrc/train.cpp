@@ -133,9 +133,12 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   const int E = (int)p->ents.size();
   for (int e = 0; e < E; ++e)
     if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
-  for (auto& mp : p->mps)
+  for (auto& mp : p->mps) {
     if (mp.aggr == IGN_AGGR_ATTENTION || mp.aggr == IGN_AGGR_CONVOLUTION || mp.feature_concat)
       return fail(IGN_ERR_UNSUPPORTED, "no backward for attention / convolution / axis-2 concat aggregations yet");
+    for (auto& nn : mp.nn)
+      if (!nn.layers.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for message networks yet");
+  }
   for (auto& cp : p->cells)
     if (cp.used && cp.pk_wt < 0)
       return fail(IGN_ERR_UNSUPPORTED, "no backward kernel for GRU shape (input %d, units %d)", cp.din, cp.H);

@@ -709,7 +709,8 @@ hipError_t launch_colsum_add(const float* B, int ldb, int64_t n_rows, int N, flo
 }
 
 bool dense_fwd_supported(int K, int M) {
-  return (K == 16 || K == 32 || K == 64 || K == 256) && M == 256;
+  return (K == 16 || K == 32 || K == 48 || K == 64 || K == 96 || K == 128 || K == 256) &&
+         (M == 16 || M == 32 || M == 64 || M == 128 || M == 256);
 }
 
 hipError_t launch_dense_fwd(const float* x, int64_t n, int K, int x_stride, const float* Wp, const float* W,
@@ -726,9 +727,40 @@ hipError_t launch_dense_fwd(const float* x, int64_t n, int K, int x_stride, cons
     hipLaunchKernelGGL((dense_fwd_kernel<KK, MM>), grid, dim3(256), 0, st, x, n, x_stride, Wp, bias, act, y);  \
     return hipGetLastError();                                                                                  \
   }
+  DF_CASE(16, 16)
+  DF_CASE(16, 32)
+  DF_CASE(16, 64)
+  DF_CASE(16, 128)
   DF_CASE(16, 256)
+  DF_CASE(32, 16)
+  DF_CASE(32, 32)
+  DF_CASE(32, 64)
+  DF_CASE(32, 128)
   DF_CASE(32, 256)
+  DF_CASE(48, 16)
+  DF_CASE(48, 32)
+  DF_CASE(48, 64)
+  DF_CASE(48, 128)
+  DF_CASE(48, 256)
+  DF_CASE(64, 16)
+  DF_CASE(64, 32)
+  DF_CASE(64, 64)
+  DF_CASE(64, 128)
   DF_CASE(64, 256)
+  DF_CASE(96, 16)
+  DF_CASE(96, 32)
+  DF_CASE(96, 64)
+  DF_CASE(96, 128)
+  DF_CASE(96, 256)
+  DF_CASE(128, 16)
+  DF_CASE(128, 32)
+  DF_CASE(128, 64)
+  DF_CASE(128, 128)
+  DF_CASE(128, 256)
+  DF_CASE(256, 16)
+  DF_CASE(256, 32)
+  DF_CASE(256, 64)
+  DF_CASE(256, 128)
   DF_CASE(256, 256)
 #undef DF_CASE
   return launch_dense_generic(x, n, K, x_stride, W, bias, M, act, y, st);

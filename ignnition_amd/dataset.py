@@ -104,7 +104,11 @@ def plan_keys(plan) -> list:
     for e, name in enumerate(plan.entities):
         keys.append("num_" + name)
         keys += [f for f, _ in plan.features[e]]
+    params = {src_adj for m in plan.mps for net, (_, a, _) in zip(m.get("nets", []), m["sources"])
+              if net and "edge_params" in net["inputs"] for src_adj in [plan.adj_slots[a].adj]}
     for slot in plan.adj_slots:
         keys += list(slot.keys)
+        if slot.adj in params:
+            keys.append("params_" + slot.adj)
     keys += list(plan.il_slots)
     return list(dict.fromkeys(keys))

@@ -55,6 +55,40 @@ class AdjSlot:
         return "src_" + self.adj, "dst_" + self.adj, "seq_" + self.src + "_" + self.dst
 
 
+def _message_net(s, dst, plan, eidx):
+    """The message-creation network of one MP source (GM:440-475), or None (direct_assignation).
+    The reference builds every network of a source under one name (its counter counts sources,
+    GM:251/281) and reads chained outputs under another (GM:458 vs 470), so exactly one network
+    per source reading hs_source / hs_dest / edge_params is what it can run."""
+    nets = [op for op in s.message_formation if op.type != "direct_assignation"]
+    if not nets:
+        return None
+    if len(nets) > 1:
+        raise UnsupportedModel("more than one message network per source (the reference cannot chain them, GM:458/470)")
+    op = nets[0]
+    inputs = list(getattr(op, "input", []))
+    for name in inputs:
+        if name not in _lib.MSG_INPUT:
+            raise UnsupportedModel("message input %r is not readable in the reference (GM:458/470)" % name)
+    layers = []
+    for l in op.model.layers:
+        if l.type != "Dense":
+            raise UnsupportedModel("message layer type %s is not lowered (Dense only)" % l.type)
+        prm = dict(l.parameters)
+        act = prm.get("activation", None)
+        if act not in _lib.ACT:
+            raise UnsupportedModel("activation %r not supported" % act)
+        known = {"units", "activation", "kernel_regularizer", "name", "use_bias"}
+        if set(prm) - known:
+            raise UnsupportedModel("Dense options %s are not lowered" % sorted(set(prm) - known))
+        layers.append((prm.get("name"), int(prm["units"]), _lib.ACT[act], int(bool(prm.get("use_bias", True))),
+                       float(prm.get("kernel_regularizer", 0.0) or 0.0)))
+    widths = {"hs_source": plan.hidden[eidx[s.name]], "hs_dest": plan.hidden[eidx[dst]],
+              "edge_params": int(s.extra_parameters)}
+    return {"prefix": "%s_to_%s_message_creation_0/" % (s.name, dst), "inputs": inputs,
+            "param_dim": int(s.extra_parameters), "din": sum(widths[i] for i in inputs), "layers": layers}
+
+
 @dataclass
 class MPPlan:
     """The lowered plan (entities, adjacency slots, MPs, cells, readout)."""
@@ -111,11 +145,11 @@ class MPPlan:
                     act = _lib.ACT[fn]
                 feature_concat = aggr == "concat" and mp.aggregation.concat_axis == 2
                 srcs = []
+                nets = []
                 din = None
                 for s in mp.source_entities:
-                    for op in s.message_formation:
-                        if op.type != "direct_assignation":
-                            raise UnsupportedModel("message-creation neural networks are not lowered yet")
+                    net = _message_net(s, dst, p, eidx)
+                    nets.append(net)
                     slot = AdjSlot(s.adj_vector, s.name, dst)
                     if slot not in p.adj_slots:
                         p.adj_slots.append(slot)
@@ -126,13 +160,15 @@ class MPPlan:
                             p.il_slots.append(key)
                         il = p.il_slots.index(key)
                     srcs.append((eidx[s.name], p.adj_slots.index(slot), il))
+                    msg_dim = net["layers"][-1][1] if net else p.hidden[eidx[s.name]]
                     # axis-2 concat feeds the GRU the sources' concatenated messages (AUX:443-456)
-                    din = (din or 0) + p.hidden[eidx[s.name]] if feature_concat else p.hidden[eidx[s.name]]
+                    din = (din or 0) + msg_dim if feature_concat else msg_dim
                 if dst not in cell_of:
                     cell_of[dst] = len(p.cells)
                     p.cells.append((dst, din, p.hidden[eidx[dst]]))
                 p.mps.append({"dst": eidx[dst], "aggr": aggr, "axis": getattr(mp.aggregation, "concat_axis", 0),
-                              "cell": cell_of[dst], "sources": srcs, "stage": stage_name, "act": act})
+                              "cell": cell_of[dst], "sources": srcs, "stage": stage_name, "act": act,
+                              "nets": nets})
                 if aggr in ("attention", "convolution"):
                     # one weight set per model: the reference overwrites self.kernel1 / conv_kernel per
                     # MP and every MP uses the last one (GM:288-300)
@@ -170,7 +206,17 @@ class MPPlan:
             *[_lib.EntityDesc(h, sum(s for _, s in f)) for h, f in zip(self.hidden, self.features)])
         mps = (_lib.MPDesc * len(self.mps))()
         for i, m in enumerate(self.mps):
-            srcs = (_lib.SourceDesc * len(m["sources"]))(*[_lib.SourceDesc(*s) for s in m["sources"]])
+            srcs = (_lib.SourceDesc * len(m["sources"]))()
+            for k, src in enumerate(m["sources"]):
+                net = m.get("nets", [None] * len(m["sources"]))[k]
+                if net:
+                    ins = (C.c_int32 * len(net["inputs"]))(*[_lib.MSG_INPUT[x] for x in net["inputs"]])
+                    lay = (_lib.DenseDesc * len(net["layers"]))(*[_lib.DenseDesc(u, a, b, l2)
+                                                                  for _, u, a, b, l2 in net["layers"]])
+                    keep += [ins, lay]
+                    srcs[k] = _lib.SourceDesc(*src, len(net["inputs"]), ins, net["param_dim"], len(net["layers"]), lay)
+                else:
+                    srcs[k] = _lib.SourceDesc(*src)
             keep.append(srcs)
             mps[i] = _lib.MPDesc(m["dst"], _lib.AGGR[m["aggr"]], int(m["axis"] or 0), m["cell"], len(m["sources"]),
                                  C.cast(srcs, C.POINTER(_lib.SourceDesc)), int(m.get("act", 0)))
@@ -190,6 +236,16 @@ class MPPlan:
         for dst, din, h in self.cells:
             specs += [(dst + "_update/kernel", (din, 3 * h)), (dst + "_update/recurrent_kernel", (h, 3 * h)),
                       (dst + "_update/bias", (2, 3 * h))]
+        for m in self.mps:
+            for net in m.get("nets", []):
+                if not net:
+                    continue
+                fan = net["din"]
+                for name, units, _, use_bias, _ in net["layers"]:
+                    specs.append((net["prefix"] + name + "/kernel", (fan, units)))
+                    if use_bias:
+                        specs.append((net["prefix"] + name + "/bias", (units,)))
+                    fan = units
         if self.convolution_dim:
             F = self.convolution_dim
             specs.append(("convolution/kernel", (F, F)))
@@ -411,13 +467,19 @@ class Batch:
         lp = C.POINTER(C.c_int64)
         feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
         mk = lambda arrs: (lp * max(len(arrs), 1))(*[a.ctypes.data_as(lp) for a in arrs])
+        prm_arrays = []
+        for slot in p.adj_slots:
+            key = "params_" + slot.adj
+            prm_arrays.append(np.ascontiguousarray(np.asarray(bg.get(key)[0], np.float32)) if key in bg else None)
         halo = None
         if halo_rows:
             halo = np.array([int(halo_rows.get(name, 0)) for name in p.entities], np.int64)
         self.halo = [0] * E if halo is None else [int(v) for v in halo]
         desc = _lib.BatchDesc(G, num.ctypes.data_as(lp), feat_ptrs, cnt.ctypes.data_as(lp), mk(srcs), mk(dsts),
                               mk(seqs), il_len.ctypes.data_as(lp), mk(ils),
-                              halo.ctypes.data_as(lp) if halo is not None else lp())
+                              halo.ctypes.data_as(lp) if halo is not None else lp(),
+                              (fp * max(A, 1))(*[a.ctypes.data_as(fp) if a is not None else fp() for a in prm_arrays]))
+        self._prm_arrays = prm_arrays
         h = C.c_void_p()
         check(lib.ign_batch_create(engine.handle, C.byref(desc), C.byref(h)))
         self.handle = h

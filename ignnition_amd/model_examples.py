@@ -52,6 +52,18 @@ def qsize_aggregation(aggregation: dict, iterations: int = 8) -> dict:
     return d
 
 
+def routenet_message_net(inputs=("hs_source", "hs_dest"), units=(32,), activation="relu", hidden: int = 32,
+                         iterations: int = 8) -> dict:
+    """RouteNet whose path -> link messages come from a message-creation network (GM:440-475)
+    on ``inputs`` (hs_source, hs_dest, edge_params) instead of direct assignation."""
+    d = routenet(hidden, iterations)
+    src = d["message_passing"]["stages"][1]["stage_mp"][0]["source_entities"][0]
+    src["message"] = [{"type": "neural_network", "nn_name": "message_nn", "input": list(inputs)}]
+    d["neural_networks"].append({"nn_name": "message_nn", "nn_type": "feed_forward", "nn_architecture": [
+        {"type_layer": "Dense", "units": u, "activation": activation} for u in units]})
+    return d
+
+
 def routenet(hidden: int = 32, iterations: int = 8) -> dict:
     """RNJ:1-165."""
     layer_names = ["1st_dense_layer", "2nd_dense_layer", "Output_layer"]

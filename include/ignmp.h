@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 4
+#define IGN_ABI_VERSION 5
 
 enum ign_status {
   IGN_OK = 0,
@@ -77,10 +77,26 @@ typedef struct {
   int32_t feature_total;           /* sum of feature sizes, features concatenated in listed order (AUX:140-153) */
 } ign_entity_desc;
 
+enum ign_message_input {        /* message-creation network inputs (GM:446-462) */
+  IGN_MSG_HS_SOURCE = 0,
+  IGN_MSG_HS_DEST = 1,
+  IGN_MSG_EDGE_PARAMS = 2
+};
+
+typedef struct ign_dense_desc_s ign_dense_desc;
+
 typedef struct {
   int32_t entity;                  /* source entity index */
   int32_t adjacency;               /* adjacency slot: index into ign_batch_desc.adj_* */
   int32_t interleave;              /* interleave slot (indices_<src>_to_<dst>) or -1 */
+  /* Message creation (GM:440-475): 0 layers = direct_assignation (message = source state);
+   * otherwise a Dense stack on the per-edge concatenation of msg_inputs (enum
+   * ign_message_input, in order).  edge_params has msg_param_dim floats per edge. */
+  int32_t msg_num_inputs;
+  const int32_t* msg_inputs;
+  int32_t msg_param_dim;
+  int32_t msg_num_layers;
+  const ign_dense_desc* msg_layers;
 } ign_source_desc;
 
 typedef struct {
@@ -98,12 +114,12 @@ typedef struct {
   int32_t units;                   /* = hidden_dim of the destination (AUX:747) */
 } ign_cell_desc;
 
-typedef struct {
+struct ign_dense_desc_s {
   int32_t units;
   int32_t activation;              /* enum ign_activation */
   int32_t use_bias;
   float l2;                        /* kernel_regularizer coefficient c: loss += c * sum(W^2) (AUX:833-834) */
-} ign_dense_desc;
+};
 
 typedef struct {
   int32_t num_iterations;          /* GM:406 */
@@ -137,7 +153,10 @@ typedef struct {
    * The caller fills them (ign_batch_bind_state + its own collective) before an MP reads them.
    * NULL = no halo. */
   const int64_t* halo_rows;        /* [num_entities] or NULL */
-} ign_batch_desc;
+  /* per adjacency: graph-concatenated params_<adj> [edges][param dim] (cast to float, GM:454-456),
+   * needed by message networks that read edge_params; NULL entries / NULL array when absent */
+  const float* const* adj_params;
+}  ign_batch_desc;
 
 typedef struct {
   int64_t num_graphs;
@@ -169,8 +188,10 @@ int  ign_plan_num_param_tensors(const ign_plan* plan, int32_t* n);
 /* tensor i: kind 0 gru kernel [in,3H], 1 gru recurrent_kernel [H,3H], 2 gru bias [2,3H],
  *           3 dense kernel [in,out], 4 dense bias [1,out]; owner = cell or dense index;
  *           5 convolution kernel [F,F], 6 attention kernel1 [F,F], 7 attention kernel2 [F,F],
- *           8 attention attn_kernel [2F,1] (one set per plan, GM:288-300; owner -1).
- * Order: cells, convolution, attention, Dense layers. */
+ *           8 attention attn_kernel [2F,1] (one set per plan, GM:288-300; owner -1);
+ *           9 message-network Dense kernel [in,out], 10 its bias [1,out] (owner = mp * 4 + source).
+ * Order: cells, message networks (MP order, source order, layer order), convolution, attention,
+ * readout Dense layers. */
 int  ign_plan_param_tensor(const ign_plan* plan, int32_t i, int32_t* kind, int32_t* owner,
                            int64_t* offset, int32_t* rows, int32_t* cols);
 int  ign_plan_set_params(ign_plan* plan, const float* params, int32_t on_device);

@@ -137,15 +137,36 @@ class DenseOracle:
         first = True
         src_input = final_len = indices = None
         for src in mp["source_entities"]:                                 # GM:423
-            for op in src["message"]:
-                if op["type"] != "direct_assignation":
-                    raise OracleError("message-creation networks are not restated")
             sname, adj = src["name"], src["adj_vector"]
             src_idx = np.asarray(x["src_" + adj], np.int64)
             dst_idx = np.asarray(x["dst_" + adj], np.int64)
             seq = np.asarray(x["seq_" + sname + "_" + dst], np.int64)
             msgs = _gather(state[sname], src_idx, "gather " + sname)      # GM:432
-            _gather(dst_states, dst_idx, "gather " + dst)                 # GM:433 (index check)
+            dst_msgs = _gather(dst_states, dst_idx, "gather " + dst)      # GM:433
+            src_messages = msgs
+            for k, op in enumerate(src["message"]):                        # GM:440-475
+                if op["type"] == "direct_assignation":
+                    continue
+                if op["type"] != "neural_network":
+                    raise OracleError("message operation %r not restated" % op["type"])
+                parts = []
+                for name in op["input"]:
+                    if name == "hs_source":
+                        parts.append(src_messages)
+                    elif name == "hs_dest":
+                        parts.append(dst_msgs)
+                    elif name == "edge_params":
+                        parts.append(np.asarray(x["params_" + adj], dt).reshape(len(src_idx), -1))
+                    else:   # other ops' outputs: stored as name+'var', read as name+'_var' (GM:458/470)
+                        raise OracleError("message input %r is not readable in the reference" % name)
+                h = np.concatenate(parts, axis=1)
+                pre = "%s_to_%s_message_creation_0/" % (sname, dst)   # the counter is per source (GM:251, 281)
+                for li, layer in enumerate(self.nn[op["nn_name"]]["nn_architecture"]):
+                    lname = layer.get("name", "layer_%d_%s_message_creation_%d" % (li, layer["type_layer"], k))
+                    b = self.p.get(pre + lname + "/bias")
+                    h = h @ self.p[pre + lname + "/kernel"] + (b if b is not None else 0)
+                    h = _act(h, layer.get("activation"))
+                msgs = h                                                  # the last operation's result
             lens = np.bincount(dst_idx, minlength=num_dst)[:num_dst].astype(np.int64)   # GM:481
             if seq.size == 0:
                 raise OracleError("empty adjacency: reduce_max of an empty seq")   # GM:484

@@ -284,3 +284,42 @@ def test_two_source_concat(axis):
     dims, graphs = _variant_inputs(desc, "qsize", 2)
     out, ref, _, _ = _run(desc, dims, graphs, seed=7, bias=0.1)
     _close(out, ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# message-creation networks (GM:440-475)
+def _with_edge_params(sample, rng):
+    s = copy.deepcopy(sample)
+    s["adj_paths_links"] = {l: [[p, [float(rng.uniform(0, 1)), float(rng.uniform(-1, 1))]] for p in ps]
+                            for l, ps in s["adj_paths_links"].items()}
+    return s
+
+
+@pytest.mark.parametrize("inputs,units", [(("hs_source", "hs_dest"), (48, 32)), (("hs_source",), (32,)),
+                                          (("hs_dest", "hs_source", "edge_params"), (32,))])
+def test_message_network_sum_mp(inputs, units):
+    from ignnition_amd.framework_operations import dimensions_of_sample
+    rng = np.random.default_rng(0)
+    desc = model_examples.routenet_message_net(inputs=inputs, units=units, activation="selu", iterations=3)
+    samples = [synthetic.routenet_sample("nsfnet", g) for g in range(2)]
+    if "edge_params" in inputs:
+        samples = [_with_edge_params(s, rng) for s in samples]
+    dims = dimensions_of_sample(samples[0])
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, samples)
+    out, ref, _, _ = _run(desc, dims, graphs, seed=8, bias=0.1)
+    _close(out, ref)
+
+
+def test_message_network_ordered_mp():
+    """A network on the link -> path (ordered) messages: the projected table is per edge."""
+    desc = model_examples.routenet(iterations=3)
+    src = desc["message_passing"]["stages"][0]["stage_mp"][0]["source_entities"][0]
+    src["message"] = [{"type": "neural_network", "nn_name": "message_nn", "input": ["hs_source", "hs_dest"]}]
+    desc["neural_networks"].append({"nn_name": "message_nn", "nn_type": "feed_forward", "nn_architecture": [
+        {"type_layer": "Dense", "units": 32, "activation": "tanh"}]})
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
+    out, ref, _, _ = _run(desc, dims, graphs, seed=9, bias=0.1)
+    _close(out, ref)
