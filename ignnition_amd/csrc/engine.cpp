@@ -1046,12 +1046,13 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   const int dst = mp.dst;
   const float* hin = b->d_state[b->cur[dst]][dst];
   float* hout = b->d_state[1 - b->cur[dst]][dst];
-  if (part != IGN_PART_BOUNDARY)
-    for (size_t s = 0; s < mp.src.size(); ++s) {   // message-creation networks (GM:440-475)
-      const MsgNN& nn = mp.nn[s];
-      if (nn.layers.empty()) continue;
-      if ((rc = run_message_net(p, nn, mb, (int)s, sbases.base[s], hin, st))) return rc;
-    }
+  for (size_t s = 0; s < mp.src.size(); ++s) {   // message-creation networks (GM:440-475)
+    const MsgNN& nn = mp.nn[s];
+    if (nn.layers.empty()) continue;
+    // the per-edge network reads halo rows: it must run after the exchange, not beside it
+    if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split with a message network");
+    if ((rc = run_message_net(p, nn, mb, (int)s, sbases.base[s], hin, st))) return rc;
+  }
   for (size_t s = 0; s < mp.src.size(); ++s)
     if (!mp.nn[s].layers.empty()) sbases.base[s] = mb.d_msg_layer[s].back();
   if (mp.sorted) {
@@ -1086,6 +1087,8 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     const int64_t count = part == IGN_PART_INTERIOR ? mb.n_interior
                         : part == IGN_PART_BOUNDARY ? mb.n_dst - mb.n_interior : mb.n_dst;
     if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343: scores, then the axis-0 softmax weights
+      // a softmax group spans interior and boundary destinations: no split
+      if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split with attention");
       const float* w12 = p->d_packed + p->pk_w12;
       tm.begin(K_OTHER, 0, 0);
       for (size_t s = 0; s < mp.src.size(); ++s) {
