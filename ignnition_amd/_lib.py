@@ -40,12 +40,18 @@ class CellDesc(C.Structure):
     _fields_ = [("input_dim", i32), ("units", i32)]
 
 
+class ReadoutOpDesc(C.Structure):
+    _fields_ = [("type", i32), ("num_inputs", i32), ("inputs", C.POINTER(i32)), ("mode", i32),
+                ("adjacency", i32), ("num_dense", i32), ("dense", C.POINTER(DenseDesc))]
+
+
 class PlanDesc(C.Structure):
     _fields_ = [("num_iterations", i32), ("num_entities", i32), ("entities", C.POINTER(EntityDesc)),
                 ("num_adjacencies", i32), ("num_interleave", i32), ("num_mps", i32),
                 ("mps", C.POINTER(MPDesc)), ("num_cells", i32), ("cells", C.POINTER(CellDesc)),
                 ("num_readout_inputs", i32), ("readout_inputs", C.POINTER(i32)),
-                ("num_dense", i32), ("dense", C.POINTER(DenseDesc))]
+                ("num_dense", i32), ("dense", C.POINTER(DenseDesc)),
+                ("num_readout_ops", i32), ("readout_ops", C.POINTER(ReadoutOpDesc))]
 
 
 class BatchDesc(C.Structure):
@@ -78,6 +84,9 @@ KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "project", "other
 
 MSG_INPUT = {"hs_source": 0, "hs_dest": 1, "edge_params": 2}
 AGGR = {"sum": 0, "ordered": 1, "interleave": 2, "concat": 3, "attention": 4, "convolution": 5}
+READOUT_OP = {"neural_network": 0, "pooling": 1, "product": 2, "extend_adjacencies": 3}
+POOLING = {"sum": 0, "mean": 1, "max": 2}
+PRODUCT = {"element_wise": 0, "dot_product": 1}
 ACT = {None: 0, "None": 0, "linear": 0, "relu": 1, "selu": 2, "sigmoid": 3, "tanh": 4}
 
 # every symbol declared in include/ignmp.h
@@ -91,7 +100,7 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get"]
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 

@@ -9,7 +9,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libignmp.so")
-SOURCES = ["engine.cpp", "train.cpp", "dataset.cpp", "kernels.hip", "train_kernels.hip"]
+SOURCES = ["engine.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "kernels.hip", "train_kernels.hip",
+           "readout_kernels.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
          "-Wno-unused-value"]
 

@@ -143,7 +143,7 @@ int ign::repack(ign_plan* p) {
     if (dp.pk_w >= 0) HIP_TRY(launch_pack_dense(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in, dp.out, p->stream));
   for (auto& dp : p->dense)
     if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
-  return IGN_OK;
+  return readout_repack(p);
 }
 
 // =============================================================================================
@@ -309,32 +309,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.used = true;
     p->mps.push_back(mp);
   }
-  // readout
-  p->ro_in.assign(d->readout_inputs, d->readout_inputs + d->num_readout_inputs);
-  if (p->ro_in.empty()) return fail(IGN_ERR_INVALID, "readout has no input");
-  int width = 0;
-  for (int e : p->ro_in) {
-    if (e < 0 || e >= d->num_entities) return fail(IGN_ERR_INVALID, "readout input entity %d", e);
-    width += p->ents[e].hidden_dim;
-  }
-  p->ro_width = width;
-  int in = width;
-  for (int l = 0; l < d->num_dense; ++l) {
-    DenseP dp;
-    dp.in = in;
-    dp.out = d->dense[l].units;
-    dp.act = d->dense[l].activation;
-    dp.use_bias = d->dense[l].use_bias;
-    dp.l2 = d->dense[l].l2;
-    if (dp.out <= 0) return fail(IGN_ERR_INVALID, "dense layer %d: units must be > 0", l);
-    if (!act_ok(dp.act)) return fail(IGN_ERR_UNSUPPORTED, "dense layer %d: activation %d", l, dp.act);
-    p->dense.push_back(dp);
-    in = dp.out;
-  }
-  if (p->dense.empty()) return fail(IGN_ERR_INVALID, "readout has no Dense layer");
-  p->fused_readout = p->dense.size() == 3 &&
-                     readout3_supported(width, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act) &&
-                     p->dense[2].out == 1 && p->dense[0].use_bias && p->dense[1].use_bias;
+  // readout program and predict (GM:605-629)
+  if (int rc = readout_plan(p.get(), d)) return rc;
 
   // parameter layout (256-B aligned tensors)
   auto align = [](int64_t x) { return (x + 63) & ~int64_t(63); };
@@ -363,6 +339,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     p->off_k2 = off; p->tensors.push_back({7, -1, off, F, F}); off = align(off + (int64_t)F * F);
     p->off_att = off; p->tensors.push_back({8, -1, off, 2 * F, 1}); off = align(off + 2LL * F);
   }
+  off = readout_layout(p.get(), off);
   for (size_t l = 0; l < p->dense.size(); ++l) {
     DenseP& dp = p->dense[l];
     dp.off_w = off; p->tensors.push_back({3, (int)l, off, dp.in, dp.out}); off = align(off + (int64_t)dp.in * dp.out);
@@ -409,6 +386,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
       }
   if (p->conv_F) { p->pk_conv = pk; pk = align(pk + (int64_t)p->conv_F * p->conv_F); }
   if (p->attn_F) { p->pk_w12 = pk; pk = align(pk + 2LL * p->attn_F); }
+  pk = readout_packed(p.get(), pk);
   p->n_packed = pk;
 
   // Device resources are allocated on first use (ensure_device), so plan validation and the
@@ -889,9 +867,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   }
 
   // readout buffers
-  const int64_t P = b->rows[p->ro_in[0]];
-  for (int e : p->ro_in)
-    if (b->rows[e] != P) return fail(IGN_ERR_INVALID, "readout inputs have different row counts (concat axis 1)");
+  if ((rc = readout_batch(p, b.get(), d))) return rc;
+  const int64_t P = space_rows(p, b.get(), p->ro_t[p->ro_in[0]]);
   b->n_pred = P;
   b->out_units = p->dense.back().out;
   if (p->ro_in.size() > 1 && (rc = dev_alloc(b.get(), &b->d_ro_in, P * p->ro_width))) return rc;
@@ -1146,13 +1123,20 @@ int readout(ign_plan* p, ign_batch* b) {
   Timer tm{p};
   // readout (GM:611-629)
   const int64_t P = b->n_pred;
-  const float* x = b->d_state[b->cur[p->ro_in[0]]][p->ro_in[0]];
+  if (!p->ro_ops.empty()) {
+    tm.begin(K_OTHER, 0, 0);
+    int rc = readout_ops_run(p, b, st);
+    tm.end();
+    if (rc) return rc;
+  }
+  const float* x = readout_tensor(p, b, p->ro_in[0]);
   int xs = p->ro_width;
   if (p->ro_in.size() > 1) {
     int col = 0;
-    for (int e : p->ro_in) {
-      HIP_TRY(launch_concat_cols(b->d_ro_in, P, p->ro_width, col, b->d_state[b->cur[e]][e], p->ents[e].hidden_dim, st));
-      col += p->ents[e].hidden_dim;
+    for (int id : p->ro_in) {
+      const int w = p->ro_t[id].width;
+      HIP_TRY(launch_concat_cols(b->d_ro_in, P, p->ro_width, col, readout_tensor(p, b, id), w, st));
+      col += w;
     }
     x = b->d_ro_in;
   }

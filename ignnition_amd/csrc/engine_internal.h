@@ -110,6 +110,33 @@ struct MPB {
   std::vector<uint32_t> h_step_code, h_msg_src, h_multi_rows;
 };
 
+// readout program (GM:611-655): tensors on row spaces, operations before predict
+enum { RS_ENTITY = 0, RS_GRAPH = 1, RS_ADJ = 2 };
+struct RoTensor {
+  int space = RS_ENTITY, sid = 0;   // sid: entity or adjacency slot
+  int width = 0;
+  bool same_space(const RoTensor& o) const { return space == o.space && (space == RS_GRAPH || sid == o.sid); }
+};
+struct RoOp {
+  int type = 0, mode = 0, adj = -1;
+  std::vector<int> in;            // tensor ids
+  std::vector<DenseP> layers;     // IGN_RO_NEURAL_NETWORK
+  int in_width = 0;               // neural_network: concatenated input width
+  int out = -1;                   // first output tensor id
+};
+struct RoBatchOp {
+  float* out[2] = {nullptr, nullptr};
+  float* cat = nullptr;           // neural_network: concatenated input
+  std::vector<float*> tmp;        // neural_network: hidden layer outputs
+  int32_t* idx[2] = {nullptr, nullptr};   // extend: global source / destination rows per edge
+  // pooling: chunks of <= POOL_CHUNK rows, per-graph chunk ranges, partial results
+  int64_t n_chunks = 0;
+  int64_t* d_chunk = nullptr;     // [n_chunks][2] global row ranges
+  int32_t* d_chunk_ptr = nullptr; // [G + 1]
+  int64_t* d_count = nullptr;     // [G] rows per graph
+  float* d_partial = nullptr;     // [n_chunks][F]
+  int64_t* d_seg = nullptr;       // product: [G + 1] row offsets of the output space
+};
 
 }  // namespace ign
 
@@ -125,8 +152,11 @@ struct ign_plan {
   int n_adj = 0, n_il = 0;
   std::vector<MPP> mps;
   std::vector<CellP> cells;
-  std::vector<int> ro_in;
+  std::vector<int> ro_in;         // predict inputs: readout tensor ids
   std::vector<DenseP> dense;
+  std::vector<RoTensor> ro_t;     // readout tensors: entity states, then the op outputs
+  std::vector<RoOp> ro_ops;
+  std::vector<int> adj_src_ent, adj_dst_ent;   // per adjacency slot (from the MPs that read it)
   // one convolution / attention weight set per plan (GM:288-300: the last MP's weights serve all)
   int conv_F = 0, attn_F = 0;
   int64_t off_conv = -1, off_k1 = -1, off_k2 = -1, off_att = -1;
@@ -174,6 +204,10 @@ struct ign_batch {
   std::vector<MPB> mp;
   float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
   std::vector<float*> d_ro_tmp;                 // generic readout intermediates
+  std::vector<RoBatchOp> ro;                    // readout ops
+  std::vector<float*> ro_buf;                   // per readout tensor: op output buffer (null for states)
+  std::vector<int64_t> adj_rows;                // per adjacency: edges in the batch
+  std::vector<std::vector<int64_t>> adj_off;    // [adjacency][graph + 1] edge offsets
   float* d_pred = nullptr;
   int64_t n_pred = 0, out_units = 1;
   int64_t edges_per_forward = 0, gru_steps = 0;
@@ -191,6 +225,15 @@ int set_device(int dev);
 int ensure_device(ign_plan* p);
 int dev_alloc(ign_batch* b, float** out, int64_t n);
 int repack(ign_plan* p);                      // fragments from d_params (set_params, optimizer)
+// readout.cpp: the readout program (operations before predict, GM:611-655)
+int readout_plan(ign_plan* p, const ign_plan_desc* d);          // parse + row spaces + widths
+int64_t readout_layout(ign_plan* p, int64_t off);              // raw parameter tensors (kinds 11/12)
+int64_t readout_packed(ign_plan* p, int64_t pk);               // packed Dense fragments
+int readout_repack(ign_plan* p);
+int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d);
+int readout_ops_run(ign_plan* p, ign_batch* b, hipStream_t st);
+const float* readout_tensor(const ign_plan* p, const ign_batch* b, int id);
+int64_t space_rows(const ign_plan* p, const ign_batch* b, const RoTensor& t);
 template <typename T>
 int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
   size_t n = std::max<size_t>(host.size(), 1);

@@ -133,6 +133,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   const int E = (int)p->ents.size();
   for (int e = 0; e < E; ++e)
     if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
+  if (!p->ro_ops.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for readout operations before predict yet");
   for (auto& mp : p->mps) {
     if (mp.aggr == IGN_AGGR_ATTENTION || mp.aggr == IGN_AGGR_CONVOLUTION || mp.feature_concat)
       return fail(IGN_ERR_UNSUPPORTED, "no backward for attention / convolution / axis-2 concat aggregations yet");

@@ -100,7 +100,11 @@ class MPPlan:
     il_slots: list = field(default_factory=list)       # indices_<src>_to_<dst> keys
     mps: list = field(default_factory=list)            # dicts
     cells: list = field(default_factory=list)          # [(dst_name, din, H)]
-    readout_inputs: list = field(default_factory=list)
+    readout_inputs: list = field(default_factory=list)  # predict inputs: readout tensor ids
+    readout_ops: list = field(default_factory=list)     # operations before predict (dicts)
+    ro_widths: list = field(default_factory=list)       # readout tensor widths (entity states first)
+    ro_spaces: list = field(default_factory=list)       # row space per tensor: ("entity", e) / ("graph",) / ("adj", slot)
+    predict_counter: int = 0                           # readout_model_<index of predict in the readout list>
     dense: list = field(default_factory=list)          # [(name, units, act, use_bias, l2)]
     iterations: int = 0
     readout_label: str = ""
@@ -173,21 +177,15 @@ class MPPlan:
                     # one weight set per model: the reference overwrites self.kernel1 / conv_kernel per
                     # MP and every MP uses the last one (GM:288-300)
                     setattr(p, aggr + "_dim", p.hidden[eidx[dst]])
-        preds = [op for op in mi.get_readout_operations() if op.type == "predict"]
-        others = [op for op in mi.get_readout_operations() if op.type != "predict"]
-        if others:
-            raise UnsupportedModel("readout operations %s are not lowered yet" % [o.type for o in others])
-        if len(preds) != 1:
-            raise UnsupportedModel("exactly one predict operation is required")
-        op = preds[0]
-        p.readout_label = op.label
-        for name in op.input:
-            if name not in eidx:
-                raise UnsupportedModel("readout input %r is not an entity state" % name)
-            p.readout_inputs.append(eidx[name])
-        for l in op.architecture.layers:
+        p._lower_readout(mi)
+        return p
+
+    @staticmethod
+    def _dense_layers(arch, what):
+        out = []
+        for l in arch.layers:
             if l.type != "Dense":
-                raise UnsupportedModel("readout layer type %s is not lowered (Dense only)" % l.type)
+                raise UnsupportedModel("%s layer type %s is not lowered (Dense only)" % (what, l.type))
             prm = dict(l.parameters)
             act = prm.get("activation", None)
             if act not in _lib.ACT:
@@ -195,9 +193,75 @@ class MPPlan:
             known = {"units", "activation", "kernel_regularizer", "name", "use_bias"}
             if set(prm) - known:
                 raise UnsupportedModel("Dense options %s are not lowered" % sorted(set(prm) - known))
-            p.dense.append((prm.get("name"), int(prm["units"]), _lib.ACT[act], int(bool(prm.get("use_bias", True))),
-                            float(prm.get("kernel_regularizer", 0.0) or 0.0)))
-        return p
+            out.append((prm.get("name"), int(prm["units"]), _lib.ACT[act], int(bool(prm.get("use_bias", True))),
+                        float(prm.get("kernel_regularizer", 0.0) or 0.0)))
+        return out
+
+    def _lower_readout(self, mi):
+        """The readout list (GM:605-655) up to the first predict, which returns (GM:629); names
+        resolve like get_global_var_or_input (GM:660-675): entity states, then op outputs, later
+        outputs shadowing earlier names."""
+        names = {n: i for i, n in enumerate(self.entities)}
+        self.ro_widths = list(self.hidden)
+        self.ro_spaces = [("entity", i) for i in range(len(self.entities))]
+
+        def resolve(name):
+            if name not in names:
+                raise UnsupportedModel("readout input %r is not an entity state or a readout output (raw input "
+                                       "features are not lowered as readout inputs)" % name)
+            return names[name]
+
+        def add(name, width, space):
+            names[name] = len(self.ro_widths)
+            self.ro_widths.append(width)
+            self.ro_spaces.append(space)
+
+        pred = None
+        for counter, op in enumerate(mi.get_readout_operations()):
+            if op.type == "predict":
+                pred = (counter, op)
+                break
+            ids = [resolve(n) for n in op.input]
+            first = self.ro_spaces[ids[0]]
+            d = {"type": op.type, "inputs": ids, "mode": 0, "adj": -1, "layers": [], "counter": counter}
+            if op.type == "neural_network":
+                d["layers"] = self._dense_layers(op.architecture, "readout")
+                d["in_width"] = sum(self.ro_widths[i] for i in ids)
+                add(op.output_name, d["layers"][-1][1], first)
+            elif op.type == "pooling":
+                if op.type_pooling not in _lib.POOLING:
+                    raise UnsupportedModel("pooling type %r is not lowered" % op.type_pooling)
+                d["mode"] = _lib.POOLING[op.type_pooling]
+                add(op.output_name, self.ro_widths[ids[0]], ("graph",))
+            elif op.type == "product":
+                if op.type_product != "element_wise":
+                    raise UnsupportedModel("product %r is not lowered: tf.tensordot(axes=0) is a rank-4 outer product "
+                                           "that the reference records as width 1 (GM:374-375)" % op.type_product)
+                if len(ids) < 2:
+                    raise UnsupportedModel("product needs two inputs")
+                space = first if first != ("graph",) else self.ro_spaces[ids[1]]
+                add(op.output_name, self.ro_widths[ids[0]], space)
+            elif op.type == "extend_adjacencies":
+                slots = [k for k, sl in enumerate(self.adj_slots) if sl.adj == op.adj_list]
+                if not slots:
+                    raise UnsupportedModel("extend_adjacencies: adjacency %r is not read by any message passing "
+                                           "(the reference's input has no src_/dst_ for it)" % op.adj_list)
+                d["adj"] = slots[0]
+                add(op.output_name[0], self.ro_widths[ids[0]], ("adj", slots[0]))
+                add(op.output_name[1], self.ro_widths[ids[1]], ("adj", slots[0]))
+            else:
+                raise UnsupportedModel("readout operation %r is not lowered" % op.type)
+            self.readout_ops.append(d)
+        if pred is None:
+            raise UnsupportedModel("the readout has no predict operation")
+        self.predict_counter, op = pred
+        self.readout_label = op.label
+        self.readout_inputs = [resolve(n) for n in op.input]
+        self.dense = self._dense_layers(op.architecture, "readout")
+
+    @property
+    def predict_space(self):
+        return self.ro_spaces[self.readout_inputs[0]]
 
     # ------------------------------------------------------------------ C structures
     def to_desc(self):
@@ -223,10 +287,18 @@ class MPPlan:
         cells = (_lib.CellDesc * len(self.cells))(*[_lib.CellDesc(din, h) for _, din, h in self.cells])
         ro = (C.c_int32 * len(self.readout_inputs))(*self.readout_inputs)
         dense = (_lib.DenseDesc * len(self.dense))(*[_lib.DenseDesc(u, a, b, l2) for _, u, a, b, l2 in self.dense])
-        keep += [ents, mps, cells, ro, dense]
+        rops = (_lib.ReadoutOpDesc * max(1, len(self.readout_ops)))()
+        for k, op in enumerate(self.readout_ops):
+            ins = (C.c_int32 * len(op["inputs"]))(*op["inputs"])
+            lay = (_lib.DenseDesc * max(1, len(op["layers"])))(*[_lib.DenseDesc(u, a, b, l2)
+                                                                 for _, u, a, b, l2 in op["layers"]])
+            keep += [ins, lay]
+            rops[k] = _lib.ReadoutOpDesc(_lib.READOUT_OP[op["type"]], len(op["inputs"]), ins, op["mode"], op["adj"],
+                                         len(op["layers"]), lay)
+        keep += [ents, mps, cells, ro, dense, rops]
         d = _lib.PlanDesc(self.iterations, len(self.entities), ents, len(self.adj_slots), len(self.il_slots),
                           len(self.mps), mps, len(self.cells), cells, len(self.readout_inputs), ro,
-                          len(self.dense), dense)
+                          len(self.dense), dense, len(self.readout_ops), rops)
         return d, keep
 
     # ------------------------------------------------------------------ parameters
@@ -252,12 +324,18 @@ class MPPlan:
         if self.attention_dim:
             F = self.attention_dim
             specs += [("attention/kernel1", (F, F)), ("attention/kernel2", (F, F)), ("attention/attn_kernel", (2 * F, 1))]
-        width = sum(self.hidden[e] for e in self.readout_inputs)
-        fan_in = width
+        for op in self.readout_ops:
+            fan_in = op.get("in_width", 0)
+            for li, (name, units, _, use_bias, _) in enumerate(op["layers"]):
+                pre = "readout_model_%d/%s" % (op["counter"], name or ("layer_%d" % li))
+                specs.append((pre + "/kernel", (fan_in, units)))
+                if use_bias:
+                    specs.append((pre + "/bias", (units,)))
+                fan_in = units
+        fan_in = sum(self.ro_widths[i] for i in self.readout_inputs)
         for li, (name, units, _, use_bias, _) in enumerate(self.dense):
-            lname = name or ("layer_%d" % li)
-            specs += [("readout_model_0/" + lname + "/kernel", (fan_in, units)),
-                      ("readout_model_0/" + lname + "/bias", (units,))]
+            pre = "readout_model_%d/%s" % (self.predict_counter, name or ("layer_%d" % li))
+            specs += [(pre + "/kernel", (fan_in, units)), (pre + "/bias", (units,))]
             fan_in = units
         return specs
 
@@ -493,6 +571,13 @@ class Batch:
         self.gru_steps_per_forward = info.gru_steps_per_forward
         self.rows = list(info.rows)[:E]
         self.graph_rows = num
+        space = p.predict_space     # rows of the predict input space per graph (GM:716-724 splits)
+        if space[0] == "entity":
+            self.graph_predictions = num[:, space[1]].copy()
+        elif space[0] == "graph":
+            self.graph_predictions = np.ones(G, np.int64)
+        else:
+            self.graph_predictions = cnt[:, space[1]].copy()
         self._arrays = None  # the engine copied what it needs
         self._bound = {}
 

@@ -101,7 +101,7 @@ def predict(model_info, params=None, batch_size: int = 1):
         start = 0
         flat = pred.reshape(-1)
         units = out.output_units
-        for n in out.graph_rows[:, model.plan.readout_inputs[0]]:
+        for n in out.graph_predictions:
             p = flat[start:start + n * units]
             start += n * units
             if output_denorm is not None:
@@ -131,6 +131,7 @@ def debug(model_description, out_dir: str = "../debug_model/"):
         "interleave_slots": plan.il_slots,
         "message_passings": plan.mps,
         "cells": plan.cells,
+        "readout_ops": plan.readout_ops,
         "readout_inputs": plan.readout_inputs,
         "dense": plan.dense,
         "parameters": [[n, list(s)] for n, s in plan.param_specs()],

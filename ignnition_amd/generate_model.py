@@ -186,7 +186,7 @@ class ComnetModel:
         """Keras ``model.losses``: l2 terms of the readout kernel_regularizers (AUX:833-834)."""
         out = []
         for (name, _, _, _, l2), (pname, _) in zip(self.plan.dense, [s for s in self.plan.param_specs()
-                                                                      if s[0].startswith("readout_model_0/")
+                                                                      if s[0].startswith("readout_model_%d/" % self.plan.predict_counter)
                                                                       and s[0].endswith("/kernel")]):
             if l2:
                 w = np.asarray(self.params[pname], np.float64)

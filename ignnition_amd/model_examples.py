@@ -64,6 +64,21 @@ def routenet_message_net(inputs=("hs_source", "hs_dest"), units=(32,), activatio
     return d
 
 
+def routenet_readout(ops: list, predict_input: list, nets: dict = None, hidden: int = 32,
+                     iterations: int = 8) -> dict:
+    """RouteNet with readout operations before predict (GM:605-655, AUX:1033-1265): ``ops`` is
+    the readout list without the predict, ``predict_input`` the predict op's inputs, ``nets``
+    extra neural networks {nn_name: [(units, activation), ...]} used by neural_network ops."""
+    d = routenet(hidden, iterations)
+    pred = d["readout"][0]
+    pred["input"] = list(predict_input)
+    d["readout"] = [copy.deepcopy(o) for o in ops] + [pred]
+    for name, layers in (nets or {}).items():
+        d["neural_networks"].append({"nn_name": name, "nn_type": "feed_forward", "nn_architecture": [
+            {"type_layer": "Dense", "units": u, "activation": a} for u, a in layers]})
+    return d
+
+
 def routenet(hidden: int = 32, iterations: int = 8) -> dict:
     """RNJ:1-165."""
     layer_names = ["1st_dense_layer", "2nd_dense_layer", "Output_layer"]

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 5
+#define IGN_ABI_VERSION 6
 
 enum ign_status {
   IGN_OK = 0,
@@ -121,6 +121,30 @@ struct ign_dense_desc_s {
   float l2;                        /* kernel_regularizer coefficient c: loss += c * sum(W^2) (AUX:833-834) */
 };
 
+enum ign_readout_op_type {     /* readout operations before predict (GM:611-655, AUX:1033-1234) */
+  IGN_RO_NEURAL_NETWORK = 0,     /* Readout_nn: Dense stack on the axis-1 concat of its inputs (GM:612-628) */
+  IGN_RO_POOLING = 1,            /* Pooling_operation: reduce over the graph's rows -> [1, F] (AUX:1163-1185) */
+  IGN_RO_PRODUCT = 2,            /* Product_operation element_wise: tf.multiply with broadcasting (AUX:1081-1088) */
+  IGN_RO_EXTEND = 3              /* Extend_adjacencies: gather both ends of an adjacency (AUX:1236-1265) */
+};
+
+enum ign_pooling { IGN_POOL_SUM = 0, IGN_POOL_MEAN = 1, IGN_POOL_MAX = 2 };
+
+/* Readout tensors are numbered: [0, num_entities) the entity hidden states, then the outputs
+ * of the readout ops in order (one each; extend_adjacencies has two: src then dst).  Every
+ * tensor lives on one row space: an entity's rows, one row per graph (pooling), or an
+ * adjacency's edges (extend_adjacencies); the predict op's inputs share one space, whose
+ * rows are the predictions. */
+typedef struct {
+  int32_t type;                    /* enum ign_readout_op_type */
+  int32_t num_inputs;
+  const int32_t* inputs;           /* readout tensor ids (GM:660-675 resolves names to states) */
+  int32_t mode;                    /* IGN_RO_POOLING: enum ign_pooling; IGN_RO_PRODUCT: 0 = element_wise */
+  int32_t adjacency;               /* IGN_RO_EXTEND: adjacency slot (one that some MP reads) */
+  int32_t num_dense;               /* IGN_RO_NEURAL_NETWORK: its Dense stack */
+  const ign_dense_desc* dense;
+} ign_readout_op_desc;
+
 typedef struct {
   int32_t num_iterations;          /* GM:406 */
   int32_t num_entities;
@@ -132,9 +156,11 @@ typedef struct {
   int32_t num_cells;
   const ign_cell_desc* cells;
   int32_t num_readout_inputs;      /* predict op inputs, concatenated on axis 1 (GM:615-621) */
-  const int32_t* readout_inputs;   /* entity indices */
+  const int32_t* readout_inputs;   /* readout tensor ids (entity indices when there are no readout ops) */
   int32_t num_dense;
   const ign_dense_desc* dense;     /* readout Dense stack (RNJ:113-142) */
+  int32_t num_readout_ops;         /* operations run before predict, in model_description order */
+  const ign_readout_op_desc* readout_ops;
 } ign_plan_desc;
 
 typedef struct {
@@ -160,7 +186,7 @@ typedef struct {
 
 typedef struct {
   int64_t num_graphs;
-  int64_t predictions;             /* rows of the predict entity (outputs = predictions * last units) */
+  int64_t predictions;             /* rows of the predict input space (outputs = predictions * last units) */
   int64_t output_units;
   int64_t edges_per_forward;       /* T * sum over MPs and sources of |adj| */
   int64_t gru_steps_per_forward;   /* GRU cell applications (per destination row / sequence step) */
@@ -189,9 +215,10 @@ int  ign_plan_num_param_tensors(const ign_plan* plan, int32_t* n);
  *           3 dense kernel [in,out], 4 dense bias [1,out]; owner = cell or dense index;
  *           5 convolution kernel [F,F], 6 attention kernel1 [F,F], 7 attention kernel2 [F,F],
  *           8 attention attn_kernel [2F,1] (one set per plan, GM:288-300; owner -1);
- *           9 message-network Dense kernel [in,out], 10 its bias [1,out] (owner = mp * 4 + source).
+ *           9 message-network Dense kernel [in,out], 10 its bias [1,out] (owner = mp * 4 + source);
+ *           11 readout neural_network op Dense kernel [in,out], 12 its bias [1,out] (owner = op * 64 + layer).
  * Order: cells, message networks (MP order, source order, layer order), convolution, attention,
- * readout Dense layers. */
+ * readout neural_network ops (op order, layer order), predict Dense layers. */
 int  ign_plan_param_tensor(const ign_plan* plan, int32_t i, int32_t* kind, int32_t* owner,
                            int64_t* offset, int32_t* rows, int32_t* cols);
 int  ign_plan_set_params(ign_plan* plan, const float* params, int32_t on_device);

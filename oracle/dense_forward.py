@@ -19,7 +19,9 @@ It follows the reference's TensorFlow op sequence literally, one graph at a time
     update               AUX:752-765 GRUCell on every destination (sum);
                          AUX:767-796 RNN(GRUCell) with sequence_mask(final_len), then
                                      gather_nd(outputs, [d, final_len-1])
-  readout              GM:611-629   concat inputs on axis 1, Dense stack (AUX:833-837)
+  readout              GM:605-655   neural_network / pooling / element-wise product /
+                                     extend_adjacencies, then predict: concat inputs on axis 1,
+                                     Dense stack (AUX:833-837)
 
 TF / Keras math (not in the reference repo, restated from their published definitions):
 GRUCell v2 defaults (tanh / sigmoid, reset_after=True, gate order z, r, h); Dense
@@ -263,19 +265,56 @@ class DenseOracle:
         pre = dst + "_update/"
         return self.p[pre + "kernel"], self.p[pre + "recurrent_kernel"], self.p[pre + "bias"]
 
+    def _dense_stack(self, h, op, counter):
+        """readout_model_<counter> (GM:352-358): Dense layers as named by Feed_forward_model."""
+        for li, layer in enumerate(self.nn[op["nn_name"]]["nn_architecture"]):
+            name = layer.get("name", "layer_%d_%s_readout" % (li, layer["type_layer"]))  # AUX:909-910
+            pre = "readout_model_%d/%s/" % (counter, name)
+            h = h @ self.p[pre + "kernel"]
+            if pre + "bias" in self.p:
+                h = h + self.p[pre + "bias"]
+            h = _act(h, layer.get("activation"))
+        return h
+
     def _readout(self, state, x):
-        for op in self.d["readout"]:
-            if op["type"] != "predict":
-                raise OracleError("readout op %s not restated" % op["type"])
-            parts = [state[i] if i in state else np.asarray(x[i], self.dtype) for i in op["input"]]
-            h = np.concatenate(parts, axis=1)
-            layers = self.nn[op["nn_name"]]["nn_architecture"]
-            for li, layer in enumerate(layers):
-                name = layer.get("name", "layer_%d_%s_readout" % (li, layer["type_layer"]))  # AUX:909-910
-                W = self.p["readout_model_0/" + name + "/kernel"]
-                b = self.p["readout_model_0/" + name + "/bias"]
-                h = _act(h @ W + b, layer.get("activation"))
-            return h
+        """GM:605-655; names resolve as get_global_var_or_input (GM:660-675): <name>_state first."""
+        var = {k: v for k, v in state.items()}
+
+        def get(name):
+            return var[name] if name in var else np.asarray(x[name], self.dtype)
+
+        for counter, op in enumerate(self.d["readout"]):
+            t = op["type"]
+            if t in ("predict", "neural_network"):                         # GM:612-628
+                h = np.concatenate([get(i) for i in op["input"]], axis=1)
+                h = self._dense_stack(h, op, counter)
+                if t == "predict":
+                    return h
+                var[op.get("output_name", "None")] = h
+            elif t == "pooling":                                           # AUX:1165-1185
+                v = get(op["input"][0])
+                kind = op["type_pooling"]
+                if kind == "sum":
+                    r = v.sum(0)
+                elif kind == "mean":
+                    with np.errstate(invalid="ignore", divide="ignore"):
+                        r = v.sum(0) / np.asarray(v.shape[0], v.dtype)      # empty: 0/0 = NaN
+                elif kind == "max":
+                    r = v.max(0) if v.shape[0] else np.full(v.shape[1], -np.inf, v.dtype)
+                else:
+                    raise OracleError("pooling %r not restated" % kind)
+                var[op["output_name"]] = r.reshape(1, -1)
+            elif t == "product":                                           # AUX:1072-1088
+                if op["type_product"] != "element_wise":
+                    raise OracleError("dot_product (rank-4 tensordot) not restated")
+                var[op["output_name"]] = get(op["input"][0]) * get(op["input"][1])
+            elif t == "extend_adjacencies":                                # AUX:1236-1265
+                src = _gather(get(op["input"][0]), x["src_" + op["adj_list"]], "extend_adjacencies src")
+                dst = _gather(get(op["input"][1]), x["dst_" + op["adj_list"]], "extend_adjacencies dst")
+                var[op["output_name_src"]] = src
+                var[op["output_name_dst"]] = dst
+            else:
+                raise OracleError("readout op %s not restated" % t)
         raise OracleError("no predict operation")
 
 
@@ -283,12 +322,12 @@ def l2_regularization(description: dict, params: dict) -> float:
     """sum(model.losses) for the Dense kernel_regularizers (AUX:833-834, GM:749)."""
     nn = {n["nn_name"]: n for n in description["neural_networks"]}
     total = 0.0
-    for op in description["readout"]:
-        if op["type"] != "predict":
+    for counter, op in enumerate(description["readout"]):
+        if op["type"] not in ("predict", "neural_network"):
             continue
         for li, layer in enumerate(nn[op["nn_name"]]["nn_architecture"]):
             if "kernel_regularizer" in layer:
                 name = layer.get("name", "layer_%d_%s_readout" % (li, layer["type_layer"]))
-                W = np.asarray(params["readout_model_0/" + name + "/kernel"], np.float64)
+                W = np.asarray(params["readout_model_%d/%s/kernel" % (counter, name)], np.float64)
                 total += float(layer["kernel_regularizer"]) * float((W * W).sum())
     return total

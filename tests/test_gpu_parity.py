@@ -323,3 +323,51 @@ def test_message_network_ordered_mp():
     graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
     out, ref, _, _ = _run(desc, dims, graphs, seed=9, bias=0.1)
     _close(out, ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# readout operations before predict (GM:605-655, AUX:1033-1265)
+_POOL = lambda kind, inp, out: {"type": "pooling", "type_pooling": kind, "input": [inp], "output_name": out}
+_NN = lambda net, ins, out: {"type": "neural_network", "nn_name": net, "input": list(ins), "output_name": out}
+_PROD = lambda a, b, out: {"type": "product", "type_product": "element_wise", "input": [a, b], "output_name": out}
+_EXT = {"type": "extend_adjacencies", "adj_list": "adj_paths_links", "input": ["path", "link"],
+        "output_name_src": "ep", "output_name_dst": "el"}
+READOUT_CASES = {
+    "pool_sum": ([_POOL("sum", "path", "g")], ["g"], None),
+    "pool_mean": ([_POOL("mean", "link", "g")], ["g"], None),
+    "pool_max": ([_POOL("max", "path", "g")], ["g"], None),
+    "nn_pool_product": ([_NN("emb", ["path", "path"], "pe"), _POOL("max", "pe", "gmax"), _PROD("gmax", "pe", "prod")],
+                        ["prod", "path"], {"emb": [(32, "relu")]}),
+    "product_width1": ([_NN("gate", ["path"], "w"), _PROD("path", "w", "gated")], ["gated"], {"gate": [(1, "sigmoid")]}),
+    "extend_nn": ([_EXT, _NN("emb", ["ep", "el"], "edge")], ["edge"], {"emb": [(16, "tanh"), (32, "selu")]}),
+    "extend_pool": ([_EXT, _PROD("ep", "el", "pl"), _POOL("sum", "pl", "g"), _POOL("mean", "path", "gp")],
+                    ["g", "gp"], None),
+    "shadow_entity_name": ([_NN("emb", ["path"], "path")], ["path"], {"emb": [(48, "tanh")]}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(READOUT_CASES))
+@pytest.mark.parametrize("n", [1, 3])
+def test_readout_operations(case, n):
+    ops, pin, nets = READOUT_CASES[case]
+    desc = model_examples.routenet_readout(ops, pin, nets, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet" if g % 2 == 0 else "geant2", g)
+                                            for g in range(n)])
+    out, ref, b, _ = _run(desc, dims, graphs, seed=11, bias=0.1)
+    _close(out, ref)
+    assert int(b.graph_predictions.sum()) * b.output_units == out.size
+
+
+@pytest.mark.parametrize("kind", ["sum", "mean", "max"])
+def test_pooling_many_chunks(kind):
+    """Graph-level prediction on a 20 000-node graph: the pooling kernel reduces 5 chunks of
+    rows per graph, then the chunk partials in a fixed order."""
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=20000, iterations=2, window=64)
+    pred = desc["readout"][0]
+    pred["input"] = ["g"]
+    desc["readout"] = [_POOL(kind, "node", "g"), pred]
+    out, ref, b, _ = _run(desc, dims, graphs, seed=5, bias=0.1)
+    _close(out, ref)
+    assert out.size == 1

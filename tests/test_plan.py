@@ -148,3 +148,47 @@ def test_attention_convolution_lowering():
     plan = MPPlan.from_model_info(Model_information(d, DIMS))
     assert dict(plan.param_specs())["convolution/kernel"] == (32, 32)
     assert plan.mps[1]["act"] == 4
+
+
+def test_readout_ops_lowering():
+    """GM:605-655: tensor ids, row spaces, readout_model_<op index> names, predict counter."""
+    ops = [{"type": "extend_adjacencies", "adj_list": "adj_paths_links", "input": ["path", "link"],
+            "output_name_src": "ep", "output_name_dst": "el"},
+           {"type": "neural_network", "nn_name": "emb", "input": ["ep", "el"], "output_name": "edge"},
+           {"type": "pooling", "type_pooling": "mean", "input": ["edge"], "output_name": "g"}]
+    d = model_examples.routenet_readout(ops, ["g"], {"emb": [(16, "tanh")]})
+    plan = MPPlan.from_model_info(Model_information(d, DIMS))
+    assert plan.ro_spaces[2:] == [("adj", 1), ("adj", 1), ("adj", 1), ("graph",)]
+    assert plan.ro_widths[2:] == [32, 32, 16, 16]
+    assert plan.readout_inputs == [5] and plan.predict_counter == 3
+    names = dict(plan.param_specs())
+    assert names["readout_model_1/layer_0_Dense_readout/kernel"] == (64, 16)
+    assert names["readout_model_3/1st_dense_layer/kernel"] == (16, 256)
+
+
+@pytest.mark.parametrize("ops,pin,msg", [
+    ([{"type": "product", "type_product": "dot_product", "input": ["path", "path"], "output_name": "x"}], ["x"],
+     "tensordot"),
+    ([], ["traffic"], "raw input features"),
+    ([{"type": "extend_adjacencies", "adj_list": "adj_nodes", "input": ["path", "link"],
+       "output_name_src": "a", "output_name_dst": "b"}], ["a"], "not read by any message passing"),
+])
+def test_readout_ops_rejected(ops, pin, msg):
+    d = model_examples.routenet_readout(ops, pin)
+    with pytest.raises(UnsupportedModel, match=msg):
+        MPPlan.from_model_info(Model_information(d, DIMS))
+
+
+def test_readout_ops_engine_validation():
+    """Row-space rules the C plan enforces (no GPU needed: plan creation validates only)."""
+    from ignnition_amd.engine import Engine
+    from ignnition_amd._lib import EngineError as IgnError
+    ops = [{"type": "product", "type_product": "element_wise", "input": ["path", "link"], "output_name": "x"}]
+    d = model_examples.routenet_readout(ops, ["x"])
+    with pytest.raises(IgnError, match="different row spaces"):
+        Engine(MPPlan.from_model_info(Model_information(d, DIMS)))
+    ops = [{"type": "extend_adjacencies", "adj_list": "adj_paths_links", "input": ["link", "path"],
+            "output_name_src": "a", "output_name_dst": "b"}]
+    d = model_examples.routenet_readout(ops, ["a"])
+    with pytest.raises(IgnError, match="source and destination entities"):
+        Engine(MPPlan.from_model_info(Model_information(d, DIMS)))
