@@ -288,7 +288,7 @@ int  ign_adam_step(ign_plan* plan, const float* grads, float* m, float* v, int64
 int  ign_plan_get_params(ign_plan* plan, float* host_out);
 
 /* ---- Native dataset reader (GEN:32-230 = the reference's generator) -----
- * Reads every <dir>/*.tar.gz (sorted by name; data.json inside, a list of samples) on `threads`
+ * Reads the *.tar.gz files of <dir> (sorted by name; data.json inside, a list of samples) on `threads`
  * host threads and builds the generator's index contract per sample.  A sample that fails
  * abandons the rest of its file and is reported through ign_dataset_error (GEN:229-230); a file
  * without data.json fails the open.  Batches are gathered by sample id; ign_dataset_get returns
