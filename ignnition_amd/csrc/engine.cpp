@@ -167,7 +167,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = atoi(v) == 1 ? 1 : 2;
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(3, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
@@ -773,8 +773,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.bytes = (double)steps * (12.0 * H + 4) + (double)ND * (8.0 * H + 12);
       b->gru_steps += steps * p->T;
     } else {
-      if (p->sum_order == 0) {
-        sort_order(order, flen, b->row_off[dst], p->graph_major);
+      if (p->sum_order == 0 || p->sum_order == 3) {   // 3: graph-major (+ XCD-aware tiles) for sum MPs only
+        sort_order(order, flen, b->row_off[dst], p->graph_major || p->sum_order == 3);
       } else if (p->sum_order == 1) {
         auto by_cnt = [&](int32_t x, int32_t y) { return flen[x] > flen[y]; };
         for (int64_t c = 0; c < ND; c += 256)
@@ -1050,8 +1050,8 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                                mb.d_table + mb.zero_row * W3, st));
       tm.end();
     }
-    if (cp.H == 64 && p->seq_variant != 2)
-      return fail(IGN_ERR_UNSUPPORTED, "64-unit ordered updates need the LDS variant (IGN_SEQ_VARIANT=2)");
+    if (cp.H == 64 && p->seq_variant < 2)
+      return fail(IGN_ERR_UNSUPPORTED, "64-unit ordered updates need the LDS variants (IGN_SEQ_VARIANT=2 or 3)");
     SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                  p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
                  mb.n_steps};
@@ -1084,7 +1084,8 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     }
     if (count > 0) {
       SumGruArgs a{hin, hout, sbases, mb.d_order + first, mb.d_msg_ptr + first, mb.d_msg_src,
-                   p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count, p->xcd_remap};
+                   p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count,
+                   p->xcd_remap || p->sum_order == 3};
       if (mp.aggr == IGN_AGGR_ATTENTION) a.msg_w = mb.d_msg_w;
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
         a.conv_kp = p->d_packed + p->pk_conv;

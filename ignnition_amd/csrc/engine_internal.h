@@ -178,7 +178,8 @@ struct ign_plan {
                                   // (producer waves gather, consumer waves MFMA), 5 = LDS + header /
                                   // index prefetch one tile ahead; IGN_SUM_VARIANT
   int sum_order = 0;              // sum MPs: 0 global in-degree sort, 1 sort within 256-row chunks
-                                  // (keeps id locality), 2 id order; IGN_SUM_ORDER
+                                  // (keeps id locality), 2 id order, 3 per-graph sort + XCD-aware
+                                  // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
   // timing
   bool timing = false;

@@ -463,6 +463,170 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Variant 3 of the ordered update: seq_gru2's math, software-pipelined across output tiles so
+// that a wave's gate VALU runs in the shadow of its own MFMAs.  In seq_gru2 a step is
+// [48 MFMAs] -> [gate VALU], strictly serial within the wave, so the matrix pipe idles while a
+// wave computes gates unless another wave happens to be in its MFMA block (measured 52 % busy).
+// Here the hidden state's unit tiles h[0..NT-1] are finished one at a time:
+//   acc_t[o] = sum_j U[j][o] h_{t-1}[j]   (j = input tile, o = output tile, per gate)
+// and h_t[o] needs only acc_t[o].  So step t issues, in order,
+//   V0   gates of tile NT-1 of step t-1           ||  M1  acc_t[*] += U[j][*] h_{t-1}[j], j < NT-1
+//   M2   acc_t[0] += U[NT-1][0] h_{t-1}[NT-1]
+//   M3_o acc_t[o+1] += U[NT-1][o+1] h_{t-1}[NT-1] ||  V_o gates of tile o of step t (o < NT-1)
+// and tile NT-1 of step t is carried into the next iteration (accP, xP, actP).  Same fma order
+// per accumulator as seq_gru2 (bias, then k ascending), so results are bitwise identical.
+template <int H>
+__device__ __forceinline__ f4 gru_gate_tile(const f4& az, const f4& ar, const f4& ah, const f4& xz, const f4& xr,
+                                            const f4& xh, const f4& h, bool act) {
+  f4 out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float z = sig2_(az[r] + xz[r]);
+    const float rr = sig2_(ar[r] + xr[r]);
+    const float c = tanh2_(xh[r] + rr * ah[r]);
+    const float hn = c + z * (h[r] - c);
+    out[r] = act ? hn : h[r];
+  }
+  return out;
+}
+
+template <int H, bool SAVE>
+__global__ __launch_bounds__(256) void seq_gru3_kernel(SeqGruArgs a) {
+  constexpr int NT = H / 16, KH = H / 4, K4 = KH / 4;
+  static_assert(NT >= 2 && K4 == NT, "pipelining needs at least two unit tiles");
+  __shared__ float sbias[4 * H];
+  __shared__ f4 su[3 * NT * K4 * 64];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+  stage_frag_lds<H>(su, a.Up, KH);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const float* tab = a.table + 4 * g;
+  __syncthreads();
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int L = valid ? a.len[pos] : 0;
+    const uint32_t* codes = a.ablate ? a.step_code + a.zero_slot
+                                     : a.step_code + (valid ? a.step_ptr[pos] : 0);
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    int Lmax = L;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+    float* hsv = nullptr;
+    if constexpr (SAVE) {
+      hsv = a.hs_save + (valid ? (int64_t)a.step_ptr[pos] + pos : 0) * H + 4 * g;
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
+      }
+    }
+
+    // pending tile NT-1 of the previous step (none before step 0: actP = false keeps h)
+    f4 accP[3] = {f4{0, 0, 0, 0}, f4{0, 0, 0, 0}, f4{0, 0, 0, 0}};
+    f4 xP[3] = {f4{0, 0, 0, 0}, f4{0, 0, 0, 0}, f4{0, 0, 0, 0}};
+    bool actP = false;
+    uint32_t code = codes[0];
+    for (int t = 0; t < Lmax; ++t) {
+      // V0: finish tile NT-1 of step t-1 (independent of M1 below; same basic block, so the
+      // scheduler can interleave the two)
+      h[NT - 1] = gru_gate_tile<H>(accP[0], accP[1], accP[2], xP[0], xP[1], xP[2], h[NT - 1], actP);
+      if constexpr (SAVE) {
+        if (actP && valid) st4(hsv + (int64_t)t * H + 16 * (NT - 1), h[NT - 1]);
+      }
+      f4 x[3][NT];
+      {
+        const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+        for (int G = 0; G < 3; ++G)
+#pragma unroll
+          for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+      }
+      const uint32_t next = codes[t + 1];
+      f4 az[NT], ar[NT], ah[NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        az[i] = f4{0, 0, 0, 0};
+        ar[i] = f4{0, 0, 0, 0};
+        ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
+      }
+      // M1: input tiles 0..NT-2 (ready since the previous iteration) into every output tile
+#pragma unroll
+      for (int s4 = 0; s4 < NT - 1; ++s4) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const f4 wz = su[((0 * NT + i) * K4 + s4) * 64 + lane];
+          const f4 wr = su[((1 * NT + i) * K4 + s4) * 64 + lane];
+          const f4 wh = su[((2 * NT + i) * K4 + s4) * 64 + lane];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float hb = h[s4][q];
+            az[i] = MFMA(wz[q], hb, az[i]);
+            ar[i] = MFMA(wr[q], hb, ar[i]);
+            ah[i] = MFMA(wh[q], hb, ah[i]);
+          }
+        }
+      }
+      // interleave V0's VALU with M1's MFMAs: the loads first, then {1 MFMA, 3 VALU} groups
+      __builtin_amdgcn_sched_group_barrier(0x0020, 3 * NT + 1, 0);   // VMEM reads (x row, code)
+      __builtin_amdgcn_sched_group_barrier(0x0100, 3 * NT, 0);       // DS reads (U fragments)
+#pragma unroll
+      for (int k = 0; k < 12 * NT * (NT - 1); ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0002, 3, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bool act = t < L;
+      // M2 / M3_o: input tile NT-1, output tile by output tile; gates of tile o follow its M
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        {
+          constexpr int s4 = NT - 1;
+          const f4 wz = su[((0 * NT + i) * K4 + s4) * 64 + lane];
+          const f4 wr = su[((1 * NT + i) * K4 + s4) * 64 + lane];
+          const f4 wh = su[((2 * NT + i) * K4 + s4) * 64 + lane];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float hb = h[s4][q];
+            az[i] = MFMA(wz[q], hb, az[i]);
+            ar[i] = MFMA(wr[q], hb, ar[i]);
+            ah[i] = MFMA(wh[q], hb, ah[i]);
+          }
+        }
+        if (i >= 1) {   // V_{i-1}: tile i-1 of step t (h[NT-1] is still h_{t-1}: read above)
+          const int o = i - 1;
+          h[o] = gru_gate_tile<H>(az[o], ar[o], ah[o], x[0][o], x[1][o], x[2][o], h[o], act);
+          if constexpr (SAVE) {
+            if (act && valid) st4(hsv + (int64_t)(t + 1) * H + 16 * o, h[o]);
+          }
+        }
+      }
+      accP[0] = az[NT - 1];
+      accP[1] = ar[NT - 1];
+      accP[2] = ah[NT - 1];
+      xP[0] = x[0][NT - 1];
+      xP[1] = x[1][NT - 1];
+      xP[2] = x[2][NT - 1];
+      actP = act;
+      code = next;
+    }
+    h[NT - 1] = gru_gate_tile<H>(accP[0], accP[1], accP[2], xP[0], xP[1], xP[2], h[NT - 1], actP);
+    if constexpr (SAVE) {
+      if (actP && valid) st4(hsv + (int64_t)Lmax * H + 16 * (NT - 1), h[NT - 1]);
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
+    }
+  }  // tile loop
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
@@ -1335,7 +1499,18 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) 
 
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (variant == 2) {
+  if (variant == 3 && h >= 32) {   // pipelined (needs >= 2 unit tiles)
+    const int64_t work = grid_for(args.n_dst, 64);
+    if (h == 32) {
+      auto k = args.hs_save ? seq_gru3_kernel<32, true> : seq_gru3_kernel<32, false>;
+      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
+    } else if (h == 64) {
+      auto k = args.hs_save ? seq_gru3_kernel<64, true> : seq_gru3_kernel<64, false>;
+      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
+    } else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (variant >= 2) {
     const int64_t work = grid_for(args.n_dst, 64);
     if (h == 32) {
       auto k = args.hs_save ? seq_gru2_kernel<32, true> : seq_gru2_kernel<32, false>;

@@ -234,6 +234,30 @@ def test_hip_graph_replay_matches_direct(monkeypatch):
     np.testing.assert_array_equal(outs["0"], outs["1"])
 
 
+@pytest.mark.parametrize("hidden", [32, 64])
+def test_ordered_update_variants_bitwise_equal(monkeypatch, hidden):
+    """The pipelined ordered update (IGN_SEQ_VARIANT=3) keeps seq_gru2's fma order per
+    accumulator and its gate math: predictions and states are bitwise equal."""
+    desc = model_examples.routenet(hidden=hidden, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", g) for g in range(3)])
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(3, bias_scale=0.2)
+    outs = {}
+    for v in ("2", "3"):
+        monkeypatch.setenv("IGN_SEQ_VARIANT", v)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        outs[v] = (b.forward().reshape(-1), b.state("path"), b.state("link"))
+        b.close()
+        eng.close()
+    for a, c in zip(outs["2"], outs["3"]):
+        np.testing.assert_array_equal(a, c)
+    _close(outs["3"][0], DenseOracle(desc, dims, prm).forward(graphs))
+
+
 def test_timing_kinds_mask():
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
     plan = MPPlan.from_model_info(mi)
