@@ -8,6 +8,31 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
+// ---- split-bf16 contraction (fp32-exact operands on the bf16 matrix path) ------------------------
+// An fp32 value has 24 significand bits; truncating it to its top 16 bits (a bf16) and repeating on
+// the exact remainders gives x = hi + mid + lo EXACTLY (each piece <= 8 significant bits; the two
+// subtractions are exact, Sterbenz).  Products of bf16 pieces are exact in fp32, so a contraction
+// built from the piece products and accumulated in fp32 is an fp32 computation: all 9 products
+// (x9) differ from an fp32 fma chain only in summation order; x6 also drops mid*lo, lo*mid and
+// lo*lo (each < 2^-23 of |a b|, below half an fp32 ulp of the product).
+// The f32 MFMA (v_mfma_f32_16x16x4_f32) issues at the fp32 vector rate and does not overlap with
+// VALU work on its SIMD (tools/probes: MFMA + VALU time = sum); v_mfma_f32_16x16x32_bf16 does 16x
+// the MACs per cycle, so even 6-9 piece products cost less than one f32 pass.
+typedef short bf8 __attribute__((ext_vector_type(8)));      // 8 bf16: A/B fragment of 16x16x32
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+#define MFMA_BF(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+__device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {
+  hi = __uint_as_float(__float_as_uint(x) & 0xFFFF0000u);
+  const float r1 = x - hi;
+  mid = __uint_as_float(__float_as_uint(r1) & 0xFFFF0000u);
+  lo = r1 - mid;
+}
+// [bf16(a) | bf16(b) << 16] of values whose low 16 bits are dropped (exact for split3 pieces)
+__device__ __forceinline__ uint32_t pack_hi16(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+
 // Gate nonlinearities on v_exp_f32 + v_rcp_f32 (1 ulp each; an IEEE divide would expand to
 // ~10 VALU instructions and dominate the recurrence's VALU stream).  Both saturate cleanly:
 // exp overflow gives rcp(inf) = 0.

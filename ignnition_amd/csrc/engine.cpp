@@ -113,6 +113,7 @@ int ign::repack(ign_plan* p) {
     HIP_TRY(launch_pack_gru(p->d_params + cp.off_k, p->d_params + cp.off_rk, p->d_params + cp.off_b,
                             p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
                             p->stream));
+    if (cp.pk_ubf >= 0) HIP_TRY(launch_pack_u_bf16(p->d_params + cp.off_rk, p->d_packed + cp.pk_ubf, cp.H, p->stream));
     if (cp.pk_wt >= 0) {
       HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
       HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
@@ -167,7 +168,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(3, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(5, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
@@ -352,6 +353,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.pk_w = pk; pk = align(pk + 3LL * cp.din * cp.H);
     cp.pk_u = pk; pk = align(pk + 3LL * cp.H * cp.H);
     cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
+    if (pack_u_bf16_floats(cp.H)) { cp.pk_ubf = pk; pk = align(pk + pack_u_bf16_floats(cp.H)); }
   }
   for (size_t l = 0; l < p->dense.size(); ++l) {
     DenseP& dp = p->dense[l];
@@ -1055,6 +1057,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                  p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
                  mb.n_steps};
+    if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
     tm.begin(K_SEQ, mb.flops, mb.bytes);
     HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
     tm.end();

@@ -37,6 +37,7 @@ struct CellP {
   int64_t off_k, off_rk, off_b;   // raw Keras-layout params
   int64_t pk_w, pk_u, pk_b;       // packed fragments (in d_packed)
   int64_t pk_wt = -1, pk_ut = -1; // backward: unscaled W^T / U^T fragments (pack_a)
+  int64_t pk_ubf = -1;            // split-bf16 recurrent-kernel fragments (seq variants 4/5)
   bool used = false;
 };
 
@@ -168,7 +169,8 @@ struct ign_plan {
   bool params_set = false;
   bool fused_readout = false;
   int ro_width = 0;
-  int seq_variant = 2;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves)
+  int seq_variant = 2;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves),
+                                  // 3 = 2 software-pipelined, 4/5 = split-bf16 h.U (6 / 9 piece products)
   // Measured on 512 x synth50 (profiles/r01): one global length sort without XCD remap is the
   // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
   bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1

@@ -30,6 +30,7 @@ struct SeqGruArgs {
   int64_t zero_slot;         // index in step_code of a padding entry (= zero row)
   float* hs_save = nullptr;  // training: [n_steps + n_dst][H], order position p writes rows
                              // step_ptr[p] + p (state before) .. + len[p] (after each step)
+  const void* Ubf = nullptr;  // variants 4/5: recurrent kernel as exact 3-piece bf16 A fragments
 };
 
 struct SumGruArgs {
@@ -87,6 +88,9 @@ hipError_t launch_project(const float* x, int64_t n, const float* Wp, const floa
 hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, const int32_t* ptr,
                             const uint32_t* rows, int W, const float* bias_row, hipStream_t st);
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st);
+// recurrent kernel -> split-bf16 A fragments for seq variants 4/5 (H = 32 or 64); floats used: 9 H^2 / 2
+hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st);
+inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H * H / 2 : 0; }
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);

@@ -627,6 +627,163 @@ __global__ __launch_bounds__(256) void seq_gru3_kernel(SeqGruArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Variants 4 / 5 of the ordered update: seq_gru2's recurrence with h.U on the bf16 matrix path,
+// fp32-exact (device_common.h, split-bf16).  U (pre-scaled as for pack_gru) is split once into
+// three bf16 pieces (pack_u_bf16); every step splits the wave's hidden state the same way and
+// forms the 9 (variant 5) or 6 (variant 4) piece products per gate tile with
+// v_mfma_f32_16x16x32_bf16, accumulated in fp32 from the bias.
+// Fragment layout of 16x16x32 (lane l, element j): A[m = l&15][k = 8(l>>4) + j],
+// B[k][n = l&15].  The k order is permuted, kperm(s, g, j) = 16 (2s + (j>>2)) + 4g + (j&3), so
+// the B fragment of k-step s is exactly registers (2s .. 2s+1) of the lane's accumulator tiles:
+// the state still never leaves the lane.
+__global__ void pack_u_bf16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out, int H) {
+  const int NT = H / 16, KS = H / 32;
+  const int64_t total = 9LL * NT * KS * 64 * 8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // ((piece * 3 + gate) * NT + tile) * KS + s
+    const int s = (int)(f % KS); f /= KS;
+    const int i = (int)(f % NT); f /= NT;
+    const int G = (int)(f % 3);
+    const int piece = (int)(f / 3);
+    const int k = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
+    const int col = G * H + 16 * i + (lane & 15);
+    const float sc = G == 2 ? IGN_2LOG2E : IGN_NLOG2E;   // as pack_gru
+    float p[3];
+    split3(sc * U[(int64_t)k * 3 * H + col], p[0], p[1], p[2]);
+    out[e] = (uint16_t)(__float_as_uint(p[piece]) >> 16);
+  }
+}
+
+template <int H, bool SAVE, int PASSES>
+__global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
+  constexpr int NT = H / 16, KS = H / 32;
+  constexpr int NF = 9 * NT * KS;            // fragments: 3 pieces x 3 gates x NT tiles x KS k-steps
+  static_assert(H == 32 || H == 64, "split-bf16 ordered update: 32 or 64 units");
+  __shared__ float sbias[4 * H];
+  __shared__ bf8 su[NF * 64];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+  {
+    const u4v* src = reinterpret_cast<const u4v*>(a.Ubf);
+    u4v* dst = reinterpret_cast<u4v*>(su);
+    for (int e = threadIdx.x; e < NF * 64; e += blockDim.x) dst[e] = src[e];
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const float* tab = a.table + 4 * g;
+  __syncthreads();
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int L = valid ? a.len[pos] : 0;
+    const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    int Lmax = L;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+    float* hsv = nullptr;
+    if constexpr (SAVE) {
+      hsv = a.hs_save + (valid ? (int64_t)a.step_ptr[pos] + pos : 0) * H + 4 * g;
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
+      }
+    }
+    uint32_t code = codes[0];
+    for (int t = 0; t < Lmax; ++t) {
+      f4 x[3][NT];
+      {
+        const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+        for (int G = 0; G < 3; ++G)
+#pragma unroll
+          for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+      }
+      const uint32_t next = codes[t + 1];
+      // B fragments: the three exact bf16 pieces of the state, k-step s = accumulator tiles 2s, 2s+1
+      bf8 hf[3][KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        u4v w0, w1, w2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e0 = 2 * q, e1 = 2 * q + 1;
+          float a0, a1, a2, b0, b1, b2;
+          split3(h[2 * s + (e0 >> 2)][e0 & 3], a0, a1, a2);
+          split3(h[2 * s + (e1 >> 2)][e1 & 3], b0, b1, b2);
+          w0[q] = pack_hi16(a0, b0);
+          w1[q] = pack_hi16(a1, b1);
+          w2[q] = pack_hi16(a2, b2);
+        }
+        hf[0][s] = __builtin_bit_cast(bf8, w0);
+        hf[1][s] = __builtin_bit_cast(bf8, w1);
+        hf[2][s] = __builtin_bit_cast(bf8, w2);
+      }
+      f4 acc[3][NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        acc[0][i] = f4{0, 0, 0, 0};
+        acc[1][i] = f4{0, 0, 0, 0};
+        acc[2][i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
+      }
+      // the fragment reads are loop-invariant: an opaque lane offset keeps the compiler from
+      // hoisting all of them out of the step loop into registers (occupancy)
+      int lofs = lane;
+      asm volatile("" : "+v"(lofs));
+      // piece products, grouped by U piece (each A fragment read once per step), small first:
+      // x9: U lo x {lo, mid, hi}, U mid x {lo, mid, hi}, U hi x {lo, mid, hi}
+      // x6: U lo x hi, U mid x {mid, hi}, U hi x {lo, mid, hi}
+#pragma unroll
+      for (int pu = 2; pu >= 0; --pu) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) {
+            bf8 w[3];
+#pragma unroll
+            for (int G = 0; G < 3; ++G) w[G] = su[(((pu * 3 + G) * NT + i) * KS + s) * 64 + lofs];
+#pragma unroll
+            for (int ph = 2; ph >= 0; --ph) {
+              if (PASSES == 6 && pu + ph > 2) continue;
+#pragma unroll
+              for (int G = 0; G < 3; ++G) acc[G][i] = MFMA_BF(w[G], hf[ph][s], acc[G][i]);
+            }
+          }
+        }
+      }
+      const bool act = t < L;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
+          const float z = sig2_(acc[0][i][r] + x[0][i][r]);
+          const float rr = sig2_(acc[1][i][r] + x[1][i][r]);
+          const float c = tanh2_(x[2][i][r] + rr * acc[2][i][r]);
+          const float hn = c + z * (h[i][r] - c);
+          h[i][r] = act ? hn : h[i][r];
+        }
+      }
+      if constexpr (SAVE) {
+        if (act && valid) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) st4(hsv + (int64_t)(t + 1) * H + 16 * i, h[i]);
+        }
+      }
+      code = next;
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
+    }
+  }  // tile loop
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
@@ -1438,6 +1595,12 @@ hipError_t launch_pack_gru(const float* W, const float* U, const float* bias, fl
   return hipGetLastError();
 }
 
+hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st) {
+  if (H != 32 && H != 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_u_bf16_kernel, dim3(64), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_dense(const float* W, float* Wp, int IN, int OUT, hipStream_t st) {
   return launch_pack_dense_pad(W, Wp, IN, IN, OUT, st);
 }
@@ -1499,6 +1662,21 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) 
 
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
+  if (variant >= 4 && (h == 32 || h == 64)) {   // split-bf16 h.U: 4 = six piece products, 5 = nine
+    if (!args.Ubf) return hipErrorInvalidValue;
+    const int64_t work = grid_for(args.n_dst, 64);
+#define SEQ_BF(HH, P)                                                                              \
+    {                                                                                              \
+      auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P> : seq_gru_bf_kernel<HH, false, P>;   \
+      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);              \
+    }
+    if (h == 32 && variant == 4) SEQ_BF(32, 6)
+    else if (h == 32) SEQ_BF(32, 9)
+    else if (variant == 4) SEQ_BF(64, 6)
+    else SEQ_BF(64, 9)
+#undef SEQ_BF
+    return hipGetLastError();
+  }
   if (variant == 3 && h >= 32) {   // pipelined (needs >= 2 unit tiles)
     const int64_t work = grid_for(args.n_dst, 64);
     if (h == 32) {

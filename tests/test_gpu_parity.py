@@ -258,6 +258,40 @@ def test_ordered_update_variants_bitwise_equal(monkeypatch, hidden):
     _close(outs["3"][0], DenseOracle(desc, dims, prm).forward(graphs))
 
 
+def _scaled_err(got, exp):
+    got = np.asarray(got, np.float64).reshape(-1)
+    exp = np.asarray(exp, np.float64).reshape(-1)
+    return float((np.abs(got - exp) / np.maximum(1.0, np.abs(exp))).max())
+
+
+@pytest.mark.parametrize("hidden", [32, 64])
+def test_split_bf16_ordered_update_is_fp32_accurate(monkeypatch, hidden):
+    """Variants 4 / 5 form h.U from exact 3-piece bf16 splits (6 / 9 piece products, fp32
+    accumulation).  Their error vs the float64 oracle stays at the level of the native f32-MFMA
+    kernel (variant 2): within 4x of it (or 1e-6), far inside the 1e-4 parity tolerance."""
+    desc = model_examples.routenet(hidden=hidden, iterations=8)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", g) for g in range(3)])
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(5, bias_scale=0.2)
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    errs = {}
+    for v in ("2", "4", "5"):
+        monkeypatch.setenv("IGN_SEQ_VARIANT", v)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        out = b.forward().reshape(-1)
+        b.close()
+        eng.close()
+        _close(out, ref)
+        errs[v] = _scaled_err(out, ref)
+    print("max scaled error vs float64 oracle:", errs)
+    for v in ("4", "5"):
+        assert errs[v] <= max(4 * errs["2"], 1e-6), errs
+
+
 def test_timing_kinds_mask():
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
     plan = MPPlan.from_model_info(mi)
