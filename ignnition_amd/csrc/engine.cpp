@@ -140,8 +140,12 @@ int ign::repack(ign_plan* p) {
   if (p->pk_w12 >= 0)
     HIP_TRY(launch_attn_vectors(p->d_params + p->off_k1, p->d_params + p->off_k2, p->d_params + p->off_att, p->attn_F,
                                 p->d_packed + p->pk_w12, p->stream));
-  for (auto& dp : p->dense)
+  for (auto& dp : p->dense) {
     if (dp.pk_w >= 0) HIP_TRY(launch_pack_dense(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in, dp.out, p->stream));
+    if (dp.pk_bf >= 0)   // layer 1 reads its input from memory (natural k), layer 2 chains from registers
+      HIP_TRY(launch_pack_dense_bf16(p->d_params + dp.off_w, p->d_packed + dp.pk_bf, dp.in, dp.out, &dp != &p->dense[0],
+                                     p->stream));
+  }
   for (auto& dp : p->dense)
     if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
   return readout_repack(p);
@@ -175,6 +179,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(5, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
+  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(3, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -360,6 +365,11 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if ((p->fused_readout && l < 2) || dense_fwd_supported(dp.in, dp.out)) {
       dp.pk_w = pk;
       pk = align(pk + (int64_t)dp.in * dp.out);
+    }
+    if (p->fused_readout && l < 2 && dp.in % 32 == 0 && dp.out % 16 == 0 &&
+        readout_bf_supported(p->dense[0].in, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act)) {
+      dp.pk_bf = pk;
+      pk = align(pk + 3LL * dp.in * dp.out / 2);
     }
   }
   // backward fragments (training): W^T / U^T per cell, W^T per Dense layer where the MFMA
@@ -1155,7 +1165,11 @@ int readout(ign_plan* p, ign_batch* b) {
     if (!a.b1 || !a.b2) return fail(IGN_ERR_UNSUPPORTED, "fused readout requires use_bias on hidden layers");
     double flops = 2.0 * P * ((double)l1.in * l1.out + (double)l2.in * l2.out + l3.in);
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0));
-    HIP_TRY(launch_readout3(a, l1.in, l1.out, l2.out, st));
+    if (p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0)
+      HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
+                                p->readout_variant == 3 ? 9 : 6, st));
+    else
+      HIP_TRY(launch_readout3(a, l1.in, l1.out, l2.out, st));
     tm.end();
   } else {
     const float* in = x;

@@ -46,6 +46,7 @@ struct DenseP {
   float l2 = 0.f;
   int64_t off_w, off_b, pk_w = -1;   // pk_w: forward fragments (fused readout, training readout)
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
+  int64_t pk_bf = -1;             // fused readout: split-bf16 A fragments (readout variants 2/3)
 };
 
 struct MsgNN {                    // message-creation network of one MP source (GM:440-475)
@@ -168,6 +169,8 @@ struct ign_plan {
   float* d_packed = nullptr;
   bool params_set = false;
   bool fused_readout = false;
+  int readout_variant = 2;        // fused readout: 1 = f32 MFMA (readout3), 2 / 3 = split-bf16 with 6 / 9
+                                  // piece products (readout_bf); IGN_READOUT_VARIANT
   int ro_width = 0;
   int seq_variant = 2;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves),
                                   // 3 = 2 software-pipelined, 4/5 = split-bf16 h.U (6 / 9 piece products)

@@ -94,6 +94,12 @@ inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
+// readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from
+// launch_pack_dense_bf16 (W1 natural k order, W2 chained); floats used: 3 IN OUT / 2
+bool readout_bf_supported(int din, int n1, int n2, int act1, int act2);
+hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
+                             hipStream_t st);
+hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
                                 int out, int act, float* y, hipStream_t st);
 hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,

@@ -1534,6 +1534,156 @@ __global__ __launch_bounds__(256) void readout3_kernel(Readout3Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused readout MLP on the bf16 matrix path, fp32-exact operands (device_common.h, split-bf16):
+// y = act2(act1(X W1 + b1) W2 + b2) . w3 + b3 with every contraction formed from exact 3-piece
+// bf16 splits of both operands (PASSES = 6 or 9 piece products, fp32 accumulation).
+// Weights: pack_dense_bf16 fragments (output tile u, k-step s, piece p), 1 KB each; a 16-unit
+// chunk of W2 is contiguous (24 KB), staged through LDS per workgroup, double-buffered.  W1 (DIN
+// = 32: 48 KB) stays in LDS for the block.  One wave = 16 rows: the layer-1 activations are
+// split once into 3 x 8 B fragments (96 VGPRs, accumulator layout = chained k order) and feed
+// all 16 chunks; layer 2 is contracted with w3 per chunk and never stored.
+__global__ void pack_dense_bf16_kernel(const float* __restrict__ W, uint16_t* __restrict__ out, int IN, int OUT,
+                                       int chained) {
+  const int KS = IN / 32;
+  const int64_t total = (int64_t)(OUT / 16) * KS * 3 * 512;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // (u * KS + s) * 3 + piece
+    const int piece = (int)(f % 3); f /= 3;
+    const int s = (int)(f % KS);
+    const int u = (int)(f / KS);
+    const int g = lane >> 4;
+    const int k = chained ? 16 * (2 * s + (j >> 2)) + 4 * g + (j & 3) : 32 * s + 8 * g + j;
+    float p[3];
+    split3(W[(int64_t)k * OUT + 16 * u + (lane & 15)], p[0], p[1], p[2]);
+    out[e] = (uint16_t)(__float_as_uint(p[piece]) >> 16);
+  }
+}
+
+// the three B fragments of 8 consecutive values v[0..7] (element j = v[j])
+__device__ __forceinline__ void split_frag(const float (&v)[8], bf8 (&f)[3]) {
+  u4v w0, w1, w2;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float a0, a1, a2, b0, b1, b2;
+    split3(v[2 * q], a0, a1, a2);
+    split3(v[2 * q + 1], b0, b1, b2);
+    w0[q] = pack_hi16(a0, b0);
+    w1[q] = pack_hi16(a1, b1);
+    w2[q] = pack_hi16(a2, b2);
+  }
+  f[0] = __builtin_bit_cast(bf8, w0);
+  f[1] = __builtin_bit_cast(bf8, w1);
+  f[2] = __builtin_bit_cast(bf8, w2);
+}
+
+// acc += sum over piece pairs (A piece pu, B piece ph) of A_pu . B_ph, small products first
+template <int PASSES>
+__device__ __forceinline__ f4 split_mfma(const bf8* __restrict__ afrag, int stride, const bf8 (&b)[3], f4 acc) {
+#pragma unroll
+  for (int pu = 2; pu >= 0; --pu) {
+    const bf8 w = afrag[pu * stride];
+#pragma unroll
+    for (int ph = 2; ph >= 0; --ph) {
+      if (PASSES == 6 && pu + ph > 2) continue;
+      acc = MFMA_BF(w, b[ph], acc);
+    }
+  }
+  return acc;
+}
+
+template <int DIN, int ACT, int WAVES, int PASSES>
+__global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, const bf8* __restrict__ W1f,
+                                                                 const bf8* __restrict__ W2f) {
+  constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
+  constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
+  constexpr int NTH = 64 * WAVES;
+  constexpr int CHF = KS2 * 3 * 64;              // bf8 per W2 chunk (24 KB)
+  constexpr bool W1_LDS = DIN == 32;
+  constexpr int W1F = W1_LDS ? U1 * KS1 * 3 * 64 : 1;
+  __shared__ bf8 sw2[2][CHF];
+  __shared__ bf8 sw1[W1F];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int j = lane & 15, g = lane >> 4;
+  const u4v* W2v = reinterpret_cast<const u4v*>(W2f);
+  if constexpr (W1_LDS) {
+    const u4v* W1v = reinterpret_cast<const u4v*>(W1f);
+    for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
+  }
+  for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
+  const int64_t r = ((int64_t)blockIdx.x * WAVES + wave) * 16 + j;
+  const bool ok = r < a.n_rows;
+  // layer-1 input fragments: lane (row j, group g) holds x[row][32s + 8g .. +8) (natural k order)
+  bf8 xf[KS1][3];
+  {
+    const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+      const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      split_frag(v, xf[s]);
+    }
+  }
+  __syncthreads();
+  // layer 1 -> activations in accumulator layout -> split once into the layer-2 B fragments
+  bf8 hf[KS2][3];
+#pragma unroll
+  for (int s2 = 0; s2 < KS2; ++s2) {
+    float v[8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int u = 2 * s2 + half;
+      f4 acc = ld4(a.b1 + 16 * u + 4 * g);
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) {
+        const bf8* af = W1_LDS ? sw1 + ((u * KS1 + s) * 3) * 64 + lane : W1f + ((u * KS1 + s) * 3) * 64 + lane;
+        acc = split_mfma<PASSES>(af, 64, xf[s], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[4 * half + q] = act_t<ACT>(acc[q]);
+    }
+    split_frag(v, hf[s2]);
+  }
+  float y = 0.f;
+#pragma unroll 1
+  for (int v = 0; v < U2; ++v) {
+    const int cur = v & 1;
+    const f4 b = ld4(a.b2 + 16 * v + 4 * g);
+    const f4 w3 = ld4(a.w3 + 16 * v + 4 * g);
+    const int nv = (v + 1) % U2;
+    constexpr int PER = (CHF + NTH - 1) / NTH;
+    u4v stage[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + NTH * k;
+      if (i < CHF) stage[k] = W2v[(int64_t)nv * CHF + i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // opaque lane offset: the LDS reads must not be hoisted out of the chunk loop (registers)
+    int lofs = lane;
+    asm volatile("" : "+v"(lofs));
+    f4 acc = b;
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) acc = split_mfma<PASSES>(sw2[cur] + s * 3 * 64 + lofs, 64, hf[s], acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y += w3[q] * act_t<ACT>(acc[q]);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + NTH * k;
+      if (i < CHF) reinterpret_cast<u4v*>(sw2[cur ^ 1])[i] = stage[k];
+    }
+    __syncthreads();
+  }
+  y += __shfl_xor(y, 16);
+  y += __shfl_xor(y, 32);
+  if (g == 0 && ok) {
+    const float b3 = a.b3 ? a.b3[0] : 0.f;
+    a.y[r] = act_apply(y + b3, a.act3);
+  }
+}
+
 // Generic Dense layer (any shape): y[n][o] = act(sum_k x[n][k] W[k][o] + b[o]).  Used for
 // readout stacks that do not match the fused 3-layer kernel.
 __global__ void dense_generic_kernel(const float* __restrict__ x, int64_t n, int in, int x_stride,
@@ -1765,6 +1915,40 @@ static hipError_t readout3_din(const Readout3Args& args, int act, dim3 grid, hip
     case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_SIGMOID>), grid, dim3(256), 0, st, args); break;
     default: hipLaunchKernelGGL((readout3_kernel<DIN, 256, 256, IGN_K_ACT_LINEAR>), grid, dim3(256), 0, st, args); break;
   }
+  return hipGetLastError();
+}
+
+template <int DIN, int WAVES, int PASSES>
+static hipError_t readout_bf_din(const Readout3Args& args, const void* W1f, const void* W2f, hipStream_t st) {
+  const dim3 grid((unsigned)((args.n_rows + 16 * WAVES - 1) / (16 * WAVES))), block(64 * WAVES);
+  const bf8* w1 = static_cast<const bf8*>(W1f);
+  const bf8* w2 = static_cast<const bf8*>(W2f);
+  switch (args.act1) {
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
+    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
+  }
+  return hipGetLastError();
+}
+
+bool readout_bf_supported(int din, int n1, int n2, int act1, int act2) {
+  return (din == 32 || din == 64) && n1 == 256 && n2 == 256 && act1 == act2;
+}
+
+hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
+                             hipStream_t st) {
+  if (args.n_rows == 0) return hipSuccess;
+  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f) return hipErrorInvalidValue;
+  if (din == 32) return passes == 9 ? readout_bf_din<32, 12, 9>(args, W1f, W2f, st) : readout_bf_din<32, 12, 6>(args, W1f, W2f, st);
+  return passes == 9 ? readout_bf_din<64, 12, 9>(args, W1f, W2f, st) : readout_bf_din<64, 12, 6>(args, W1f, W2f, st);
+}
+
+hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st) {
+  if (IN % 32 || OUT % 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_dense_bf16_kernel, dim3(128), dim3(256), 0, st, W, static_cast<uint16_t*>(out), IN, OUT,
+                     chained);
   return hipGetLastError();
 }
 
