@@ -172,7 +172,7 @@ struct ign_plan {
   int readout_variant = 2;        // fused readout: 1 = f32 MFMA (readout3), 2 / 3 = split-bf16 with 6 / 9
                                   // piece products (readout_bf); IGN_READOUT_VARIANT
   int ro_width = 0;
-  int seq_variant = 2;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves),
+  int seq_variant = 4;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves),
                                   // 3 = 2 software-pipelined, 4/5 = split-bf16 h.U (6 / 9 piece products)
   // Measured on 512 x synth50 (profiles/r01): one global length sort without XCD remap is the
   // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.

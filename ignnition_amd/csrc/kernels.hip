@@ -1593,13 +1593,14 @@ __device__ __forceinline__ f4 split_mfma(const bf8* __restrict__ afrag, int stri
   return acc;
 }
 
-template <int DIN, int ACT, int WAVES, int PASSES>
+template <int DIN, int ACT, int WAVES, int PASSES, int CT>
 __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, const bf8* __restrict__ W1f,
                                                                  const bf8* __restrict__ W2f) {
   constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
   constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
   constexpr int NTH = 64 * WAVES;
-  constexpr int CHF = KS2 * 3 * 64;              // bf8 per W2 chunk (24 KB)
+  constexpr int CHF = CT * KS2 * 3 * 64;         // bf8 per W2 chunk of CT output tiles (24 KB each)
+  constexpr int NCH = U2 / CT;
   constexpr bool W1_LDS = DIN == 32;
   constexpr int W1F = W1_LDS ? U1 * KS1 * 3 * 64 : 1;
   __shared__ bf8 sw2[2][CHF];
@@ -1648,11 +1649,15 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
   }
   float y = 0.f;
 #pragma unroll 1
-  for (int v = 0; v < U2; ++v) {
+  for (int v = 0; v < NCH; ++v) {
     const int cur = v & 1;
-    const f4 b = ld4(a.b2 + 16 * v + 4 * g);
-    const f4 w3 = ld4(a.w3 + 16 * v + 4 * g);
-    const int nv = (v + 1) % U2;
+    f4 b[CT], w3[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      b[c] = ld4(a.b2 + 16 * (CT * v + c) + 4 * g);
+      w3[c] = ld4(a.w3 + 16 * (CT * v + c) + 4 * g);
+    }
+    const int nv = (v + 1) % NCH;
     constexpr int PER = (CHF + NTH - 1) / NTH;
     u4v stage[PER];
 #pragma unroll
@@ -1664,11 +1669,18 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     // opaque lane offset: the LDS reads must not be hoisted out of the chunk loop (registers)
     int lofs = lane;
     asm volatile("" : "+v"(lofs));
-    f4 acc = b;
+    f4 acc[CT];
 #pragma unroll
-    for (int s = 0; s < KS2; ++s) acc = split_mfma<PASSES>(sw2[cur] + s * 3 * 64 + lofs, 64, hf[s], acc);
+    for (int c = 0; c < CT; ++c) acc[c] = b[c];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) y += w3[q] * act_t<ACT>(acc[q]);
+    for (int s = 0; s < KS2; ++s)
+#pragma unroll
+      for (int c = 0; c < CT; ++c)
+        acc[c] = split_mfma<PASSES>(sw2[cur] + (c * KS2 + s) * 3 * 64 + lofs, 64, hf[s], acc[c]);
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y += w3[c][q] * act_t<ACT>(acc[c][q]);
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + NTH * k;
@@ -1918,17 +1930,17 @@ static hipError_t readout3_din(const Readout3Args& args, int act, dim3 grid, hip
   return hipGetLastError();
 }
 
-template <int DIN, int WAVES, int PASSES>
+template <int DIN, int WAVES, int PASSES, int CT>
 static hipError_t readout_bf_din(const Readout3Args& args, const void* W1f, const void* W2f, hipStream_t st) {
   const dim3 grid((unsigned)((args.n_rows + 16 * WAVES - 1) / (16 * WAVES))), block(64 * WAVES);
   const bf8* w1 = static_cast<const bf8*>(W1f);
   const bf8* w2 = static_cast<const bf8*>(W2f);
   switch (args.act1) {
-    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
-    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
   }
   return hipGetLastError();
 }
@@ -1941,8 +1953,13 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
                              hipStream_t st) {
   if (args.n_rows == 0) return hipSuccess;
   if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f) return hipErrorInvalidValue;
-  if (din == 32) return passes == 9 ? readout_bf_din<32, 12, 9>(args, W1f, W2f, st) : readout_bf_din<32, 12, 6>(args, W1f, W2f, st);
-  return passes == 9 ? readout_bf_din<64, 12, 9>(args, W1f, W2f, st) : readout_bf_din<64, 12, 6>(args, W1f, W2f, st);
+  // 32-unit W2 chunks (two accumulators per wave, 8 barriers per tile); LDS 96 + 48 KB at DIN 32
+  // (passes < 0: 16-unit chunks, diagnostics).  DIN 64 keeps 16-unit chunks (registers)
+  if (din == 32) {
+    if (passes < 0) return readout_bf_din<32, 12, 6, 1>(args, W1f, W2f, st);
+    return passes == 9 ? readout_bf_din<32, 12, 9, 2>(args, W1f, W2f, st) : readout_bf_din<32, 12, 6, 2>(args, W1f, W2f, st);
+  }
+  return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
 }
 
 hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st) {
