@@ -11,7 +11,7 @@ from collections import defaultdict
 
 import re
 
-KINDS = {"seq_gru": r"seq_gru\w*_kernel", "sum_gru": r"sum_gru\w*_kernel", "readout": r"readout3_kernel",
+KINDS = {"seq_gru": r"seq_gru\w*_kernel", "sum_gru": r"sum_gru\w*_kernel", "readout": r"readout\w*_kernel",
          "project": r"project_kernel", "init_state": r"init_state_kernel"}
 
 
