@@ -1885,6 +1885,15 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
     else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args);    \
     return hipGetLastError();                                                              \
   }
+  if (din == 32 && h == 32 && mode == 0 && variant >= 2) {
+    // W/U fragments in LDS (24 KB per block) instead of 96 VGPRs: 6+ waves per SIMD keep more
+    // source-row gathers in flight than the register-weight kernel's 2
+    constexpr int WV = 4;
+    auto kern = variant == 5 ? sum_gru_lds_kernel<32, 32, WV, 8> : sum_gru_lds_kernel<32, 32, WV, 4>;
+    const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
+    hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
+    return hipGetLastError();
+  }
   SUM_CASE(32, 32)
   SUM_CASE(16, 16)
   SUM_CASE(16, 32)
