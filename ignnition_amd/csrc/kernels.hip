@@ -787,13 +787,16 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
-// MODE 0 sum (AUX:261); 1 attention: messages weighted by their softmax coefficient (AUX:339-342);
+// MODE 0 sum (AUX:261), 3 the same sum with the tile's message indices staged in LDS; 1 attention: messages weighted by their softmax coefficient (AUX:339-342);
 // 2 convolution: x = act((sum_m h_src . K + h) / deg) (AUX:384-401; K.sum = sum.K, exact
 // reassociation).  Then one GRU step (AUX:764).
+constexpr int kIdxCap = 1024;   // MODE 3: staged message indices per wave
+
 template <int DIN, int H, int MODE>
 __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
   constexpr int NC = DIN / 16, NT = H / 16;
   __shared__ float sbias[4 * H];
+  __shared__ uint32_t sidx[MODE == 3 ? 4 : 1][MODE == 3 ? kIdxCap : 1];
   for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
 
   const int lane = threadIdx.x & 63;
@@ -815,7 +818,46 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
     int64_t m = m0;
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == 3) {
+      // plain sum with the tile's message indices staged in LDS: the 16 rows' CSR ranges are one
+      // contiguous range, read with coalesced loads in one memory round trip, so the row gathers
+      // no longer wait behind dependent index loads (18 -> 10 round trips at ~36 messages)
+      const int64_t p0 = tile * 16, p1 = p0 + 16 < a.n_dst ? p0 + 16 : a.n_dst;
+      const int64_t t0 = a.msg_ptr[p0], t1 = a.msg_ptr[p1];
+      uint32_t* sx = sidx[wave];
+      for (int64_t base = t0; base < t1; base += kIdxCap) {
+        const int cnt = (int)(t1 - base < kIdxCap ? t1 - base : kIdxCap);
+        for (int i = lane; i < cnt; i += 64) sx[i] = a.msg_src[base + i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t lo = m0 > base ? m0 : base, hi = m1 < base + cnt ? m1 : base + cnt;
+        int64_t q = lo;
+        for (; q + 4 <= hi; q += 4) {
+          const uint32_t* c = sx + (q - base);
+          const float* r0 = src_ptr(a.src, c[0], DIN);
+          const float* r1 = src_ptr(a.src, c[1], DIN);
+          const float* r2 = src_ptr(a.src, c[2], DIN);
+          const float* r3 = src_ptr(a.src, c[3], DIN);
+          f4 v0[NC], v1[NC], v2[NC], v3[NC];
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) {
+            v0[cc] = ld4(r0 + 16 * cc + 4 * g);
+            v1[cc] = ld4(r1 + 16 * cc + 4 * g);
+            v2[cc] = ld4(r2 + 16 * cc + 4 * g);
+            v3[cc] = ld4(r3 + 16 * cc + 4 * g);
+          }
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) x[cc] = (((x[cc] + v0[cc]) + v1[cc]) + v2[cc]) + v3[cc];
+        }
+        for (; q < hi; ++q) {
+          const float* r = src_ptr(a.src, sx[q - base], DIN);
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) x[cc] += ld4(r + 16 * cc + 4 * g);
+        }
+        __builtin_amdgcn_wave_barrier();   // every lane is done with sx before the next chunk
+      }
+    } else if constexpr (MODE == 1) {
       for (; m < m1; ++m) {
         const float w = a.msg_w[m];
         const float* p = src_ptr(a.src, a.msg_src[m], DIN);
@@ -1882,12 +1924,13 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
     if (mode == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 1>), grid, dim3(256), 0, st, args); \
     else if (mode == 2 && D == HH) hipLaunchKernelGGL((sum_gru_kernel<D, (D == HH ? HH : D), (D == HH ? 2 : 0)>), grid, dim3(256), 0, st, args); \
     else if (mode == 2) return hipErrorInvalidValue;                                       \
-    else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args);    \
+    else if (variant == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args); \
+    else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 3>), grid, dim3(256), 0, st, args);    \
     return hipGetLastError();                                                              \
   }
-  if (din == 32 && h == 32 && mode == 0 && variant >= 2) {
-    // W/U fragments in LDS (24 KB per block) instead of 96 VGPRs: 6+ waves per SIMD keep more
-    // source-row gathers in flight than the register-weight kernel's 2
+  if (din == 32 && h == 32 && mode == 0 && (variant == 4 || variant == 5)) {   // measured slower: diagnostics
+    // W/U fragments in LDS (24 KB per block) instead of 96 VGPRs: 4-5 waves per SIMD instead of 2
+    // (0.124-0.137 ms vs 0.114 on 512 x synth50: more waves did not help)
     constexpr int WV = 4;
     auto kern = variant == 5 ? sum_gru_lds_kernel<32, 32, WV, 8> : sum_gru_lds_kernel<32, 32, WV, 4>;
     const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
