@@ -177,8 +177,9 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
-  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(5, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(6, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
+  if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v) != 0;
   if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(4, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
@@ -864,6 +865,60 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
           if ((rc = dev_alloc(b.get(), &mb.d_s_src[s], rows_s))) return rc;
         }
       }
+      // windowed sum: one workgroup per (graph, chunk of <= 256 destinations by message count), the
+      // destination's source rows ascending (a fixed summation order), LDS windows over the graph's
+      // source rows; the GRU step then reads x through an identity CSR over the same order
+      // (small graphs only: a workgroup walks all of its graph's windows, at most 4 of them)
+      int64_t max_src_rows = 0;
+      if (S == 1)
+        for (int g = 0; g < G; ++g)
+          max_src_rows = std::max(max_src_rows, b->row_off[mp.src[0].entity][g + 1] - b->row_off[mp.src[0].entity][g]);
+      const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
+      if (p->sum_window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
+          b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
+        const int se = mp.src[0].entity;
+        std::vector<int64_t> dstart(ND + 1, 0);
+        for (size_t k = 0; k < mdst.size(); ++k) dstart[mdst[k] + 1]++;
+        for (int64_t r = 0; r < ND; ++r) dstart[r + 1] += dstart[r];
+        std::vector<int32_t> rows_by(mdst.size());
+        {
+          std::vector<int64_t> fill(dstart.begin(), dstart.end() - 1);
+          for (size_t k = 0; k < mdst.size(); ++k) rows_by[fill[mdst[k]]++] = (int32_t)(mcode[k] & IGN_ROW_MASK);
+        }
+        for (int64_t r = 0; r < ND; ++r) std::sort(rows_by.begin() + dstart[r], rows_by.begin() + dstart[r + 1]);
+        std::vector<int64_t> wg;
+        std::vector<int32_t> wdst, wptr(1, 0), wsrc;
+        wdst.reserve(ND);
+        wsrc.reserve(mdst.size());
+        for (int g = 0; g < G; ++g) {
+          std::vector<int32_t> ds;
+          for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r) ds.push_back((int32_t)r);
+          std::stable_sort(ds.begin(), ds.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
+          for (size_t c0 = 0; c0 < ds.size(); c0 += 256) {
+            const size_t c1 = std::min(ds.size(), c0 + 256);
+            wg.push_back((int64_t)wdst.size());
+            wg.push_back((int64_t)(wdst.size() + (c1 - c0)));
+            wg.push_back(b->row_off[se][g]);
+            wg.push_back(b->row_off[se][g + 1]);
+            for (size_t q = c0; q < c1; ++q) {
+              const int32_t r = ds[q];
+              wdst.push_back(r);
+              wsrc.insert(wsrc.end(), rows_by.begin() + dstart[r], rows_by.begin() + dstart[r + 1]);
+              wptr.push_back((int32_t)wsrc.size());
+            }
+          }
+        }
+        std::vector<int32_t> id_ptr(ND + 1);
+        std::vector<uint32_t> id_src(ND);
+        for (int64_t i = 0; i <= ND; ++i) id_ptr[i] = (int32_t)i;
+        for (int64_t i = 0; i < ND; ++i) id_src[i] = (uint32_t)order[i];   // slot 0: the x table
+        mb.n_win_wg = (int64_t)wg.size() / 4;
+        if ((rc = dev_upload(b.get(), &mb.d_win_wg, wg)) || (rc = dev_upload(b.get(), &mb.d_win_dst, wdst)) ||
+            (rc = dev_upload(b.get(), &mb.d_win_ptr, wptr)) || (rc = dev_upload(b.get(), &mb.d_win_src, wsrc)) ||
+            (rc = dev_upload(b.get(), &mb.d_id_ptr, id_ptr)) || (rc = dev_upload(b.get(), &mb.d_id_src, id_src)) ||
+            (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
+          return rc;
+      }
       mb.n_msgs = (int64_t)msrc.size();
       if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
       if ((rc = dev_upload(b.get(), &mb.d_msg_ptr, ptr))) return rc;
@@ -1095,7 +1150,19 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       HIP_TRY(launch_attn_softmax(aa, st));
       tm.end();
     }
-    if (count > 0) {
+    if (count > 0 && mb.n_win_wg > 0 && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
+      // windowed aggregation, then the GRU step on x (one message per destination: x itself)
+      const float* srcs = sbases.base[0];
+      SumWinArgs wa{srcs, mb.d_win_wg, mb.d_win_dst, mb.d_win_ptr, mb.d_win_src, mb.d_xsum, mb.n_win_wg};
+      SrcBases xb{};
+      xb.base[0] = mb.d_xsum;
+      SumGruArgs a{hin, hout, xb, mb.d_order, mb.d_id_ptr, mb.d_id_src, p->d_packed + cp.pk_w,
+                   p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
+      tm.begin(K_SUM, mb.flops, mb.bytes);
+      HIP_TRY(launch_sum_win(wa, mp.din, st));
+      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
+      tm.end();
+    } else if (count > 0) {
       SumGruArgs a{hin, hout, sbases, mb.d_order + first, mb.d_msg_ptr + first, mb.d_msg_src,
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count,
                    p->xcd_remap || p->sum_order == 3};

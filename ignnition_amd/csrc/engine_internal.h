@@ -106,6 +106,16 @@ struct MPB {
   float* d_edge_params[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
   float* d_msg_in[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<float*> d_msg_layer[IGN_MAX_SLOTS];
+  // windowed sum (SumWinArgs; single-source sums over graph-local rows): the aggregation runs per
+  // (graph, destination chunk) from LDS windows, then the GRU step reads x through an identity CSR
+  int64_t n_win_wg = 0;
+  int64_t* d_win_wg = nullptr;
+  int32_t* d_win_dst = nullptr;
+  int32_t* d_win_ptr = nullptr;
+  int32_t* d_win_src = nullptr;
+  float* d_xsum = nullptr;
+  int32_t* d_id_ptr = nullptr;
+  uint32_t* d_id_src = nullptr;
   double flops = 0, bytes = 0;    // algorithmic, per launch
   // host copies of the index tables (the training path builds their transposes)
   std::vector<int32_t> h_order, h_len, h_step_ptr, h_msg_ptr, h_multi_ptr;
@@ -186,6 +196,7 @@ struct ign_plan {
                                   // (keeps id locality), 2 id order, 3 per-graph sort + XCD-aware
                                   // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
+  bool sum_window = true;         // windowed sum aggregation where eligible; IGN_SUM_WINDOW=0 disables
   // timing
   bool timing = false;
   uint32_t timing_kinds = ~0u;    // kernel kinds that get event pairs (ign_plan_set_timing_kinds)

@@ -92,6 +92,21 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
 hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H * H / 2 : 0; }
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
+
+// Windowed sum (AUX:254-262 for single-source sum MPs of graph-local batches): one workgroup per
+// (graph, destination chunk) stages the graph's source rows through LDS in windows with coalesced
+// loads, so each source row leaves HBM once per chunk instead of once per message; x[dst] = sum of
+// the destination's source rows (ascending source order) is written for the GRU step.
+struct SumWinArgs {
+  const float* src;        // source states [rows][DIN]
+  const int64_t* wg;       // [n_wg][4]: first / end window position, first / end source row
+  const int32_t* dst;      // [positions] destination row
+  const int32_t* ptr;      // [positions + 1] message range
+  const int32_t* srow;     // [messages] source rows, ascending per destination
+  float* xsum;             // [rows][DIN]
+  int64_t n_wg;
+};
+hipError_t launch_sum_win(const SumWinArgs& args, int din, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

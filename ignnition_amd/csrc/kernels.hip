@@ -787,7 +787,9 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
-// MODE 0 sum (AUX:261), 3 the same sum with the tile's message indices staged in LDS; 1 attention: messages weighted by their softmax coefficient (AUX:339-342);
+// MODE 0 sum (AUX:261); 3 the same sum with the tile's message indices staged in LDS (IGN_SUM_VARIANT=6,
+// measured slower: 0.157 vs 0.112 ms on 512 x synth50); 1 attention: messages weighted by their
+// softmax coefficient (AUX:339-342);
 // 2 convolution: x = act((sum_m h_src . K + h) / deg) (AUX:384-401; K.sum = sum.K, exact
 // reassociation).  Then one GRU step (AUX:764).
 constexpr int kIdxCap = 1024;   // MODE 3: staged message indices per wave
@@ -918,6 +920,56 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Windowed sum aggregation (see SumWinArgs).  1024 threads: wave w owns window positions
+// 16w .. 16w+15 of its chunk, lanes as in sum_gru (row j, quarter g).  Per window the block
+// copies source rows [wb, we) into LDS (coalesced f4 loads), then every lane adds the prefix of
+// its ascending source list that falls in the window (8 index loads in flight).
+template <int DIN, int WIN_ROWS>
+__global__ __launch_bounds__(1024) void sum_win_kernel(SumWinArgs a) {
+  constexpr int NC = DIN / 16, F4 = DIN / 4;
+  __shared__ f4 win[WIN_ROWS * F4];
+  const int64_t* w = a.wg + 4 * (int64_t)blockIdx.x;
+  const int64_t pos0 = w[0], pos1 = w[1], s0 = w[2], s1 = w[3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = pos0 + 16 * wave + j;
+  const bool valid = pos < pos1;
+  int32_t m = valid ? a.ptr[pos] : 0;
+  const int32_t m1 = valid ? a.ptr[pos + 1] : 0;
+  f4 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+  for (int64_t wb = s0; wb < s1; wb += WIN_ROWS) {
+    const int64_t we = wb + WIN_ROWS < s1 ? wb + WIN_ROWS : s1;
+    if (wb != s0) __syncthreads();   // the previous window is consumed
+    const f4* sv = reinterpret_cast<const f4*>(a.src) + wb * F4;
+    const int n = (int)(we - wb) * F4;
+    for (int i = threadIdx.x; i < n; i += 1024) win[i] = sv[i];
+    __syncthreads();
+    while (m < m1) {
+      int32_t r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = m + k < m1 ? a.srow[m + k] : 0x7FFFFFFF;
+      int k = 0;
+#pragma unroll
+      for (; k < 8; ++k) {
+        if (r[k] >= we) break;
+        const f4* row = win + (int64_t)(r[k] - wb) * F4 + g;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] += row[4 * c];
+      }
+      m += k;
+      if (k < 8) break;   // the window (or the list) ends inside this batch
+    }
+  }
+  if (valid) {
+    const int64_t d = a.dst[pos];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) st4(a.xsum + d * DIN + 16 * c + 4 * g, x[c]);
   }
 }
 
@@ -1913,6 +1965,16 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
   return hipGetLastError();
 }
 
+hipError_t launch_sum_win(const SumWinArgs& args, int din, hipStream_t st) {
+  if (args.n_wg == 0) return hipSuccess;
+  const dim3 grid((unsigned)args.n_wg), block(1024);
+  if (din == 32) hipLaunchKernelGGL((sum_win_kernel<32, 1200>), grid, block, 0, st, args);
+  else if (din == 16) hipLaunchKernelGGL((sum_win_kernel<16, 2400>), grid, block, 0, st, args);
+  else if (din == 64) hipLaunchKernelGGL((sum_win_kernel<64, 600>), grid, block, 0, st, args);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
   // one tile per wave: measured faster than a persistent grid for this latency-bound gather
@@ -1924,8 +1986,8 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
     if (mode == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 1>), grid, dim3(256), 0, st, args); \
     else if (mode == 2 && D == HH) hipLaunchKernelGGL((sum_gru_kernel<D, (D == HH ? HH : D), (D == HH ? 2 : 0)>), grid, dim3(256), 0, st, args); \
     else if (mode == 2) return hipErrorInvalidValue;                                       \
-    else if (variant == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args); \
-    else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 3>), grid, dim3(256), 0, st, args);    \
+    else if (variant == 6) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 3>), grid, dim3(256), 0, st, args); \
+    else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args);    \
     return hipGetLastError();                                                              \
   }
   if (din == 32 && h == 32 && mode == 0 && (variant == 4 || variant == 5)) {   // measured slower: diagnostics
