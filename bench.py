@@ -240,6 +240,16 @@ def main():
             cpu = cpu_baseline(sd, sdims, prm, sg * 16, args.cpu_seconds, "25k-node / 250k-edge synthetic graphs")
         else:
             cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
+    seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "4"))
+    ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "2"))
+    split = lambda v, six: ("split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
+                            % (6 if six else 9)) if v else "f32 MFMA"
+    contraction = {"ordered_update_hU": split(seq_v >= 4, seq_v == 4),
+                   "readout": split(ro_v in (2, 3, 4), ro_v != 3),
+                   "sum_update_and_projection": "f32 MFMA"}
+    if roof is not None:
+        roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,
+                                                                                              "sum_update_and_projection")]
     line = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
@@ -255,7 +265,7 @@ def main():
                    "parallelism": ("edge-cut over %d ranks, RCCL halo all-to-all per iteration (rank 0 halo rows: %d)"
                                    % (world, halo_rows)) if synthetic else
                                   "graph-sharded (%d ranks), no collective in the forward" % world,
-                   "batch_build_s": round(t_build, 3)},
+                   "batch_build_s": round(t_build, 3), "contraction": contraction},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

@@ -782,8 +782,11 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       if ((rc = dev_alloc(b.get(), &mb.d_table, tfloats))) return rc;
       HIP_TRY(hipMemset(mb.d_table, 0, (tfloats + 256) * sizeof(float)));   // zero row stays zero
       // per launch of the recurrence: h.U + gates per step; one projected row (3H floats) per step
+      // FLOPs executed (fp32-equivalent): h.U + gates per step (x.W is hoisted into project);
+      // bytes per SURVEY §8d, B_stage = E (4 + 4H) + 2 N_d 4H + 4 (N_d + 1): one message row and
+      // code per step, the state read and written once per destination
       mb.flops = (double)steps * (2.0 * H * 3 * H + 14.0 * H);
-      mb.bytes = (double)steps * (12.0 * H + 4) + (double)ND * (8.0 * H + 12);
+      mb.bytes = (double)steps * (4.0 * H + 4) + (double)ND * 8.0 * H + 4.0 * (ND + 1);
       b->gru_steps += steps * p->T;
     } else {
       if (p->sum_order == 0 || p->sum_order == 3) {   // 3: graph-major (+ XCD-aware tiles) for sum MPs only

@@ -196,7 +196,8 @@ struct ign_plan {
                                   // (keeps id locality), 2 id order, 3 per-graph sort + XCD-aware
                                   // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
-  bool sum_window = true;         // windowed sum aggregation where eligible; IGN_SUM_WINDOW=0 disables
+  bool sum_window = false;        // windowed sum aggregation where eligible (IGN_SUM_WINDOW=1): measured
+                                  // 0.120 vs 0.112 ms (RouteNet link update), 0.156 vs 0.206 (Q-size)
   // timing
   bool timing = false;
   uint32_t timing_kinds = ~0u;    // kernel kinds that get event pairs (ign_plan_set_timing_kinds)
