@@ -1,18 +1,23 @@
-"""Build libignmp.so in-tree with hipcc for gfx950 (``python -m ignnition_amd.build``)."""
+"""Build libignmp.so in-tree with hipcc for gfx950 (``python -m ignnition_amd.build``).
+
+Every source compiles to its own object (in parallel, under build/), then one link.  kernels_bf.hip
+(the split-bf16 kernels) is compiled with MFMA accumulators in VGPRs."""
 
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "libignmp.so")
-SOURCES = ["engine.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "kernels.hip", "train_kernels.hip",
-           "readout_kernels.hip"]
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-         "-Wno-unused-value"]
+SOURCES = ["engine.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "kernels.hip", "kernels_bf.hip",
+           "train_kernels.hip", "readout_kernels.hip"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
+EXTRA = {"kernels_bf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def needs_build() -> bool:
@@ -27,8 +32,21 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    os.makedirs(OBJ, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(OBJ, src + ".o")
+        cmd = [hipcc] + FLAGS + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), os.cpu_count() or 1, 8))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = OUT + ".tmp"
-    cmd = [hipcc] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp, "-lz", "-lpthread"]
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", tmp, "-lz", "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,417 @@
+// kernels_bf.hip — the split-bf16 kernels: fp32 contractions formed from exact
+// 3-piece bf16 splits on v_mfma_f32_16x16x32_bf16.  A separate translation unit so that it can be
+// compiled with -mllvm -amdgpu-mfma-vgpr-form (accumulators in VGPRs: the gate / activation VALU
+// reads them without v_accvgpr_read), which the f32-MFMA kernels of kernels.hip measured slower with.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include "kernels.h"
+
+#include "device_common.h"
+
+namespace {
+
+int64_t grid_for(int64_t n, int64_t per_block) { return (n + per_block - 1) / per_block; }
+
+// resident blocks per CU (occupancy API) x CUs, at most the work
+template <typename K>
+int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  const int64_t g = (int64_t)per_cu * cus;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, n_blocks_of_work));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Variants 4 / 5 of the ordered update: seq_gru2's recurrence with h.U on the bf16 matrix path,
+// fp32-exact (device_common.h, split-bf16).  U (pre-scaled as for pack_gru) is split once into
+// three bf16 pieces (pack_u_bf16); every step splits the wave's hidden state the same way and
+// forms the 9 (variant 5) or 6 (variant 4) piece products per gate tile with
+// v_mfma_f32_16x16x32_bf16, accumulated in fp32 from the bias.
+// Fragment layout of 16x16x32 (lane l, element j): A[m = l&15][k = 8(l>>4) + j],
+// B[k][n = l&15].  The k order is permuted, kperm(s, g, j) = 16 (2s + (j>>2)) + 4g + (j&3), so
+// the B fragment of k-step s is exactly registers (2s .. 2s+1) of the lane's accumulator tiles:
+// the state still never leaves the lane.
+__global__ void pack_u_bf16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out, int H) {
+  const int NT = H / 16, KS = H / 32;
+  const int64_t total = 9LL * NT * KS * 64 * 8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // ((piece * 3 + gate) * NT + tile) * KS + s
+    const int s = (int)(f % KS); f /= KS;
+    const int i = (int)(f % NT); f /= NT;
+    const int G = (int)(f % 3);
+    const int piece = (int)(f / 3);
+    const int k = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
+    const int col = G * H + 16 * i + (lane & 15);
+    const float sc = G == 2 ? IGN_2LOG2E : IGN_NLOG2E;   // as pack_gru
+    float p[3];
+    split3(sc * U[(int64_t)k * 3 * H + col], p[0], p[1], p[2]);
+    out[e] = (uint16_t)(__float_as_uint(p[piece]) >> 16);
+  }
+}
+
+template <int H, bool SAVE, int PASSES>
+__global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
+  constexpr int NT = H / 16, KS = H / 32;
+  constexpr int NF = 9 * NT * KS;            // fragments: 3 pieces x 3 gates x NT tiles x KS k-steps
+  static_assert(H == 32 || H == 64, "split-bf16 ordered update: 32 or 64 units");
+  __shared__ float sbias[4 * H];
+  __shared__ bf8 su[NF * 64];
+  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
+  {
+    const u4v* src = reinterpret_cast<const u4v*>(a.Ubf);
+    u4v* dst = reinterpret_cast<u4v*>(su);
+    for (int e = threadIdx.x; e < NF * 64; e += blockDim.x) dst[e] = src[e];
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const float* tab = a.table + 4 * g;
+  __syncthreads();
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int L = valid ? a.len[pos] : 0;
+    const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    int Lmax = L;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+    float* hsv = nullptr;
+    if constexpr (SAVE) {
+      hsv = a.hs_save + (valid ? (int64_t)a.step_ptr[pos] + pos : 0) * H + 4 * g;
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
+      }
+    }
+    uint32_t code = codes[0];
+    for (int t = 0; t < Lmax; ++t) {
+      f4 x[3][NT];
+      {
+        const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+        for (int G = 0; G < 3; ++G)
+#pragma unroll
+          for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+      }
+      const uint32_t next = codes[t + 1];
+      // B fragments: the three exact bf16 pieces of the state, k-step s = accumulator tiles 2s, 2s+1
+      bf8 hf[3][KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        u4v w0, w1, w2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e0 = 2 * q, e1 = 2 * q + 1;
+          float a0, a1, a2, b0, b1, b2;
+          split3(h[2 * s + (e0 >> 2)][e0 & 3], a0, a1, a2);
+          split3(h[2 * s + (e1 >> 2)][e1 & 3], b0, b1, b2);
+          w0[q] = pack_hi16(a0, b0);
+          w1[q] = pack_hi16(a1, b1);
+          w2[q] = pack_hi16(a2, b2);
+        }
+        hf[0][s] = __builtin_bit_cast(bf8, w0);
+        hf[1][s] = __builtin_bit_cast(bf8, w1);
+        hf[2][s] = __builtin_bit_cast(bf8, w2);
+      }
+      f4 acc[3][NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        acc[0][i] = f4{0, 0, 0, 0};
+        acc[1][i] = f4{0, 0, 0, 0};
+        acc[2][i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
+      }
+      // the fragment reads are loop-invariant: an opaque lane offset keeps the compiler from
+      // hoisting all of them out of the step loop into registers (occupancy)
+      int lofs = lane;
+      asm volatile("" : "+v"(lofs));
+      // piece products, grouped by U piece (each A fragment read once per step), small first:
+      // x9: U lo x {lo, mid, hi}, U mid x {lo, mid, hi}, U hi x {lo, mid, hi}
+      // x6: U lo x hi, U mid x {mid, hi}, U hi x {lo, mid, hi}
+#pragma unroll
+      for (int pu = 2; pu >= 0; --pu) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) {
+            bf8 w[3];
+#pragma unroll
+            for (int G = 0; G < 3; ++G) w[G] = su[(((pu * 3 + G) * NT + i) * KS + s) * 64 + lofs];
+#pragma unroll
+            for (int ph = 2; ph >= 0; --ph) {
+              if (PASSES == 6 && pu + ph > 2) continue;
+#pragma unroll
+              for (int G = 0; G < 3; ++G) acc[G][i] = MFMA_BF(w[G], hf[ph][s], acc[G][i]);
+            }
+          }
+        }
+      }
+      const bool act = t < L;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
+          const float z = sig2_(acc[0][i][r] + x[0][i][r]);
+          const float rr = sig2_(acc[1][i][r] + x[1][i][r]);
+          const float c = tanh2_(x[2][i][r] + rr * acc[2][i][r]);
+          const float hn = c + z * (h[i][r] - c);
+          h[i][r] = act ? hn : h[i][r];
+        }
+      }
+      if constexpr (SAVE) {
+        if (act && valid) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) st4(hsv + (int64_t)(t + 1) * H + 16 * i, h[i]);
+        }
+      }
+      code = next;
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
+    }
+  }  // tile loop
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused readout MLP on the bf16 matrix path, fp32-exact operands (device_common.h, split-bf16):
+// y = act2(act1(X W1 + b1) W2 + b2) . w3 + b3 with every contraction formed from exact 3-piece
+// bf16 splits of both operands (PASSES = 6 or 9 piece products, fp32 accumulation).
+// Weights: pack_dense_bf16 fragments (output tile u, k-step s, piece p), 1 KB each; a 16-unit
+// chunk of W2 is contiguous (24 KB), staged through LDS per workgroup, double-buffered.  W1 (DIN
+// = 32: 48 KB) stays in LDS for the block.  One wave = 16 rows: the layer-1 activations are
+// split once into 3 x 8 B fragments (96 VGPRs, accumulator layout = chained k order) and feed
+// all 16 chunks; layer 2 is contracted with w3 per chunk and never stored.
+__global__ void pack_dense_bf16_kernel(const float* __restrict__ W, uint16_t* __restrict__ out, int IN, int OUT,
+                                       int chained) {
+  const int KS = IN / 32;
+  const int64_t total = (int64_t)(OUT / 16) * KS * 3 * 512;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // (u * KS + s) * 3 + piece
+    const int piece = (int)(f % 3); f /= 3;
+    const int s = (int)(f % KS);
+    const int u = (int)(f / KS);
+    const int g = lane >> 4;
+    const int k = chained ? 16 * (2 * s + (j >> 2)) + 4 * g + (j & 3) : 32 * s + 8 * g + j;
+    float p[3];
+    split3(W[(int64_t)k * OUT + 16 * u + (lane & 15)], p[0], p[1], p[2]);
+    out[e] = (uint16_t)(__float_as_uint(p[piece]) >> 16);
+  }
+}
+
+// the three B fragments of 8 consecutive values v[0..7] (element j = v[j])
+__device__ __forceinline__ void split_frag(const float (&v)[8], bf8 (&f)[3]) {
+  u4v w0, w1, w2;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float a0, a1, a2, b0, b1, b2;
+    split3(v[2 * q], a0, a1, a2);
+    split3(v[2 * q + 1], b0, b1, b2);
+    w0[q] = pack_hi16(a0, b0);
+    w1[q] = pack_hi16(a1, b1);
+    w2[q] = pack_hi16(a2, b2);
+  }
+  f[0] = __builtin_bit_cast(bf8, w0);
+  f[1] = __builtin_bit_cast(bf8, w1);
+  f[2] = __builtin_bit_cast(bf8, w2);
+}
+
+// acc += sum over piece pairs (A piece pu, B piece ph) of A_pu . B_ph, small products first
+template <int PASSES>
+__device__ __forceinline__ f4 split_mfma(const bf8* __restrict__ afrag, int stride, const bf8 (&b)[3], f4 acc) {
+#pragma unroll
+  for (int pu = 2; pu >= 0; --pu) {
+    const bf8 w = afrag[pu * stride];
+#pragma unroll
+    for (int ph = 2; ph >= 0; --ph) {
+      if (PASSES == 6 && pu + ph > 2) continue;
+      acc = MFMA_BF(w, b[ph], acc);
+    }
+  }
+  return acc;
+}
+
+template <int DIN, int ACT, int WAVES, int PASSES, int CT>
+__global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, const bf8* __restrict__ W1f,
+                                                                 const bf8* __restrict__ W2f) {
+  constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
+  constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
+  constexpr int NTH = 64 * WAVES;
+  constexpr int CHF = CT * KS2 * 3 * 64;         // bf8 per W2 chunk of CT output tiles (24 KB each)
+  constexpr int NCH = U2 / CT;
+  constexpr bool W1_LDS = DIN == 32;
+  constexpr int W1F = W1_LDS ? U1 * KS1 * 3 * 64 : 1;
+  __shared__ bf8 sw2[2][CHF];
+  __shared__ bf8 sw1[W1F];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int j = lane & 15, g = lane >> 4;
+  const u4v* W2v = reinterpret_cast<const u4v*>(W2f);
+  if constexpr (W1_LDS) {
+    const u4v* W1v = reinterpret_cast<const u4v*>(W1f);
+    for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
+  }
+  for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
+  const int64_t r = ((int64_t)blockIdx.x * WAVES + wave) * 16 + j;
+  const bool ok = r < a.n_rows;
+  // layer-1 input fragments: lane (row j, group g) holds x[row][32s + 8g .. +8) (natural k order)
+  bf8 xf[KS1][3];
+  {
+    const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+      const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      split_frag(v, xf[s]);
+    }
+  }
+  __syncthreads();
+  // layer 1 -> activations in accumulator layout -> split once into the layer-2 B fragments
+  bf8 hf[KS2][3];
+#pragma unroll
+  for (int s2 = 0; s2 < KS2; ++s2) {
+    float v[8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int u = 2 * s2 + half;
+      f4 acc = ld4(a.b1 + 16 * u + 4 * g);
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) {
+        const bf8* af = W1_LDS ? sw1 + ((u * KS1 + s) * 3) * 64 + lane : W1f + ((u * KS1 + s) * 3) * 64 + lane;
+        acc = split_mfma<PASSES>(af, 64, xf[s], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[4 * half + q] = act_t<ACT>(acc[q]);
+    }
+    split_frag(v, hf[s2]);
+  }
+  float y = 0.f;
+#pragma unroll 1
+  for (int v = 0; v < NCH; ++v) {
+    const int cur = v & 1;
+    f4 b[CT], w3[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      b[c] = ld4(a.b2 + 16 * (CT * v + c) + 4 * g);
+      w3[c] = ld4(a.w3 + 16 * (CT * v + c) + 4 * g);
+    }
+    const int nv = (v + 1) % NCH;
+    constexpr int PER = (CHF + NTH - 1) / NTH;
+    u4v stage[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + NTH * k;
+      if (i < CHF) stage[k] = W2v[(int64_t)nv * CHF + i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // opaque lane offset: the LDS reads must not be hoisted out of the chunk loop (registers)
+    int lofs = lane;
+    asm volatile("" : "+v"(lofs));
+    f4 acc[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[c] = b[c];
+#pragma unroll
+    for (int s = 0; s < KS2; ++s)
+#pragma unroll
+      for (int c = 0; c < CT; ++c)
+        acc[c] = split_mfma<PASSES>(sw2[cur] + (c * KS2 + s) * 3 * 64 + lofs, 64, hf[s], acc[c]);
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y += w3[c][q] * act_t<ACT>(acc[c][q]);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + NTH * k;
+      if (i < CHF) reinterpret_cast<u4v*>(sw2[cur ^ 1])[i] = stage[k];
+    }
+    __syncthreads();
+  }
+  y += __shfl_xor(y, 16);
+  y += __shfl_xor(y, 32);
+  if (g == 0 && ok) {
+    const float b3 = a.b3 ? a.b3[0] : 0.f;
+    a.y[r] = act_apply(y + b3, a.act3);
+  }
+}
+
+hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  if (!args.Ubf || (h != 32 && h != 64)) return hipErrorInvalidValue;
+  const int64_t work = grid_for(args.n_dst, 64);
+#define SEQ_BF(HH, P)                                                                              \
+  {                                                                                                \
+    auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P> : seq_gru_bf_kernel<HH, false, P>;     \
+    hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);                \
+  }
+  if (h == 32 && passes == 6) SEQ_BF(32, 6)
+  else if (h == 32) SEQ_BF(32, 9)
+  else if (passes == 6) SEQ_BF(64, 6)
+  else SEQ_BF(64, 9)
+#undef SEQ_BF
+  return hipGetLastError();
+}
+
+template <int DIN, int WAVES, int PASSES, int CT>
+static hipError_t readout_bf_din(const Readout3Args& args, const void* W1f, const void* W2f, hipStream_t st) {
+  const dim3 grid((unsigned)((args.n_rows + 16 * WAVES - 1) / (16 * WAVES))), block(64 * WAVES);
+  const bf8* w1 = static_cast<const bf8*>(W1f);
+  const bf8* w2 = static_cast<const bf8*>(W2f);
+  switch (args.act1) {
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+  }
+  return hipGetLastError();
+}
+
+bool readout_bf_supported(int din, int n1, int n2, int act1, int act2) {
+  return (din == 32 || din == 64) && n1 == 256 && n2 == 256 && act1 == act2;
+}
+
+hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
+                             hipStream_t st) {
+  if (args.n_rows == 0) return hipSuccess;
+  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f) return hipErrorInvalidValue;
+  // 32-unit W2 chunks (two accumulators per wave, 8 barriers per tile); LDS 96 + 48 KB at DIN 32
+  // 16-unit chunks measured faster than 32-unit ones (1.10 vs 1.18 ms, 512 x synth50); passes < 0
+  // selects the 32-unit form (diagnostics)
+  if (din == 32) {
+    if (passes < 0) return readout_bf_din<32, 12, 6, 2>(args, W1f, W2f, st);
+    return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 12, 6, 1>(args, W1f, W2f, st);
+  }
+  return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
+}
+
+hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st) {
+  if (IN % 32 || OUT % 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_dense_bf16_kernel, dim3(128), dim3(256), 0, st, W, static_cast<uint16_t*>(out), IN, OUT,
+                     chained);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st) {
+  if (H != 32 && H != 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_u_bf16_kernel, dim3(64), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H);
+  return hipGetLastError();
+}
+
