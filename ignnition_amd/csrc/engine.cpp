@@ -172,7 +172,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(5, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(6, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);

@@ -89,7 +89,7 @@ hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, c
                             const uint32_t* rows, int W, const float* bias_row, hipStream_t st);
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st);
 // split-bf16 ordered update (kernels_bf.hip), passes 6 or 9
-hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStream_t st);
+hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int prefetch, hipStream_t st);
 // recurrent kernel -> split-bf16 A fragments for seq variants 4/5 (H = 32 or 64); floats used: 9 H^2 / 2
 hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H * H / 2 : 0; }

@@ -1593,8 +1593,8 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) 
 
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (variant >= 4 && (h == 32 || h == 64))   // split-bf16 h.U (kernels_bf.hip)
-    return launch_seq_gru_bf(args, h, variant == 4 ? 6 : 9, st);
+  if (variant >= 4 && (h == 32 || h == 64))   // split-bf16 h.U (kernels_bf.hip); 6: + row prefetch
+    return launch_seq_gru_bf(args, h, variant == 5 ? 9 : 6, variant == 6, st);
   if (variant == 3 && h >= 32) {   // pipelined (needs >= 2 unit tiles)
     const int64_t work = grid_for(args.n_dst, 64);
     if (h == 32) {

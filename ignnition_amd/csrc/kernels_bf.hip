@@ -62,7 +62,7 @@ __global__ void pack_u_bf16_kernel(const float* __restrict__ U, uint16_t* __rest
   }
 }
 
-template <int H, bool SAVE, int PASSES>
+template <int H, bool SAVE, int PASSES, bool PF>
 __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
   constexpr int NT = H / 16, KS = H / 32;
   constexpr int NF = 9 * NT * KS;            // fragments: 3 pieces x 3 gates x NT tiles x KS k-steps
@@ -102,16 +102,37 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
       }
     }
     uint32_t code = codes[0];
+    // PF: the projected row of step t+1 is loaded during step t, and its z / r parts seed the
+    // accumulators (x + h.U instead of h.U, then + x: 16 fewer adds per step)
+    f4 xn[3][NT];
+    if constexpr (PF) {
+      const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) xn[G][i] = ld4(p + G * H + 16 * i);
+      code = codes[1];
+    }
     for (int t = 0; t < Lmax; ++t) {
       f4 x[3][NT];
-      {
+      if constexpr (PF) {
+#pragma unroll
+        for (int G = 0; G < 3; ++G)
+#pragma unroll
+          for (int i = 0; i < NT; ++i) x[G][i] = xn[G][i];
+        const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+        for (int G = 0; G < 3; ++G)
+#pragma unroll
+          for (int i = 0; i < NT; ++i) xn[G][i] = ld4(p + G * H + 16 * i);
+      } else {
         const float* p = tab + (int64_t)code * (3 * H);
 #pragma unroll
         for (int G = 0; G < 3; ++G)
 #pragma unroll
           for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
       }
-      const uint32_t next = codes[t + 1];
+      const uint32_t next = codes[t + (PF ? 2 : 1)];
       // B fragments: the three exact bf16 pieces of the state, k-step s = accumulator tiles 2s, 2s+1
       bf8 hf[3][KS];
 #pragma unroll
@@ -134,8 +155,8 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
       f4 acc[3][NT];
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        acc[0][i] = f4{0, 0, 0, 0};
-        acc[1][i] = f4{0, 0, 0, 0};
+        acc[0][i] = PF ? x[0][i] : f4{0, 0, 0, 0};
+        acc[1][i] = PF ? x[1][i] : f4{0, 0, 0, 0};
         acc[2][i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
       }
       // the fragment reads are loop-invariant: an opaque lane offset keeps the compiler from
@@ -168,8 +189,8 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
-          const float z = sig2_(acc[0][i][r] + x[0][i][r]);
-          const float rr = sig2_(acc[1][i][r] + x[1][i][r]);
+          const float z = sig2_(PF ? acc[0][i][r] : acc[0][i][r] + x[0][i][r]);
+          const float rr = sig2_(PF ? acc[1][i][r] : acc[1][i][r] + x[1][i][r]);
           const float c = tanh2_(x[2][i][r] + rr * acc[2][i][r]);
           const float hn = c + z * (h[i][r] - c);
           h[i][r] = act ? hn : h[i][r];
@@ -352,19 +373,29 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
   }
 }
 
-hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
+hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int prefetch, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
   if (!args.Ubf || (h != 32 && h != 64)) return hipErrorInvalidValue;
   const int64_t work = grid_for(args.n_dst, 64);
 #define SEQ_BF(HH, P)                                                                              \
   {                                                                                                \
-    auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P> : seq_gru_bf_kernel<HH, false, P>;     \
+    auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P, PFX> : seq_gru_bf_kernel<HH, false, P, PFX>; \
     hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);                \
   }
-  if (h == 32 && passes == 6) SEQ_BF(32, 6)
-  else if (h == 32) SEQ_BF(32, 9)
-  else if (passes == 6) SEQ_BF(64, 6)
-  else SEQ_BF(64, 9)
+  if (h == 32 && passes == 6) {
+    if (prefetch) {
+      constexpr bool PFX = true;
+      SEQ_BF(32, 6)
+    } else {
+      constexpr bool PFX = false;
+      SEQ_BF(32, 6)
+    }
+  } else {
+    constexpr bool PFX = false;
+    if (h == 32) SEQ_BF(32, 9)
+    else if (passes == 6) SEQ_BF(64, 6)
+    else SEQ_BF(64, 9)
+  }
 #undef SEQ_BF
   return hipGetLastError();
 }
