@@ -270,7 +270,7 @@ __device__ __forceinline__ f4 split_mfma(const bf8* __restrict__ afrag, int stri
   return acc;
 }
 
-template <int DIN, int ACT, int WAVES, int PASSES, int CT>
+template <int DIN, int ACT, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32)>
 __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, const bf8* __restrict__ W1f,
                                                                  const bf8* __restrict__ W2f) {
   constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
   constexpr int NTH = 64 * WAVES;
   constexpr int CHF = CT * KS2 * 3 * 64;         // bf8 per W2 chunk of CT output tiles (24 KB each)
   constexpr int NCH = U2 / CT;
-  constexpr bool W1_LDS = DIN == 32;
+  constexpr bool W1_LDS = W1L;   // W1 pieces in LDS (DIN 32) or read from L2 per wave
   constexpr int W1F = W1_LDS ? U1 * KS1 * 3 * 64 : 1;
   __shared__ bf8 sw2[2][CHF];
   __shared__ bf8 sw1[W1F];
@@ -400,17 +400,17 @@ hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int pref
   return hipGetLastError();
 }
 
-template <int DIN, int WAVES, int PASSES, int CT>
+template <int DIN, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32)>
 static hipError_t readout_bf_din(const Readout3Args& args, const void* W1f, const void* W2f, hipStream_t st) {
   const dim3 grid((unsigned)((args.n_rows + 16 * WAVES - 1) / (16 * WAVES))), block(64 * WAVES);
   const bf8* w1 = static_cast<const bf8*>(W1f);
   const bf8* w2 = static_cast<const bf8*>(W2f);
   switch (args.act1) {
-    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
-    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
+    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
   }
   return hipGetLastError();
 }
@@ -427,7 +427,8 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   // 16-unit chunks measured faster than 32-unit ones (1.10 vs 1.18 ms, 512 x synth50); passes < 0
   // selects the 32-unit form (diagnostics)
   if (din == 32) {
-    if (passes < 0) return readout_bf_din<32, 12, 6, 2>(args, W1f, W2f, st);
+    if (passes == -6) return readout_bf_din<32, 12, 6, 2>(args, W1f, W2f, st);
+    if (passes == -7) return readout_bf_din<32, 4, 6, 1, false>(args, W1f, W2f, st);   // 3 blocks per CU
     return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 12, 6, 1>(args, W1f, W2f, st);
   }
   return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
