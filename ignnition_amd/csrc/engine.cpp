@@ -266,6 +266,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
           dp.out = s.msg_layers[l].units;
           dp.act = s.msg_layers[l].activation;
           dp.use_bias = s.msg_layers[l].use_bias;
+          dp.l2 = s.msg_layers[l].l2;   // kernel_regularizer: part of model.losses (AUX:833-834)
           if (dp.out <= 0) return fail(IGN_ERR_INVALID, "mp %d: message layer %d units", m, l);
           if (!act_ok(dp.act)) return fail(IGN_ERR_UNSUPPORTED, "mp %d: message layer activation %d", m, dp.act);
           nn.layers.push_back(dp);
@@ -1018,7 +1019,7 @@ struct Timer {
 };
 
 // message network of one source: per-edge [inputs...] then the Dense stack into d_msg_layer[s]
-int run_message_net(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
+int message_net_fwd(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
                     const float* dst_state, hipStream_t st) {
   MsgGatherArgs g{};
   g.out = mb.d_msg_in[s];
@@ -1098,7 +1099,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     if (nn.layers.empty()) continue;
     // the per-edge network reads halo rows: it must run after the exchange, not beside it
     if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split with a message network");
-    if ((rc = run_message_net(p, nn, mb, (int)s, sbases.base[s], hin, st))) return rc;
+    if ((rc = message_net_fwd(p, nn, mb, (int)s, sbases.base[s], hin, st))) return rc;
   }
   for (size_t s = 0; s < mp.src.size(); ++s)
     if (!mp.nn[s].layers.empty()) sbases.base[s] = mb.d_msg_layer[s].back();
@@ -1418,3 +1419,8 @@ int ign_stats(const ign_plan* p, ign_stats_t* out) {
 }
 
 }  // extern "C"
+
+int ign::run_message_net(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
+                         const float* dst_state, hipStream_t st) {
+  return message_net_fwd(p, nn, mb, s, src_state, dst_state, st);
+}

@@ -243,6 +243,10 @@ int set_device(int dev);
 int ensure_device(ign_plan* p);
 int dev_alloc(ign_batch* b, float** out, int64_t n);
 int repack(ign_plan* p);                      // fragments from d_params (set_params, optimizer)
+// message-creation network of MP source s (GM:440-475): per-edge inputs, then the Dense stack into
+// mb.d_msg_layer[s] (the last layer's rows are the messages)
+int run_message_net(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
+                    const float* dst_state, hipStream_t st);
 // readout.cpp: the readout program (operations before predict, GM:611-655)
 int readout_plan(ign_plan* p, const ign_plan_desc* d);          // parse + row spaces + widths
 int64_t readout_layout(ign_plan* p, int64_t off);              // raw parameter tensors (kinds 11/12)

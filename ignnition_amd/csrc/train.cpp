@@ -31,7 +31,13 @@ struct MPTrain {
   std::vector<float*> xs;     // sum MPs: per iteration [rows][DIN]
   int64_t hs_rows = 0;
   std::vector<int32_t*> tptr, tidx;   // per source slot: source row -> steps (sorted) / dst rows (sum)
-  std::vector<int64_t> trows;
+  std::vector<int64_t> trows;         // (a source with a message network: its rows are the edges)
+  // message networks, per source slot: state row -> its edges (ascending), for the hs_source /
+  // hs_dest columns of the network's input gradient
+  int32_t* nsrc_ptr[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  int32_t* nsrc_idx[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  int32_t* ndst_ptr[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  int32_t* ndst_idx[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 struct MPRec {
@@ -54,6 +60,9 @@ struct TrainState {
   float* part = nullptr;
   float* ro_x = nullptr;                  // concatenated readout input (several input entities)
   float* dro = nullptr;
+  float* dmsg = nullptr;                  // message networks: d(messages) [edges][out]
+  float* mz[2] = {nullptr, nullptr};      // ... layer gradients (ping-pong) [edges][widest]
+  float* mdin = nullptr;                  // ... d(network input) [edges][din]
   bool forward_done = false;
   std::vector<void*> allocs;
 };
@@ -120,6 +129,47 @@ int build_table(ign_plan* p, const MPP& mp, const MPB& mb, const CellP& cp, cons
   return IGN_OK;
 }
 
+// Backward of MP source s's message-creation network (GM:440-475), given d(messages) in t->dmsg:
+// Dense stack in reverse (weight / bias gradients, l2 terms), then the hs_source / hs_dest column
+// slices of d(input) gathered back to the state rows they were read from.  The layer activations
+// are the ones run_message_net left in mb (recomputed for this MP instance by the caller).
+int msg_net_backward(ign_plan* p, ign_batch* b, TrainState* t, const MPP& mp, const MPB& mb, const MPTrain& mt,
+                     int s, float* dsrc, float* ddst, float* grads, hipStream_t st) {
+  const MsgNN& nn = mp.nn[s];
+  const int64_t ne = mb.n_edges[s];
+  const int L = (int)nn.layers.size();
+  int zi = 0;
+  HIP_TRY(launch_act_bwd(t->dmsg, mb.d_msg_layer[s][L - 1], ne * nn.layers[L - 1].out, nn.layers[L - 1].act,
+                         t->mz[0], st));
+  for (int l = L - 1; l >= 0; --l) {
+    const DenseP& d = nn.layers[l];
+    const int K = l == 0 ? nn.din : nn.layers[l - 1].out;
+    const float* A = l == 0 ? mb.d_msg_in[s] : mb.d_msg_layer[s][l - 1];
+    const int lda = l == 0 ? nn.din_pad : nn.layers[l - 1].out;
+    HIP_TRY(launch_tsgemm_add(A, lda, t->mz[zi], d.out, ne, K, d.out, t->part, grads + d.off_w,
+                              d.use_bias ? grads + d.off_b : nullptr, st));
+    if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)K * d.out, st));
+    if (l > 0)
+      HIP_TRY(launch_row_gemm_t_generic(t->mz[zi], ne, d.out, p->d_params + d.off_w, K, t->mz[1 - zi], 0,
+                                        nn.layers[l - 1].act, mb.d_msg_layer[s][l - 1], st));
+    else
+      HIP_TRY(launch_row_gemm_t_generic(t->mz[zi], ne, d.out, p->d_params + d.off_w, K, t->mdin, 0, -1, nullptr, st));
+    zi = 1 - zi;
+  }
+  int col = 0;
+  for (size_t q = 0; q < nn.inputs.size(); ++q) {
+    const int w = nn.widths[q];
+    if (nn.inputs[q] == IGN_MSG_HS_SOURCE)
+      HIP_TRY(launch_csr_gather_cols_add(dsrc, b->rows[mp.src[s].entity], mt.nsrc_ptr[s], mt.nsrc_idx[s], t->mdin,
+                                         nn.din, col, w, 1, st));
+    else if (nn.inputs[q] == IGN_MSG_HS_DEST)
+      HIP_TRY(launch_csr_gather_cols_add(ddst, b->rows[mp.dst], mt.ndst_ptr[s], mt.ndst_idx[s], t->mdin, nn.din,
+                                         col, w, 1, st));
+    col += w;   // edge_params: input data, no gradient
+  }
+  return IGN_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -137,8 +187,6 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   for (auto& mp : p->mps) {
     if (mp.aggr == IGN_AGGR_ATTENTION || mp.aggr == IGN_AGGR_CONVOLUTION || mp.feature_concat)
       return fail(IGN_ERR_UNSUPPORTED, "no backward for attention / convolution / axis-2 concat aggregations yet");
-    for (auto& nn : mp.nn)
-      if (!nn.layers.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for message networks yet");
   }
   for (auto& cp : p->cells)
     if (cp.used && cp.pk_wt < 0)
@@ -163,7 +211,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       t->dS[k].push_back(f);
     }
   }
-  int64_t ga_n = 0, gu_n = 0, dx_n = 0, dtab_n = 0, part_n = 0;
+  int64_t ga_n = 0, gu_n = 0, dx_n = 0, dtab_n = 0, part_n = 0, dmsg_n = 0, mz_n = 0, mdin_n = 0;
   auto need_part = [&](int64_t rows, int M, int N) {
     part_n = std::max(part_n, tsgemm_partial_floats(rows, M, N));
   };
@@ -226,18 +274,48 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     need_part(std::max<int64_t>(mb.n_steps, mb.n_dst), 1, 3 * H);   // colsum
     for (int s = 0; s < S; ++s) {
       const int se = mp.src[s].entity;
+      const MsgNN& nn = mp.nn[s];
+      const int64_t rows_s = nn.layers.empty() ? b->rows[se] : mb.n_edges[s];
       std::vector<int32_t> ptr, idx;
-      build_csr(b->rows[se], kv[s], ptr, idx);
+      build_csr(rows_s, kv[s], ptr, idx);
       int32_t *dp = nullptr, *di = nullptr;
       if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
       mt.tptr.push_back(dp);
       mt.tidx.push_back(di);
-      mt.trows.push_back(b->rows[se]);
+      mt.trows.push_back(rows_s);
+      if (nn.layers.empty()) continue;
+      // message network (GM:440-475): buffers for its backward, and the state row -> edge CSRs
+      const int64_t ne = mb.n_edges[s];
+      int widest = nn.din_pad;
+      for (size_t l = 0; l < nn.layers.size(); ++l) {
+        widest = std::max(widest, nn.layers[l].out);
+        need_part(ne, l == 0 ? nn.din : nn.layers[l].in, nn.layers[l].out);
+      }
+      dmsg_n = std::max(dmsg_n, ne * nn.dout());
+      mz_n = std::max(mz_n, ne * widest);
+      mdin_n = std::max(mdin_n, ne * nn.din);
+      std::vector<int32_t> es(ne), ed(ne);
+      HIP_TRY(hipMemcpy(es.data(), mb.d_edge_src[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(ed.data(), mb.d_edge_dst[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost));
+      std::vector<std::pair<int64_t, int32_t>> ks(ne), kd(ne);
+      for (int64_t e = 0; e < ne; ++e) {
+        ks[e] = {es[e], (int32_t)e};
+        kd[e] = {ed[e], (int32_t)e};
+      }
+      std::vector<int32_t> p1, i1, p2, i2;
+      build_csr(b->rows[se], ks, p1, i1);
+      build_csr(b->rows[mp.dst], kd, p2, i2);
+      if ((rc = tupload(t.get(), &mt.nsrc_ptr[s], p1)) || (rc = tupload(t.get(), &mt.nsrc_idx[s], i1)) ||
+          (rc = tupload(t.get(), &mt.ndst_ptr[s], p2)) || (rc = tupload(t.get(), &mt.ndst_idx[s], i2)))
+        return rc;
     }
     t->mp.push_back(std::move(mt));
   }
   if ((rc = talloc(t.get(), &t->ga, ga_n)) || (rc = talloc(t.get(), &t->gu, gu_n)) ||
       (rc = talloc(t.get(), &t->dx, dx_n)) || (rc = talloc(t.get(), &t->dtab, dtab_n)))
+    return rc;
+  if (dmsg_n && ((rc = talloc(t.get(), &t->dmsg, dmsg_n)) || (rc = talloc(t.get(), &t->mz[0], mz_n)) ||
+                 (rc = talloc(t.get(), &t->mz[1], mz_n)) || (rc = talloc(t.get(), &t->mdin, mdin_n))))
     return rc;
   // readout
   int64_t widest = p->ro_width;
@@ -288,6 +366,11 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
       }
       const float* hin = t->ver[mp.dst][rec.v_in];
       float* hout = t->ver[mp.dst][rec.v_in + 1];
+      for (size_t s = 0; s < mp.src.size(); ++s) {   // message-creation networks (GM:440-475)
+        if (mp.nn[s].layers.empty()) continue;
+        if ((rc = run_message_net(p, mp.nn[s], mb, (int)s, srcs[s], hin, st))) return rc;
+        srcs[s] = sb.base[s] = mb.d_msg_layer[s].back();
+      }
       if (mp.sorted) {
         if ((rc = build_table(p, mp, mb, cp, srcs))) return rc;
         SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
@@ -399,6 +482,15 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     float* dh_out = t->dS[1 - dcur[dst]][dst];
     const float* srcs[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
     for (size_t s = 0; s < mp.src.size(); ++s) srcs[s] = t->ver[mp.src[s].entity][rec.src_v[s]];
+    for (size_t s = 0; s < mp.src.size(); ++s) {   // recompute this instance's message networks
+      if (mp.nn[s].layers.empty()) continue;
+      if ((rc = run_message_net(p, mp.nn[s], mb, (int)s, srcs[s], t->ver[dst][rec.v_in], st))) return rc;
+      srcs[s] = mb.d_msg_layer[s].back();
+    }
+    auto src_grad = [&](size_t s) -> float* {      // where d(state of source s) accumulates
+      const int se = mp.src[s].entity;
+      return se == dst ? dh_out : t->dS[dcur[se]][se];
+    };
     float* gk = grads + cp.off_k;
     float* grk = grads + cp.off_rk;
     float* gb = grads + cp.off_b;
@@ -414,8 +506,11 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
         const int se = mp.src[s].entity;
         HIP_TRY(launch_csr_gather_add(t->dtab, mt.trows[s], mt.tptr[s], mt.tidx[s], t->ga, H3, 0, st));
         HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, nullptr, st));
-        float* target = se == dst ? dh_out : t->dS[dcur[se]][se];
-        HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, 1, -1, nullptr, st));
+        const bool net = !mp.nn[s].layers.empty();
+        float* target = net ? t->dmsg : se == dst ? dh_out : t->dS[dcur[se]][se];
+        HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, net ? 0 : 1, -1,
+                                  nullptr, st));
+        if (net && (rc = msg_net_backward(p, b, t, mp, mb, mt, (int)s, src_grad(s), dh_out, grads, st))) return rc;
       }
     } else {
       const float* hin = t->ver[dst][rec.v_in];
@@ -425,9 +520,10 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, gb, st));
       HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, gb + H3, st));
       for (size_t s = 0; s < mp.src.size(); ++s) {
-        const int se = mp.src[s].entity;
-        float* target = se == dst ? dh_out : t->dS[dcur[se]][se];
-        HIP_TRY(launch_csr_gather_add(target, mt.trows[s], mt.tptr[s], mt.tidx[s], t->dx, DIN, 1, st));
+        const bool net = !mp.nn[s].layers.empty();
+        float* target = net ? t->dmsg : src_grad(s);
+        HIP_TRY(launch_csr_gather_add(target, mt.trows[s], mt.tptr[s], mt.tidx[s], t->dx, DIN, net ? 0 : 1, st));
+        if (net && (rc = msg_net_backward(p, b, t, mp, mb, mt, (int)s, src_grad(s), dh_out, grads, st))) return rc;
       }
     }
     dcur[dst] = 1 - dcur[dst];
@@ -462,7 +558,13 @@ int ign_l2_loss(ign_plan* p, double* loss) {
   constexpr int NB = 64;
   if (!p->d_red) HIP_TRY(hipMalloc(&p->d_red, 1024 * sizeof(double)));
   double total = 0;
-  for (auto& d : p->dense) {
+  std::vector<const DenseP*> layers;   // readout and message-network Dense layers (model.losses)
+  for (auto& d : p->dense) layers.push_back(&d);
+  for (auto& mp : p->mps)
+    for (auto& nn : mp.nn)
+      for (auto& d : nn.layers) layers.push_back(&d);
+  for (const DenseP* dl : layers) {
+    const DenseP& d = *dl;
     if (d.l2 == 0.f) continue;
     HIP_TRY(launch_sumsq(p->d_params + d.off_w, (int64_t)d.in * d.out, p->d_red, NB, p->stream));
     double h[NB];

@@ -283,6 +283,21 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
   }
 }
 
+// out[r][c] (+)= sum over k in ptr[r] .. ptr[r+1] of in[idx[k]][col0 + c], c < width: a column slice
+// of a per-edge gradient gathered back to the rows it came from (any width / offset).
+__global__ void csr_gather_cols_add_kernel(float* __restrict__ out, int64_t n_rows, const int32_t* __restrict__ ptr,
+                                           const int32_t* __restrict__ idx, const float* __restrict__ in,
+                                           int in_stride, int col0, int width, int accumulate) {
+  const int64_t total = n_rows * width;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / width;
+    const int c = (int)(e - r * width);
+    float acc = accumulate ? out[e] : 0.f;
+    for (int k = ptr[r]; k < ptr[r + 1]; ++k) acc += in[(int64_t)idx[k] * in_stride + col0 + c];
+    out[e] = acc;
+  }
+}
+
 // out[r][m] (+)= sum_k in[r][k] Mat[m][k]; optional *= act'(aprev[r][m]).  One wave = 16 rows.
 template <int K, int M>
 __global__ __launch_bounds__(256) void row_gemm_t_kernel(const float* __restrict__ in, int64_t n,
@@ -621,6 +636,15 @@ hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t s
   SB_CASE(64, 64)
 #undef SB_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_csr_gather_cols_add(float* out, int64_t n_rows, const int32_t* ptr, const int32_t* idx,
+                                      const float* in, int in_stride, int col0, int width, int accumulate,
+                                      hipStream_t st) {
+  if (n_rows == 0 || width == 0) return hipSuccess;
+  hipLaunchKernelGGL(csr_gather_cols_add_kernel, dim3(blocks_for(n_rows * width)), dim3(256), 0, st, out, n_rows, ptr,
+                     idx, in, in_stride, col0, width, accumulate);
+  return hipGetLastError();
 }
 
 hipError_t launch_csr_gather_add(float* out, int64_t n_rows, const int32_t* ptr, const int32_t* idx, const float* in,

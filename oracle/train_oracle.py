@@ -103,6 +103,28 @@ class TorchOracle:
             dst_idx = torch.as_tensor(np.asarray(x["dst_" + adj], np.int64))
             seq = torch.as_tensor(np.asarray(x["seq_" + sname + "_" + dst], np.int64))
             msgs = state[sname][src_idx]                                  # GM:432
+            for k, op in enumerate(src.get("message", [])):                # GM:440-475
+                if op["type"] == "direct_assignation":
+                    continue
+                if op["type"] != "neural_network":
+                    raise OracleError("message operation %r not restated" % op["type"])
+                parts = []
+                for name in op["input"]:
+                    if name == "hs_source":
+                        parts.append(state[sname][src_idx])
+                    elif name == "hs_dest":
+                        parts.append(state[dst][dst_idx])                 # GM:433
+                    elif name == "edge_params":
+                        parts.append(torch.tensor(np.asarray(x["params_" + adj], np.float64).reshape(len(src_idx), -1),
+                                                  dtype=_T))
+                    else:
+                        raise OracleError("message input %r is not readable in the reference" % name)
+                h = torch.cat(parts, 1)
+                for layer, pre in self._msg_layers(sname, dst, op, k):
+                    b = self.p.get(pre + "/bias")
+                    h = h @ self.p[pre + "/kernel"] + (b if b is not None else 0)
+                    h = _act(h, layer.get("activation"))
+                msgs = h
             lens = torch.bincount(dst_idx, minlength=num_dst)[:num_dst]   # GM:481
             L = int(seq.max()) + 1
             s = torch.zeros((num_dst, L, msgs.shape[1]), dtype=_T).index_put((dst_idx, seq), msgs, accumulate=True)
@@ -150,6 +172,12 @@ class TorchOracle:
         pre = dst + "_update/"
         return self.p[pre + "kernel"], self.p[pre + "recurrent_kernel"], self.p[pre + "bias"]
 
+    def _msg_layers(self, sname, dst, op, k):
+        # one network name per source (the reference's counter counts sources, GM:251/281)
+        for li, layer in enumerate(self.nn[op["nn_name"]]["nn_architecture"]):
+            lname = layer.get("name", "layer_%d_%s_message_creation_%d" % (li, layer["type_layer"], k))
+            yield layer, "%s_to_%s_message_creation_0/%s" % (sname, dst, lname)
+
     def _layers(self, op):
         for li, layer in enumerate(self.nn[op["nn_name"]]["nn_architecture"]):
             name = layer.get("name", "layer_%d_%s_readout" % (li, layer["type_layer"]))
@@ -167,7 +195,19 @@ class TorchOracle:
 
     # ---------------------------------------------------------------- loss (GM:745-753)
     def regularization(self):
+        """sum(model.losses): kernel_regularizer of every Dense layer the model owns (AUX:833-834),
+        the readout's and the message-creation networks'."""
         total = torch.zeros((), dtype=_T)
+        for stage in self.d["message_passing"]["stages"]:
+            for mp in stage["stage_mp"]:
+                for src in mp["source_entities"]:
+                    for k, op in enumerate(src.get("message", [])):
+                        if op["type"] != "neural_network":
+                            continue
+                        for layer, pre in self._msg_layers(src["name"], mp["destination_entity"], op, k):
+                            if "kernel_regularizer" in layer:
+                                W = self.p[pre + "/kernel"]
+                                total = total + float(layer["kernel_regularizer"]) * (W * W).sum()
         for op in self.d["readout"]:
             if op["type"] != "predict":
                 continue

@@ -115,3 +115,41 @@ def test_training_reduces_loss():
         b.backward(dpred, grads)
         eng.adam_step(grads, m, v, it, 0.003)
     assert losses[-1] < 0.5 * losses[0]
+
+
+# ---------------------------------------------------------------------------------------------
+# message-creation networks (GM:440-475): gradients through the per-edge Dense stack
+def _msg_net_case(inputs, units, activation, ordered=False, l2=None):
+    from ignnition_amd.framework_operations import dimensions_of_sample
+    rng = np.random.default_rng(3)
+    if ordered:   # network on the link -> path (ordered) messages
+        desc = model_examples.routenet(iterations=3)
+        src = desc["message_passing"]["stages"][0]["stage_mp"][0]["source_entities"][0]
+        src["message"] = [{"type": "neural_network", "nn_name": "message_nn", "input": list(inputs)}]
+        desc["neural_networks"].append({"nn_name": "message_nn", "nn_type": "feed_forward", "nn_architecture": [
+            {"type_layer": "Dense", "units": u, "activation": activation} for u in units]})
+    else:
+        desc = model_examples.routenet_message_net(inputs=inputs, units=units, activation=activation, iterations=3)
+    if l2:
+        net = [n for n in desc["neural_networks"] if n["nn_name"] == "message_nn"][0]
+        net["nn_architecture"][0]["kernel_regularizer"] = l2
+    samples = [synthetic.routenet_sample("nsfnet", g) for g in range(2)]
+    if "edge_params" in inputs:
+        for s in samples:
+            s["adj_paths_links"] = {l: [[p, [float(rng.uniform(0, 1)), float(rng.uniform(-1, 1))]] for p in ps]
+                                    for l, ps in s["adj_paths_links"].items()}
+    dims = dimensions_of_sample(samples[0])
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, labels = workloads.graph_inputs(mi, samples)
+    prm = MPPlan.from_model_info(mi).init_params(6, bias_scale=0.1)
+    return desc, dims, graphs, labels, prm
+
+
+@pytest.mark.parametrize("inputs,units,act,ordered,l2", [
+    (("hs_source", "hs_dest"), (24, 32), "selu", False, 0.01),
+    (("hs_dest", "hs_source", "edge_params"), (32,), "tanh", False, None),
+    (("hs_source", "hs_dest"), (32,), "tanh", True, None),
+])
+def test_gradients_message_networks(inputs, units, act, ordered, l2):
+    desc, dims, graphs, labels, prm = _msg_net_case(inputs, units, act, ordered, l2)
+    _check(desc, dims, graphs, labels, prm)
