@@ -130,7 +130,8 @@ int build_table(ign_plan* p, const MPP& mp, const MPB& mb, const CellP& cp, cons
 }
 
 // Backward of MP source s's message-creation network (GM:440-475), given d(messages) in t->dmsg:
-// Dense stack in reverse (weight / bias gradients, l2 terms), then the hs_source / hs_dest column
+// Dense stack in reverse (weight / bias gradients; the l2 terms are added once per step by
+// ign_backward, not per MP instance), then the hs_source / hs_dest column
 // slices of d(input) gathered back to the state rows they were read from.  The layer activations
 // are the ones run_message_net left in mb (recomputed for this MP instance by the caller).
 int msg_net_backward(ign_plan* p, ign_batch* b, TrainState* t, const MPP& mp, const MPB& mb, const MPTrain& mt,
@@ -148,7 +149,6 @@ int msg_net_backward(ign_plan* p, ign_batch* b, TrainState* t, const MPP& mp, co
     const int lda = l == 0 ? nn.din_pad : nn.layers[l - 1].out;
     HIP_TRY(launch_tsgemm_add(A, lda, t->mz[zi], d.out, ne, K, d.out, t->part, grads + d.off_w,
                               d.use_bias ? grads + d.off_b : nullptr, st));
-    if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)K * d.out, st));
     if (l > 0)
       HIP_TRY(launch_row_gemm_t_generic(t->mz[zi], ne, d.out, p->d_params + d.off_w, K, t->mz[1 - zi], 0,
                                         nn.layers[l - 1].act, mb.d_msg_layer[s][l - 1], st));
@@ -528,6 +528,13 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     }
     dcur[dst] = 1 - dcur[dst];
   }
+  for (auto& mp : p->mps)   // message-network l2 terms (AUX:833-834), once per step
+    for (auto& nn : mp.nn)
+      for (size_t l = 0; l < nn.layers.size(); ++l) {
+        const DenseP& d = nn.layers[l];
+        const int K = l == 0 ? nn.din : nn.layers[l - 1].out;
+        if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)K * d.out, st));
+      }
   return IGN_OK;
 }
 
