@@ -790,8 +790,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.bytes = (double)steps * (4.0 * H + 4) + (double)ND * 8.0 * H + 4.0 * (ND + 1);
       b->gru_steps += steps * p->T;
     } else {
-      if (p->sum_order == 0 || p->sum_order == 3) {   // 3: graph-major (+ XCD-aware tiles) for sum MPs only
-        sort_order(order, flen, b->row_off[dst], p->graph_major || p->sum_order == 3);
+      if (p->sum_order == 0 || p->sum_order >= 3) {   // 3 / 4: graph-major for sum MPs (3: + XCD-aware tiles)
+        sort_order(order, flen, b->row_off[dst], p->graph_major || p->sum_order >= 3);
       } else if (p->sum_order == 1) {
         auto by_cnt = [&](int32_t x, int32_t y) { return flen[x] > flen[y]; };
         for (int64_t c = 0; c < ND; c += 256)
