@@ -49,6 +49,7 @@ struct SumGruArgs {
   const float* msg_w = nullptr;    // attention: per-message weight (CSR order), x = sum w_m h_src
   const float* conv_kp = nullptr;  // convolution: packed kernel; x = act((sum h_src . K + h) / deg)
   int conv_act = 0;
+  float* sum_save = nullptr;       // training, convolution: [rows][DIN] message sums before K
 };
 
 // Attention weights (AUX:287-343): per (graph, position) group of dense cells, the axis-0 softmax

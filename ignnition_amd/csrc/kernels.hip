@@ -739,6 +739,10 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
     for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
     if constexpr (MODE == 2) {
       static_assert(MODE != 2 || DIN == H, "convolution needs message dim == destination dim");
+      if (a.sum_save && valid) {   // training: the message sum before the convolution kernel
+#pragma unroll
+        for (int c = 0; c < NC; ++c) st4(a.sum_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+      }
       f4 y[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) y[c] = f4{0, 0, 0, 0};

@@ -29,6 +29,8 @@
 struct MPTrain {
   std::vector<float*> hs;     // sorted MPs: per iteration [(n_steps + n_dst)][H]
   std::vector<float*> xs;     // sum MPs: per iteration [rows][DIN]
+  std::vector<float*> ss;     // convolution MPs: per iteration, message sums before K [rows][DIN]
+  float* deg = nullptr;       // convolution MPs: messages per destination row (float)
   int64_t hs_rows = 0;
   std::vector<int32_t*> tptr, tidx;   // per source slot: source row -> steps (sorted) / dst rows (sum)
   std::vector<int64_t> trows;         // (a source with a message network: its rows are the edges)
@@ -185,8 +187,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
   if (!p->ro_ops.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for readout operations before predict yet");
   for (auto& mp : p->mps) {
-    if (mp.aggr == IGN_AGGR_ATTENTION || mp.aggr == IGN_AGGR_CONVOLUTION || mp.feature_concat)
-      return fail(IGN_ERR_UNSUPPORTED, "no backward for attention / convolution / axis-2 concat aggregations yet");
+    if (mp.aggr == IGN_AGGR_ATTENTION || mp.feature_concat)
+      return fail(IGN_ERR_UNSUPPORTED, "no backward for attention / axis-2 concat aggregations yet");
   }
   for (auto& cp : p->cells)
     if (cp.used && cp.pk_wt < 0)
@@ -260,6 +262,18 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         float* f = nullptr;
         if ((rc = talloc(t.get(), &f, mb.n_dst * DIN))) return rc;
         mt.xs.push_back(f);
+        if (mp.aggr == IGN_AGGR_CONVOLUTION) {
+          if ((rc = talloc(t.get(), &f, mb.n_dst * DIN))) return rc;
+          mt.ss.push_back(f);
+        }
+      }
+      if (mp.aggr == IGN_AGGR_CONVOLUTION) {
+        std::vector<float> deg(mb.n_dst, 0.f);
+        for (int64_t pos = 0; pos < mb.n_dst; ++pos)
+          deg[mb.h_order[pos]] = (float)(mb.h_msg_ptr[pos + 1] - mb.h_msg_ptr[pos]);
+        if ((rc = tupload(t.get(), &mt.deg, deg))) return rc;
+        dtab_n = std::max(dtab_n, 2 * mb.n_dst * DIN);   // du and d(sum) of the convolution
+        need_part(mb.n_dst, DIN, DIN);
       }
       for (int64_t pos = 0; pos < mb.n_dst; ++pos)
         for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) {
@@ -382,6 +396,11 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
         SumGruArgs a{hin, hout, sb, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, p->d_packed + cp.pk_w,
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         a.x_save = mt.xs[it];
+        if (mp.aggr == IGN_AGGR_CONVOLUTION) {   // AUX:384-401
+          a.conv_kp = p->d_packed + p->pk_conv;
+          a.conv_act = mp.act;
+          a.sum_save = mt.ss[it];
+        }
         HIP_TRY(launch_sum_gru(a, mp.din, cp.H, cp.H == 64 ? 3 : p->sum_variant, st));
       }
       t->cur[mp.dst] = rec.v_in + 1;
@@ -519,10 +538,20 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
       HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, gb, st));
       HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, gb + H3, st));
+      const float* dmsgs = t->dx;   // gradient of the aggregated messages, by destination row
+      if (mp.aggr == IGN_AGGR_CONVOLUTION) {
+        // x = act((s.K + h) / deg): du = dx act'(x) / deg, dh += du, dK += s^T du, ds = du K^T
+        float* du = t->dtab;
+        float* ds = t->dtab + mb.n_dst * DIN;
+        HIP_TRY(launch_conv_bwd(t->dx, mt.xs[rec.it], mt.deg, mb.n_dst, DIN, mp.act, du, dh_out, st));
+        HIP_TRY(launch_tsgemm_add(mt.ss[rec.it], DIN, du, DIN, mb.n_dst, DIN, DIN, t->part, grads + p->off_conv, nullptr, st));
+        HIP_TRY(launch_row_gemm_t_generic(du, mb.n_dst, DIN, p->d_params + p->off_conv, DIN, ds, 0, -1, nullptr, st));
+        dmsgs = ds;
+      }
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const bool net = !mp.nn[s].layers.empty();
         float* target = net ? t->dmsg : src_grad(s);
-        HIP_TRY(launch_csr_gather_add(target, mt.trows[s], mt.tptr[s], mt.tidx[s], t->dx, DIN, net ? 0 : 1, st));
+        HIP_TRY(launch_csr_gather_add(target, mt.trows[s], mt.tptr[s], mt.tidx[s], dmsgs, DIN, net ? 0 : 1, st));
         if (net && (rc = msg_net_backward(p, b, t, mp, mb, mt, (int)s, src_grad(s), dh_out, grads, st))) return rc;
       }
     }

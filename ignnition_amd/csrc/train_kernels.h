@@ -45,6 +45,9 @@ bool bwd_shape_supported(int din, int h);
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st);
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);
 // out[r][:cols] (+)= sum over k in [ptr[r], ptr[r+1]) of in[idx[k]][:cols]   (cols % 4 == 0)
+// convolution backward, elementwise: du = dx act'(x) / deg[row]; dh += du  ([n][F], rows by dst row)
+hipError_t launch_conv_bwd(const float* dx, const float* x, const float* deg, int64_t n, int F, int act, float* du,
+                           float* dh, hipStream_t st);
 // out[r][0:width] (+)= sum over the CSR list of r of in[idx][col0 : col0 + width] (row stride in_stride)
 hipError_t launch_csr_gather_cols_add(float* out, int64_t n_rows, const int32_t* ptr, const int32_t* idx,
                                       const float* in, int in_stride, int col0, int width, int accumulate,

@@ -283,6 +283,19 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
   }
 }
 
+// Convolution aggregation backward, elementwise part (AUX:384-401): x = act((s.K + h) / deg), so
+// du = dx act'(x) / deg (act' through the output x), and the destination's own state gets du.
+__global__ void conv_bwd_kernel(const float* __restrict__ dx, const float* __restrict__ x,
+                                const float* __restrict__ deg, int64_t n, int F, int act, float* __restrict__ du,
+                                float* __restrict__ dh) {
+  const int64_t total = n * F;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = dx[i] * act_grad(x[i], act) / deg[i / F];
+    du[i] = v;
+    dh[i] += v;
+  }
+}
+
 // out[r][c] (+)= sum over k in ptr[r] .. ptr[r+1] of in[idx[k]][col0 + c], c < width: a column slice
 // of a per-edge gradient gathered back to the rows it came from (any width / offset).
 __global__ void csr_gather_cols_add_kernel(float* __restrict__ out, int64_t n_rows, const int32_t* __restrict__ ptr,
@@ -636,6 +649,13 @@ hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t s
   SB_CASE(64, 64)
 #undef SB_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_conv_bwd(const float* dx, const float* x, const float* deg, int64_t n, int F, int act, float* du,
+                           float* dh, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(conv_bwd_kernel, dim3(blocks_for(n * F)), dim3(256), 0, st, dx, x, deg, n, F, act, du, dh);
+  return hipGetLastError();
 }
 
 hipError_t launch_csr_gather_cols_add(float* out, int64_t n_rows, const int32_t* ptr, const int32_t* idx,

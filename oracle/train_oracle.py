@@ -141,11 +141,19 @@ class TorchOracle:
             else:
                 if first:
                     src_input, final_len, first = s, lens, False
+                    comb_src, comb_dst = msgs, dst_idx                     # GM:528
                 else:
                     src_input = torch.cat([src_input, s], 1)
                     final_len = final_len + lens
+                    comb_src = torch.cat([comb_src, msgs], 0)              # GM:533-541
+                    comb_dst = torch.cat([comb_dst, dst_idx], 0)
         if aggr == "sum":
             src_input = src_input.sum(1)
+        elif aggr == "convolution":                                       # AUX:384-401
+            Kc = self.p["convolution/kernel"]
+            ns = torch.zeros((num_dst, Kc.shape[1]), dtype=_T).index_add(0, comb_dst, comb_src @ Kc)
+            deg = torch.bincount(comb_dst, minlength=num_dst)[:num_dst].to(_T)
+            src_input = _act((ns + state[dst]) / deg[:, None], mp["aggregation"].get("activation_function", "relu"))
         elif aggr == "interleave":
             t = src_input.transpose(0, 1)
             flat = indices.reshape(-1)
@@ -153,7 +161,7 @@ class TorchOracle:
             src_input = t.transpose(0, 1)
         cell = self._cell(dst)
         old = state[dst]
-        if aggr == "sum":
+        if aggr in ("sum", "convolution"):
             new = gru_cell(src_input, old, *cell)
         else:
             if bool((final_len == 0).any()):

@@ -153,3 +153,15 @@ def _msg_net_case(inputs, units, activation, ordered=False, l2=None):
 def test_gradients_message_networks(inputs, units, act, ordered, l2):
     desc, dims, graphs, labels, prm = _msg_net_case(inputs, units, act, ordered, l2)
     _check(desc, dims, graphs, labels, prm)
+
+
+@pytest.mark.parametrize("aggr", [{"type": "convolution"}, {"type": "convolution", "activation_function": "tanh"},
+                                  {"type": "convolution", "activation_function": "selu"}])
+def test_gradients_convolution(aggr):
+    """Convolution aggregation (AUX:384-401): x = act((sum_m h_src K + h) / deg) into the GRU."""
+    desc = model_examples.routenet_aggregation(aggr, hidden=32, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    _check(desc, dims, graphs, labels, prm)

@@ -54,6 +54,18 @@ def test_torch_forward_message_network_matches_dense_oracle(inputs):
     np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize("aggr", [{"type": "convolution"}, {"type": "convolution", "activation_function": "tanh"}])
+def test_torch_forward_convolution_matches_dense_oracle(aggr):
+    desc = model_examples.routenet_aggregation(aggr, hidden=32, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    got = TorchOracle(desc, dims, prm).forward(graphs).detach().numpy()
+    exp = DenseOracle(desc, dims, prm).forward(graphs)
+    np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
+
+
 def test_regularization_matches():
     desc, dims, graphs, labels, prm = _setup("routenet")
     reg = float(TorchOracle(desc, dims, prm).regularization().detach())
