@@ -114,10 +114,8 @@ int ign::repack(ign_plan* p) {
                             p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
                             p->stream));
     if (cp.pk_ubf >= 0) HIP_TRY(launch_pack_u_bf16(p->d_params + cp.off_rk, p->d_packed + cp.pk_ubf, cp.H, p->stream));
-    if (cp.pk_wt >= 0) {
-      HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
-      HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
-    }
+    if (cp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
+    if (cp.pk_ut >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
   }
   for (auto& mp : p->mps)
     if (mp.feature_concat) {
@@ -377,9 +375,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   // backward fragments (training): W^T / U^T per cell, W^T per Dense layer where the MFMA
   // row GEMM is instantiated
   for (auto& cp : p->cells) {
-    if (!cp.used || !bwd_shape_supported(cp.din, cp.H)) continue;
-    cp.pk_wt = pk; pk = align(pk + 3LL * cp.din * cp.H);
+    if (!cp.used || !bwd_shape_supported(cp.H, cp.H)) continue;   // U^T: the recurrent backward
     cp.pk_ut = pk; pk = align(pk + 3LL * cp.H * cp.H);
+    if (!bwd_shape_supported(cp.din, cp.H)) continue;            // W^T (an axis-2 concat cell goes generic)
+    cp.pk_wt = pk; pk = align(pk + 3LL * cp.din * cp.H);
   }
   for (auto& dp : p->dense) {
     if (!row_gemm_supported(dp.out, dp.in)) continue;

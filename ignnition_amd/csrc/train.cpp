@@ -121,10 +121,13 @@ int check_train(ign_plan* p, ign_batch* b) {
 // project every source of sorted MP mb into its table, from the given source states
 int build_table(ign_plan* p, const MPP& mp, const MPB& mb, const CellP& cp, const float* const* src) {
   const int W3 = 3 * cp.H;
-  for (size_t s = 0; s < mp.src.size(); ++s)
-    HIP_TRY(launch_project(src[s], mb.src_rows[s], p->d_packed + cp.pk_w, p->d_packed + cp.pk_b,
-                           mb.d_table + mb.src_off[s] * W3, s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr, mp.din,
-                           cp.H, p->stream));
+  for (size_t s = 0; s < mp.src.size(); ++s) {
+    // axis-2 concat (AUX:443-456): each source through its own row slice of the input kernel
+    const int sdin = mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : mp.din;
+    const float* wp = p->d_packed + (mp.feature_concat ? mp.pk_slice[s] : cp.pk_w);
+    HIP_TRY(launch_project(src[s], mb.src_rows[s], wp, p->d_packed + cp.pk_b, mb.d_table + mb.src_off[s] * W3,
+                           s == 0 ? mb.d_table + mb.zero_row * W3 : nullptr, sdin, cp.H, p->stream));
+  }
   if (mb.n_multi)
     HIP_TRY(launch_multi_sum(mb.d_table, mb.zero_row + 1, mb.n_multi, mb.d_multi_ptr, mb.d_multi_rows, W3,
                              mb.d_table + mb.zero_row * W3, p->stream));
@@ -187,12 +190,18 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
   if (!p->ro_ops.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for readout operations before predict yet");
   for (auto& mp : p->mps) {
-    if (mp.aggr == IGN_AGGR_ATTENTION || mp.feature_concat)
-      return fail(IGN_ERR_UNSUPPORTED, "no backward for attention / axis-2 concat aggregations yet");
+    if (mp.aggr == IGN_AGGR_ATTENTION)
+      return fail(IGN_ERR_UNSUPPORTED, "no backward for the attention aggregation yet");
   }
-  for (auto& cp : p->cells)
-    if (cp.used && cp.pk_wt < 0)
+  for (size_t c = 0; c < p->cells.size(); ++c) {
+    const CellP& cp = p->cells[c];
+    if (!cp.used) continue;
+    bool concat_only = true;   // W^T is not needed by a cell fed only by axis-2 concat MPs
+    for (auto& mp : p->mps)
+      if (mp.cell == (int)c && !mp.feature_concat) concat_only = false;
+    if (cp.pk_ut < 0 || (cp.pk_wt < 0 && !concat_only))
       return fail(IGN_ERR_UNSUPPORTED, "no backward kernel for GRU shape (input %d, units %d)", cp.din, cp.H);
+  }
   std::unique_ptr<TrainState, void (*)(TrainState*)> t(new TrainState(), train_state_destroy);
   const int64_t P = b->n_pred;
   // hidden-state versions: 1 + T x (MPs updating the entity)
@@ -255,7 +264,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       need_part(mt.hs_rows, H, 3 * H);
       for (int s = 0; s < S; ++s) {
         dtab_n = std::max(dtab_n, mb.src_rows[s] * 3 * H);
-        need_part(mb.src_rows[s], DIN, 3 * H);
+        need_part(mb.src_rows[s], mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : DIN, 3 * H);
       }
     } else {
       for (int it = 0; it < p->T; ++it) {
@@ -524,11 +533,19 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const int se = mp.src[s].entity;
         HIP_TRY(launch_csr_gather_add(t->dtab, mt.trows[s], mt.tptr[s], mt.tidx[s], t->ga, H3, 0, st));
-        HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, nullptr, st));
         const bool net = !mp.nn[s].layers.empty();
         float* target = net ? t->dmsg : se == dst ? dh_out : t->dS[dcur[se]][se];
-        HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, net ? 0 : 1, -1,
-                                  nullptr, st));
+        if (mp.feature_concat) {   // AUX:443-456: the source's slice of the input kernel
+          const int sdin = p->ents[se].hidden_dim;
+          const int64_t koff = (int64_t)mp.slice_off[s] * H3;
+          HIP_TRY(launch_tsgemm_add(srcs[s], sdin, t->dtab, H3, mt.trows[s], sdin, H3, t->part, gk + koff, nullptr, st));
+          HIP_TRY(launch_row_gemm_t_generic(t->dtab, mt.trows[s], H3, p->d_params + cp.off_k + koff, sdin, target,
+                                            net ? 0 : 1, -1, nullptr, st));
+        } else {
+          HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, nullptr, st));
+          HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, net ? 0 : 1, -1,
+                                    nullptr, st));
+        }
         if (net && (rc = msg_net_backward(p, b, t, mp, mb, mt, (int)s, src_grad(s), dh_out, grads, st))) return rc;
       }
     } else {

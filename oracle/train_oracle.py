@@ -136,8 +136,13 @@ class TorchOracle:
                     src_input = torch.cat([src_input, s], 1)
                     indices = torch.stack([indices, ind], 0)
                     final_len = final_len + lens
-            elif aggr == "concat" and int(mp["aggregation"]["concat_axis"]) != 1:
-                raise OracleError("concat on axis 2 not restated")
+            elif aggr == "concat" and int(mp["aggregation"]["concat_axis"]) != 1:   # GM:496-505
+                if first:
+                    src_input, final_len, first = s, lens, False            # the first source's lens
+                else:
+                    if s.shape[1] != src_input.shape[1]:
+                        raise OracleError("ConcatOp: sources with different Lmax")
+                    src_input = torch.cat([src_input, s], 2)
             else:
                 if first:
                     src_input, final_len, first = s, lens, False

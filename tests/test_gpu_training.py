@@ -165,3 +165,14 @@ def test_gradients_convolution(aggr):
     graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
     prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
     _check(desc, dims, graphs, labels, prm)
+
+
+@pytest.mark.parametrize("axis", [1, 2])
+def test_gradients_concat(axis):
+    """{link, node} -> path concatenated on axis 1 (slots) or 2 (features, AUX:443-456)."""
+    desc = model_examples.qsize_aggregation({"type": "concat", "concat_axis": axis}, iterations=3)
+    _, dims, _ = workloads.model("qsize")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    _check(desc, dims, graphs, labels, prm)

@@ -66,6 +66,17 @@ def test_torch_forward_convolution_matches_dense_oracle(aggr):
     np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
 
 
+def test_torch_forward_concat_axis2_matches_dense_oracle():
+    desc = model_examples.qsize_aggregation({"type": "concat", "concat_axis": 2}, iterations=3)
+    _, dims, _ = workloads.model("qsize")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    got = TorchOracle(desc, dims, prm).forward(graphs).detach().numpy()
+    exp = DenseOracle(desc, dims, prm).forward(graphs)
+    np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
+
+
 def test_regularization_matches():
     desc, dims, graphs, labels, prm = _setup("routenet")
     reg = float(TorchOracle(desc, dims, prm).regularization().detach())
