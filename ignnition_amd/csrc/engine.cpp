@@ -1137,20 +1137,8 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343: scores, then the axis-0 softmax weights
       // a softmax group spans interior and boundary destinations: no split
       if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split with attention");
-      const float* w12 = p->d_packed + p->pk_w12;
       tm.begin(K_OTHER, 0, 0);
-      for (size_t s = 0; s < mp.src.size(); ++s) {
-        const int se = mp.src[s].entity;
-        const int64_t rows_s = mp.nn[s].layers.empty() ? b->rows[se] + b->halo[se] : mb.n_edges[s];
-        HIP_TRY(launch_dense_fwd(sbases.base[s], rows_s, mp.din, mp.din, nullptr, w12, nullptr, 1, IGN_ACT_LINEAR,
-                                 mb.d_s_src[s], st));
-      }
-      HIP_TRY(launch_dense_fwd(hin, mb.n_dst, cp.H, cp.H, nullptr, w12 + p->attn_F, nullptr, 1, IGN_ACT_LINEAR,
-                               mb.d_s_dst, st));
-      AttnArgs aa{mb.d_group_ptr, mb.d_group_empty, mb.d_cell_dst, mb.d_cell_ptr, mb.d_cell_msgs, mb.d_msg_src,
-                  {mb.d_s_src[0], mb.d_s_src[1], mb.d_s_src[2], mb.d_s_src[3]}, mb.d_s_dst, mb.d_ecell, mb.d_msg_w,
-                  mb.n_groups};
-      HIP_TRY(launch_attn_softmax(aa, st));
+      if ((rc = attention_weights(p, b, mp, mb, sbases.base, hin, st))) return rc;
       tm.end();
     }
     if (count > 0 && mb.n_win_wg > 0 && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
@@ -1422,4 +1410,25 @@ int ign_stats(const ign_plan* p, ign_stats_t* out) {
 int ign::run_message_net(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
                          const float* dst_state, hipStream_t st) {
   return message_net_fwd(p, nn, mb, s, src_state, dst_state, st);
+}
+
+// Attention weights of one MP instance (AUX:287-343): per-row scores s_src = h_src (K1 a1),
+// s_dst = h_dst (K2 a2), then the axis-0 softmax over (graph, position) cells into mb.d_msg_w.
+int ign::attention_weights(ign_plan* p, ign_batch* b, const MPP& mp, const MPB& mb, const float* const* srcs,
+                           const float* hin, hipStream_t st) {
+  const CellP& cp = p->cells[mp.cell];
+  const float* w12 = p->d_packed + p->pk_w12;
+  for (size_t s = 0; s < mp.src.size(); ++s) {
+    const int se = mp.src[s].entity;
+    const int64_t rows_s = mp.nn[s].layers.empty() ? b->rows[se] + b->halo[se] : mb.n_edges[s];
+    HIP_TRY(launch_dense_fwd(srcs[s], rows_s, mp.din, mp.din, nullptr, w12, nullptr, 1, IGN_ACT_LINEAR, mb.d_s_src[s],
+                             st));
+  }
+  HIP_TRY(launch_dense_fwd(hin, mb.n_dst, cp.H, cp.H, nullptr, w12 + p->attn_F, nullptr, 1, IGN_ACT_LINEAR, mb.d_s_dst,
+                           st));
+  AttnArgs aa{mb.d_group_ptr, mb.d_group_empty, mb.d_cell_dst, mb.d_cell_ptr, mb.d_cell_msgs, mb.d_msg_src,
+              {mb.d_s_src[0], mb.d_s_src[1], mb.d_s_src[2], mb.d_s_src[3]}, mb.d_s_dst, mb.d_ecell, mb.d_msg_w,
+              mb.n_groups};
+  HIP_TRY(launch_attn_softmax(aa, st));
+  return IGN_OK;
 }

@@ -247,6 +247,9 @@ int repack(ign_plan* p);                      // fragments from d_params (set_pa
 // mb.d_msg_layer[s] (the last layer's rows are the messages)
 int run_message_net(ign_plan* p, const MsgNN& nn, const MPB& mb, int s, const float* src_state,
                     const float* dst_state, hipStream_t st);
+// attention weights of one MP instance (AUX:287-343) into mb.d_msg_w (scores in mb.d_s_src / d_s_dst)
+int attention_weights(ign_plan* p, ign_batch* b, const MPP& mp, const MPB& mb, const float* const* srcs,
+                      const float* hin, hipStream_t st);
 // readout.cpp: the readout program (operations before predict, GM:611-655)
 int readout_plan(ign_plan* p, const ign_plan_desc* d);          // parse + row spaces + widths
 int64_t readout_layout(ign_plan* p, int64_t off);              // raw parameter tensors (kinds 11/12)

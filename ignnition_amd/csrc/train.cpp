@@ -31,6 +31,8 @@ struct MPTrain {
   std::vector<float*> xs;     // sum MPs: per iteration [rows][DIN]
   std::vector<float*> ss;     // convolution MPs: per iteration, message sums before K [rows][DIN]
   float* deg = nullptr;       // convolution MPs: messages per destination row (float)
+  int32_t* amdst = nullptr;   // attention MPs: destination row of every CSR message
+  std::vector<int32_t*> asptr, asidx;   // attention MPs, per slot: source row -> CSR messages
   int64_t hs_rows = 0;
   std::vector<int32_t*> tptr, tidx;   // per source slot: source row -> steps (sorted) / dst rows (sum)
   std::vector<int64_t> trows;         // (a source with a message network: its rows are the edges)
@@ -65,6 +67,11 @@ struct TrainState {
   float* dmsg = nullptr;                  // message networks: d(messages) [edges][out]
   float* mz[2] = {nullptr, nullptr};      // ... layer gradients (ping-pong) [edges][widest]
   float* mdin = nullptr;                  // ... d(network input) [edges][din]
+  float* adw = nullptr;                   // attention: d(weight) and d(score input) per message,
+  float* adv = nullptr;                   //   d(score) per source / destination row, d(w1 | w2)
+  float* ads_src = nullptr;
+  float* ads_dst = nullptr;
+  float* adw12 = nullptr;
   bool forward_done = false;
   std::vector<void*> allocs;
 };
@@ -191,7 +198,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   if (!p->ro_ops.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for readout operations before predict yet");
   for (auto& mp : p->mps) {
     if (mp.aggr == IGN_AGGR_ATTENTION)
-      return fail(IGN_ERR_UNSUPPORTED, "no backward for the attention aggregation yet");
+      for (auto& nn : mp.nn)
+        if (!nn.layers.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for attention over message networks");
   }
   for (size_t c = 0; c < p->cells.size(); ++c) {
     const CellP& cp = p->cells[c];
@@ -223,6 +231,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     }
   }
   int64_t ga_n = 0, gu_n = 0, dx_n = 0, dtab_n = 0, part_n = 0, dmsg_n = 0, mz_n = 0, mdin_n = 0;
+  int64_t amsg_n = 0, arows_n = 0;
   auto need_part = [&](int64_t rows, int M, int N) {
     part_n = std::max(part_n, tsgemm_partial_floats(rows, M, N));
   };
@@ -275,6 +284,29 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
           if ((rc = talloc(t.get(), &f, mb.n_dst * DIN))) return rc;
           mt.ss.push_back(f);
         }
+      }
+      if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343: message -> destination row, row -> messages
+        std::vector<int32_t> mdst(mb.n_msgs);
+        for (int64_t pos = 0; pos < mb.n_dst; ++pos)
+          for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) mdst[m] = mb.h_order[pos];
+        if ((rc = tupload(t.get(), &mt.amdst, mdst))) return rc;
+        std::vector<std::vector<std::pair<int64_t, int32_t>>> am(S);
+        for (int64_t m = 0; m < mb.n_msgs; ++m)
+          am[mb.h_msg_src[m] >> IGN_SLOT_SHIFT].push_back({(int64_t)(mb.h_msg_src[m] & IGN_ROW_MASK), (int32_t)m});
+        for (int s = 0; s < S; ++s) {
+          const int64_t rows_s = b->rows[mp.src[s].entity];
+          std::vector<int32_t> ptr, idx;
+          build_csr(rows_s, am[s], ptr, idx);
+          int32_t *dp = nullptr, *di = nullptr;
+          if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
+          mt.asptr.push_back(dp);
+          mt.asidx.push_back(di);
+          arows_n = std::max(arows_n, rows_s);
+          need_part(rows_s, DIN, 1);
+        }
+        amsg_n = std::max(amsg_n, mb.n_msgs);
+        arows_n = std::max(arows_n, mb.n_dst);
+        need_part(mb.n_dst, H, 1);
       }
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
         std::vector<float> deg(mb.n_dst, 0.f);
@@ -336,6 +368,10 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   }
   if ((rc = talloc(t.get(), &t->ga, ga_n)) || (rc = talloc(t.get(), &t->gu, gu_n)) ||
       (rc = talloc(t.get(), &t->dx, dx_n)) || (rc = talloc(t.get(), &t->dtab, dtab_n)))
+    return rc;
+  if (amsg_n && ((rc = talloc(t.get(), &t->adw, amsg_n)) || (rc = talloc(t.get(), &t->adv, amsg_n)) ||
+                 (rc = talloc(t.get(), &t->ads_src, arows_n)) || (rc = talloc(t.get(), &t->ads_dst, arows_n)) ||
+                 (rc = talloc(t.get(), &t->adw12, 2 * p->attn_F))))
     return rc;
   if (dmsg_n && ((rc = talloc(t.get(), &t->dmsg, dmsg_n)) || (rc = talloc(t.get(), &t->mz[0], mz_n)) ||
                  (rc = talloc(t.get(), &t->mz[1], mz_n)) || (rc = talloc(t.get(), &t->mdin, mdin_n))))
@@ -405,6 +441,10 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
         SumGruArgs a{hin, hout, sb, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, p->d_packed + cp.pk_w,
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         a.x_save = mt.xs[it];
+        if (mp.aggr == IGN_AGGR_ATTENTION) {     // AUX:287-343
+          if ((rc = attention_weights(p, b, mp, mb, srcs, hin, st))) return rc;
+          a.msg_w = mb.d_msg_w;
+        }
         if (mp.aggr == IGN_AGGR_CONVOLUTION) {   // AUX:384-401
           a.conv_kp = p->d_packed + p->pk_conv;
           a.conv_act = mp.act;
@@ -555,6 +595,32 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
       HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, gb, st));
       HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, gb + H3, st));
+      if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343 (see train_kernels.hip)
+        if ((rc = attention_weights(p, b, mp, mb, srcs, hin, st))) return rc;   // this instance's weights
+        const int F = DIN;
+        SrcBases sb{};
+        for (size_t s = 0; s < mp.src.size(); ++s) sb.base[s] = srcs[s];
+        AttnArgs aa{mb.d_group_ptr, mb.d_group_empty, mb.d_cell_dst, mb.d_cell_ptr, mb.d_cell_msgs, mb.d_msg_src,
+                    {mb.d_s_src[0], mb.d_s_src[1], mb.d_s_src[2], mb.d_s_src[3]}, mb.d_s_dst, mb.d_ecell, mb.d_msg_w,
+                    mb.n_groups};
+        const float* w12 = p->d_packed + p->pk_w12;
+        HIP_TRY(hipMemsetAsync(t->adw12, 0, 2 * p->attn_F * sizeof(float), st));
+        HIP_TRY(launch_attn_bwd_parts(aa, t->dx, mt.amdst, sb, F, mb.n_msgs, t->adw, t->adv, st));
+        for (size_t s = 0; s < mp.src.size(); ++s) {
+          const int64_t rows_s = b->rows[mp.src[s].entity];
+          HIP_TRY(launch_attn_src_bwd(rows_s, mt.asptr[s], mt.asidx[s], mb.d_msg_w, t->adv, mt.amdst, t->dx, w12, F,
+                                      src_grad(s), t->ads_src, st));
+          HIP_TRY(launch_tsgemm_add(srcs[s], F, t->ads_src, 1, rows_s, F, 1, t->part, t->adw12, nullptr, st));
+        }
+        HIP_TRY(launch_attn_dst_bwd(mb.n_dst, mb.d_order, mb.d_msg_ptr, t->adv, w12 + p->attn_F, H, dh_out, t->ads_dst,
+                                    st));
+        HIP_TRY(launch_tsgemm_add(hin, H, t->ads_dst, 1, mb.n_dst, H, 1, t->part, t->adw12 + p->attn_F, nullptr, st));
+        HIP_TRY(launch_attn_param_bwd(t->adw12, p->d_params + p->off_k1, p->d_params + p->off_k2,
+                                      p->d_params + p->off_att, p->attn_F, grads + p->off_k1, grads + p->off_k2,
+                                      grads + p->off_att, st));
+        dcur[dst] = 1 - dcur[dst];
+        continue;
+      }
       const float* dmsgs = t->dx;   // gradient of the aggregated messages, by destination row
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
         // x = act((s.K + h) / deg): du = dx act'(x) / deg, dh += du, dK += s^T du, ds = du K^T

@@ -45,6 +45,17 @@ bool bwd_shape_supported(int din, int h);
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st);
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);
 // out[r][:cols] (+)= sum over k in [ptr[r], ptr[r+1]) of in[idx[k]][:cols]   (cols % 4 == 0)
+// attention backward (AUX:287-343; see train_kernels.hip): per-message dw / dv, then per source row
+// and per destination the state gradients and the score-vector gradients ds; then the weights
+hipError_t launch_attn_bwd_parts(const AttnArgs& a, const float* dx, const int32_t* mdst, SrcBases src, int F,
+                                  int64_t n_msgs, float* dw, float* dv, hipStream_t st);
+hipError_t launch_attn_src_bwd(int64_t rows, const int32_t* sptr, const int32_t* sidx, const float* msg_w,
+                               const float* dv, const int32_t* mdst, const float* dx, const float* w1, int F, float* dh,
+                               float* ds, hipStream_t st);
+hipError_t launch_attn_dst_bwd(int64_t n_pos, const int32_t* order, const int32_t* ptr, const float* dv, const float* w2,
+                               int F, float* dh, float* ds, hipStream_t st);
+hipError_t launch_attn_param_bwd(const float* dw12, const float* K1, const float* K2, const float* av, int F, float* dK1,
+                                 float* dK2, float* dav, hipStream_t st);
 // convolution backward, elementwise: du = dx act'(x) / deg[row]; dh += du  ([n][F], rows by dst row)
 hipError_t launch_conv_bwd(const float* dx, const float* x, const float* deg, int64_t n, int F, int act, float* du,
                            float* dh, hipStream_t st);

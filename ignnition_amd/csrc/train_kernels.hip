@@ -283,6 +283,116 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Attention aggregation backward (AUX:287-343).  Forward: v_m = s_src(src_m) + s_dst(d_m),
+// e_c = sum_{m in cell c} LeakyReLU_0.2(v_m), w = softmax over each (graph, position) group of
+// cells (empty cells count as 0), x_d = sum_m w_{c(m)} h_src(src_m).
+//   dw_m  = dx_d . h_src(src_m)                               attn_dcoef
+//   de_c  = w_c (sum_{m in c} dw_m - S_g), S_g = sum_c w_c dw_c  attn_softmax_bwd (one wave per group)
+//   dv_m  = de_c LeakyReLU'(v_m)
+//   dh_src += sum_m w_m dx_{d_m} + (sum_m dv_m) w1             attn_src_bwd (also ds_src per row)
+//   dh_dst += (sum_{m -> d} dv_m) w2                           attn_dst_bwd (also ds_dst per row)
+__device__ __forceinline__ const float* attn_row(const SrcBases& sb, uint32_t code, int F) {
+  return sb.base[code >> IGN_SLOT_SHIFT] + (int64_t)(code & IGN_ROW_MASK) * F;
+}
+
+__global__ void attn_dcoef_kernel(const float* __restrict__ dx, const int32_t* __restrict__ mdst,
+                                  const uint32_t* __restrict__ msg_src, SrcBases src, int F, int64_t n,
+                                  float* __restrict__ dw) {
+  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (int64_t)gridDim.x * blockDim.x) {
+    const float* h = attn_row(src, msg_src[m], F);
+    const float* g = dx + (int64_t)mdst[m] * F;
+    float s = 0.f;
+    for (int k = 0; k < F; ++k) s += g[k] * h[k];
+    dw[m] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(AttnArgs a, const float* __restrict__ dw,
+                                                               float* __restrict__ dv) {
+  const int lane = threadIdx.x & 63;
+  const int64_t grp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (grp >= a.n_groups) return;
+  const int c0 = a.group_ptr[grp], c1 = a.group_ptr[grp + 1];
+  float S = 0.f;
+  for (int c = c0 + lane; c < c1; c += 64) {
+    float dc = 0.f;
+    for (int q = a.cell_ptr[c]; q < a.cell_ptr[c + 1]; ++q) dc += dw[a.cell_msgs[q]];
+    S += a.msg_w[a.cell_msgs[a.cell_ptr[c]]] * dc;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) S += __shfl_xor(S, o);
+  for (int c = c0 + lane; c < c1; c += 64) {
+    float dc = 0.f;
+    for (int q = a.cell_ptr[c]; q < a.cell_ptr[c + 1]; ++q) dc += dw[a.cell_msgs[q]];
+    const float de = a.msg_w[a.cell_msgs[a.cell_ptr[c]]] * (dc - S);
+    const float sd = a.s_dst[a.cell_dst[c]];
+    for (int q = a.cell_ptr[c]; q < a.cell_ptr[c + 1]; ++q) {
+      const int m = a.cell_msgs[q];
+      const uint32_t code = a.msg_src[m];
+      const float v = a.s_src[code >> IGN_SLOT_SHIFT][code & IGN_ROW_MASK] + sd;
+      dv[m] = v > 0.f ? de : 0.2f * de;
+    }
+  }
+}
+
+// one thread per (source row, column): rows of one source slot; sptr / sidx: row -> CSR messages
+__global__ void attn_src_bwd_kernel(int64_t rows, const int32_t* __restrict__ sptr, const int32_t* __restrict__ sidx,
+                                    const float* __restrict__ msg_w, const float* __restrict__ dv,
+                                    const int32_t* __restrict__ mdst, const float* __restrict__ dx,
+                                    const float* __restrict__ w1, int F, float* __restrict__ dh,
+                                    float* __restrict__ ds) {
+  const int64_t total = rows * F;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / F;
+    const int c = (int)(e - r * F);
+    float acc = 0.f, sv = 0.f;
+    for (int k = sptr[r]; k < sptr[r + 1]; ++k) {
+      const int m = sidx[k];
+      acc += msg_w[m] * dx[(int64_t)mdst[m] * F + c];
+      sv += dv[m];
+    }
+    dh[e] += acc + sv * w1[c];
+    if (c == 0) ds[r] = sv;
+  }
+}
+
+// one thread per (order position, column): the destination's messages are CSR range ptr[pos] ..
+__global__ void attn_dst_bwd_kernel(int64_t n_pos, const int32_t* __restrict__ order, const int32_t* __restrict__ ptr,
+                                    const float* __restrict__ dv, const float* __restrict__ w2, int F,
+                                    float* __restrict__ dh, float* __restrict__ ds) {
+  const int64_t total = n_pos * F;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pos = e / F;
+    const int c = (int)(e - pos * F);
+    float sv = 0.f;
+    for (int m = ptr[pos]; m < ptr[pos + 1]; ++m) sv += dv[m];
+    const int64_t d = order[pos];
+    dh[d * F + c] += sv * w2[c];
+    if (c == 0) ds[d] = sv;
+  }
+}
+
+// w1 = K1 a1, w2 = K2 a2 (attn_vectors): dK1 += dw1 a1^T, da1 += K1^T dw1 (same for K2, a2)
+__global__ void attn_param_bwd_kernel(const float* __restrict__ dw12, const float* __restrict__ K1,
+                                      const float* __restrict__ K2, const float* __restrict__ av, int F,
+                                      float* __restrict__ dK1, float* __restrict__ dK2, float* __restrict__ dav) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 2 * F * F) {
+    const int which = i / (F * F), r = (i % (F * F)) / F, c = i % F;
+    if (which == 0) dK1[r * F + c] += dw12[r] * av[c];
+    else dK2[r * F + c] += dw12[F + r] * av[F + c];
+  }
+  if (i < 2 * F) {
+    const int which = i / F, c = i % F;
+    const float* K = which ? K2 : K1;
+    const float* d = dw12 + which * F;
+    float s = 0.f;
+    for (int r = 0; r < F; ++r) s += K[r * F + c] * d[r];
+    dav[which * F + c] += s;
+  }
+}
+
 // Convolution aggregation backward, elementwise part (AUX:384-401): x = act((s.K + h) / deg), so
 // du = dx act'(x) / deg (act' through the output x), and the destination's own state gets du.
 __global__ void conv_bwd_kernel(const float* __restrict__ dx, const float* __restrict__ x,
@@ -649,6 +759,39 @@ hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t s
   SB_CASE(64, 64)
 #undef SB_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_attn_bwd_parts(const AttnArgs& a, const float* dx, const int32_t* mdst, SrcBases src, int F,
+                                  int64_t n_msgs, float* dw, float* dv, hipStream_t st) {
+  if (n_msgs == 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_dcoef_kernel, dim3(blocks_for(n_msgs)), dim3(256), 0, st, dx, mdst, a.msg_src, src, F, n_msgs, dw);
+  if (a.n_groups)
+    hipLaunchKernelGGL(attn_softmax_bwd_kernel, dim3((unsigned)((a.n_groups + 3) / 4)), dim3(256), 0, st, a, dw, dv);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_src_bwd(int64_t rows, const int32_t* sptr, const int32_t* sidx, const float* msg_w,
+                               const float* dv, const int32_t* mdst, const float* dx, const float* w1, int F, float* dh,
+                               float* ds, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_src_bwd_kernel, dim3(blocks_for(rows * F)), dim3(256), 0, st, rows, sptr, sidx, msg_w, dv, mdst,
+                     dx, w1, F, dh, ds);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_dst_bwd(int64_t n_pos, const int32_t* order, const int32_t* ptr, const float* dv, const float* w2,
+                               int F, float* dh, float* ds, hipStream_t st) {
+  if (n_pos == 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_dst_bwd_kernel, dim3(blocks_for(n_pos * F)), dim3(256), 0, st, n_pos, order, ptr, dv, w2, F,
+                     dh, ds);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_param_bwd(const float* dw12, const float* K1, const float* K2, const float* av, int F, float* dK1,
+                                 float* dK2, float* dav, hipStream_t st) {
+  hipLaunchKernelGGL(attn_param_bwd_kernel, dim3((2 * F * F + 255) / 256), dim3(256), 0, st, dw12, K1, K2, av, F, dK1,
+                     dK2, dav);
+  return hipGetLastError();
 }
 
 hipError_t launch_conv_bwd(const float* dx, const float* x, const float* deg, int64_t n, int F, int act, float* du,

@@ -146,14 +146,25 @@ class TorchOracle:
             else:
                 if first:
                     src_input, final_len, first = s, lens, False
-                    comb_src, comb_dst = msgs, dst_idx                     # GM:528
+                    comb_src, comb_dst, comb_seq = msgs, dst_idx, seq      # GM:528
                 else:
                     src_input = torch.cat([src_input, s], 1)
                     final_len = final_len + lens
                     comb_src = torch.cat([comb_src, msgs], 0)              # GM:533-541
                     comb_dst = torch.cat([comb_dst, dst_idx], 0)
+                    comb_seq = torch.cat([comb_seq, seq + lens[dst_idx]], 0)   # quirk: own lens (GM:539-540)
         if aggr == "sum":
             src_input = src_input.sum(1)
+        elif aggr == "attention":                                         # AUX:287-343
+            K1, K2, A = self.p["attention/kernel1"], self.p["attention/kernel2"], self.p["attention/attn_kernel"]
+            ai = torch.cat([comb_src @ K1, state[dst][comb_dst] @ K2], 1) @ A
+            ai = torch.where(ai > 0, ai, 0.2 * ai)                         # LeakyReLU(alpha=0.2)
+            max_len = int(comb_seq.max()) + 1
+            aux = torch.zeros((num_dst, max_len, 1), dtype=_T).index_put((comb_dst, comb_seq), ai, accumulate=True)
+            aux = aux - aux.max(0, keepdim=True).values                    # softmax over axis 0 (AUX:336)
+            coef = torch.exp(aux) / torch.exp(aux).sum(0, keepdim=True)
+            fc = coef[comb_dst, comb_seq]
+            src_input = torch.zeros((num_dst, comb_src.shape[1]), dtype=_T).index_add(0, comb_dst, comb_src * fc)
         elif aggr == "convolution":                                       # AUX:384-401
             Kc = self.p["convolution/kernel"]
             ns = torch.zeros((num_dst, Kc.shape[1]), dtype=_T).index_add(0, comb_dst, comb_src @ Kc)
@@ -166,7 +177,7 @@ class TorchOracle:
             src_input = t.transpose(0, 1)
         cell = self._cell(dst)
         old = state[dst]
-        if aggr in ("sum", "convolution"):
+        if aggr in ("sum", "attention", "convolution"):
             new = gru_cell(src_input, old, *cell)
         else:
             if bool((final_len == 0).any()):

@@ -176,3 +176,24 @@ def test_gradients_concat(axis):
     graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
     prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
     _check(desc, dims, graphs, labels, prm)
+
+
+def test_gradients_attention_routenet():
+    """Attention aggregation (AUX:287-343): scores, the axis-0 softmax over (graph, position)
+    cells, the weighted sum, into the GRU; gradients reach K1, K2 and the attention vector."""
+    desc = model_examples.routenet_aggregation({"type": "attention"}, hidden=32, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    _check(desc, dims, graphs, labels, prm)
+
+
+def test_gradients_attention_two_sources():
+    """{link, node} -> path attention: the combined edge list and the position quirk (GM:539-541)."""
+    desc = model_examples.qsize_aggregation({"type": "attention"}, iterations=3)
+    _, dims, _ = workloads.model("qsize")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    _check(desc, dims, graphs, labels, prm)

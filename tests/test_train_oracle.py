@@ -54,7 +54,8 @@ def test_torch_forward_message_network_matches_dense_oracle(inputs):
     np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
 
 
-@pytest.mark.parametrize("aggr", [{"type": "convolution"}, {"type": "convolution", "activation_function": "tanh"}])
+@pytest.mark.parametrize("aggr", [{"type": "convolution"}, {"type": "convolution", "activation_function": "tanh"},
+                                  {"type": "attention"}])
 def test_torch_forward_convolution_matches_dense_oracle(aggr):
     desc = model_examples.routenet_aggregation(aggr, hidden=32, iterations=3)
     _, dims, _ = workloads.model("routenet")
@@ -66,8 +67,9 @@ def test_torch_forward_convolution_matches_dense_oracle(aggr):
     np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
 
 
-def test_torch_forward_concat_axis2_matches_dense_oracle():
-    desc = model_examples.qsize_aggregation({"type": "concat", "concat_axis": 2}, iterations=3)
+@pytest.mark.parametrize("aggr", [{"type": "concat", "concat_axis": 2}, {"type": "attention"}])
+def test_torch_forward_qsize_aggregations_match_dense_oracle(aggr):
+    desc = model_examples.qsize_aggregation(aggr, iterations=3)
     _, dims, _ = workloads.model("qsize")
     mi = Model_information(copy.deepcopy(desc), dims)
     graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
