@@ -148,6 +148,8 @@ struct RoBatchOp {
   int64_t* d_count = nullptr;     // [G] rows per graph
   float* d_partial = nullptr;     // [n_chunks][F]
   int64_t* d_seg = nullptr;       // product: [G + 1] row offsets of the output space
+  int64_t* d_inoff = nullptr;     // pooling: [G + 1] row offsets of the input space (backward)
+  std::vector<int32_t> h_idx[2];  // extend: host copies of idx (the backward's transposed CSRs)
 };
 
 }  // namespace ign
@@ -256,7 +258,8 @@ int64_t readout_layout(ign_plan* p, int64_t off);              // raw parameter 
 int64_t readout_packed(ign_plan* p, int64_t pk);               // packed Dense fragments
 int readout_repack(ign_plan* p);
 int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d);
-int readout_ops_run(ign_plan* p, ign_batch* b, hipStream_t st);
+// ent: entity-state tensors to read (training keeps every version); null = the batch's current states
+int readout_ops_run(ign_plan* p, ign_batch* b, hipStream_t st, const float* const* ent = nullptr);
 const float* readout_tensor(const ign_plan* p, const ign_batch* b, int id);
 int64_t space_rows(const ign_plan* p, const ign_batch* b, const RoTensor& t);
 template <typename T>

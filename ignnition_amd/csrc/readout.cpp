@@ -257,7 +257,7 @@ int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d) {
         }
         bo.n_chunks = (int64_t)chunk.size() / 2;
         if ((rc = dev_upload(b, &bo.d_chunk, chunk)) || (rc = dev_upload(b, &bo.d_chunk_ptr, cptr)) ||
-            (rc = dev_upload(b, &bo.d_count, count)))
+            (rc = dev_upload(b, &bo.d_count, count)) || (rc = dev_upload(b, &bo.d_inoff, off)))
           return rc;
         if ((rc = dev_alloc(b, &bo.d_partial, std::max<int64_t>(1, bo.n_chunks * t0.width)))) return rc;
         break;
@@ -281,6 +281,8 @@ int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d) {
             id[e] = (int32_t)(b->row_off[de][g] + t);
           }
         if ((rc = dev_upload(b, &bo.idx[0], is)) || (rc = dev_upload(b, &bo.idx[1], id))) return rc;
+        bo.h_idx[0] = std::move(is);
+        bo.h_idx[1] = std::move(id);
         break;
       }
     }
@@ -288,8 +290,12 @@ int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d) {
   return IGN_OK;
 }
 
-int readout_ops_run(ign_plan* p, ign_batch* b, hipStream_t st) {
+int readout_ops_run(ign_plan* p, ign_batch* b, hipStream_t st, const float* const* ent) {
   const float* prm = p->d_params;
+  const int NE = (int)p->ents.size();
+  auto readout_tensor = [&](const ign_plan* pp, const ign_batch* bb, int id) -> const float* {
+    return ent && id < NE ? ent[id] : ign::readout_tensor(pp, bb, id);
+  };
   for (size_t k = 0; k < p->ro_ops.size(); ++k) {
     const RoOp& op = p->ro_ops[k];
     RoBatchOp& bo = b->ro[k];

@@ -25,3 +25,11 @@ hipError_t launch_pool(const float* x, int F, int64_t n_chunks, const int64_t* c
 hipError_t launch_product(const ProductArgs& a, hipStream_t st);
 // tf.gather on axis 0 (AUX:1236-1265)
 hipError_t launch_gather(const float* src, int F, const int32_t* idx, int64_t n, float* dst, hipStream_t st);
+
+// backward (training): pooling over each graph's rows (off: [G + 1] row offsets of the input
+// space; ties: [G][F] scratch for max), dx accumulated
+hipError_t launch_pool_bwd(const float* x, const float* y, const float* dy, float* ties, int F, const int64_t* off, int G,
+                           int mode, int64_t n, float* dx, hipStream_t st);
+// d(a) of out = a * b (seg: [G + 1] row offsets of the output space), accumulated
+hipError_t launch_product_bwd(const float* dout, const float* b, int Fa, int Fb, int F, int a_graph, int b_graph,
+                              const int64_t* seg, int G, int64_t n_a, float* da, hipStream_t st);

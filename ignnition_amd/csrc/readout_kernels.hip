@@ -3,6 +3,7 @@
 // (AUX:1236-1265).  All HBM-bound row work: coalesced row-major reads, no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -103,6 +104,57 @@ int grid_of(int64_t total) {
   return (int)(b < 16384 ? b : 16384);
 }
 
+// ---- backward (training through the readout operations) --------------------------------------
+// tf.reduce_max's gradient splits equally among the rows that equal the maximum: their count
+__global__ void pool_ties_kernel(const float* __restrict__ x, const float* __restrict__ y, int F,
+                                 const int64_t* __restrict__ off, int G, float* __restrict__ ties) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)G * F) return;
+  const int g = (int)(i / F), c = (int)(i % F);
+  float n = 0.f;
+  for (int64_t r = off[g]; r < off[g + 1]; ++r) n += x[r * F + c] == y[i] ? 1.f : 0.f;
+  ties[i] = n;
+}
+
+// dx[r] += dy[g(r)] (sum), / count (mean), or on the maximal rows / ties (max)
+__global__ void pool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                const float* __restrict__ dy, const float* __restrict__ ties, int F,
+                                const int64_t* __restrict__ off, int G, int mode, int64_t n,
+                                float* __restrict__ dx) {
+  const int64_t total = n * F;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / F;
+    const int c = (int)(e - r * F);
+    const int64_t g = graph_of(off, G, r);
+    const int64_t gi = g * F + c;
+    float v = dy[gi];
+    if (mode == POOL_MEAN) v /= (float)(off[g + 1] - off[g]);
+    else if (mode == POOL_MAX) v = x[e] == y[gi] ? v / ties[gi] : 0.f;
+    dx[e] += v;
+  }
+}
+
+// out = a * b (widths Fa / Fb, 1 broadcasts; a graph-space operand broadcasts over its graph's
+// rows).  da[ra][ca] += sum over the output elements it fed of dout * b.  One thread per element
+// of a: deterministic, no atomics.
+__global__ void product_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ b, int Fa, int Fb, int F,
+                                   int a_graph, int b_graph, const int64_t* __restrict__ seg, int G, int64_t n_a,
+                                   float* __restrict__ da) {
+  const int64_t total = n_a * Fa;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ra = e / Fa;
+    const int ca = (int)(e - ra * Fa);
+    const int64_t r0 = a_graph ? seg[ra] : ra, r1 = a_graph ? seg[ra + 1] : ra + 1;
+    const int c0 = (Fa == 1 && F > 1) ? 0 : ca, c1 = (Fa == 1 && F > 1) ? F : ca + 1;
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t rb = b_graph ? graph_of(seg, G, r) : r;
+      for (int c = c0; c < c1; ++c) s += dout[r * F + c] * b[rb * Fb + (Fb == 1 ? 0 : c)];
+    }
+    da[e] += s;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_pool(const float* x, int F, int64_t n_chunks, const int64_t* chunk, const int32_t* chunk_ptr,
@@ -128,5 +180,26 @@ hipError_t launch_product(const ProductArgs& a, hipStream_t st) {
 hipError_t launch_gather(const float* src, int F, const int32_t* idx, int64_t n, float* dst, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(gather_kernel, dim3(grid_of(n * F)), dim3(kThreads), 0, st, src, F, idx, n, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool_bwd(const float* x, const float* y, const float* dy, float* ties, int F, const int64_t* off, int G,
+                           int mode, int64_t n, float* dx, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (mode == POOL_MAX)
+    hipLaunchKernelGGL(pool_ties_kernel, dim3((unsigned)(((int64_t)G * F + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       st, x, y, F, off, G, ties);
+  const int64_t blocks = std::min<int64_t>((n * F + kThreads - 1) / kThreads, 16384);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st, x, y, dy, ties, F, off, G, mode, n,
+                     dx);
+  return hipGetLastError();
+}
+
+hipError_t launch_product_bwd(const float* dout, const float* b, int Fa, int Fb, int F, int a_graph, int b_graph,
+                              const int64_t* seg, int G, int64_t n_a, float* da, hipStream_t st) {
+  if (n_a == 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n_a * Fa + kThreads - 1) / kThreads, 16384);
+  hipLaunchKernelGGL(product_bwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st, dout, b, Fa, Fb, F, a_graph,
+                     b_graph, seg, G, n_a, da);
   return hipGetLastError();
 }

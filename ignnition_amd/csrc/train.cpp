@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "engine_internal.h"
+#include "readout_kernels.h"
 #include "train_kernels.h"
 
 struct MPTrain {
@@ -72,6 +73,12 @@ struct TrainState {
   float* ads_src = nullptr;
   float* ads_dst = nullptr;
   float* adw12 = nullptr;
+  // readout operations before predict (GM:605-655): d(tensor) per op output, Dense scratch
+  std::vector<float*> dT;                 // per readout tensor id (null for entity states)
+  float* rz[2] = {nullptr, nullptr};
+  float* rcat = nullptr;
+  float* rties = nullptr;
+  std::vector<int32_t*> rx_ptr, rx_idx;   // extend ops: per op 2 transposed CSRs (input row -> edges)
   bool forward_done = false;
   std::vector<void*> allocs;
 };
@@ -195,7 +202,6 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   const int E = (int)p->ents.size();
   for (int e = 0; e < E; ++e)
     if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
-  if (!p->ro_ops.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for readout operations before predict yet");
   for (auto& mp : p->mps) {
     if (mp.aggr == IGN_AGGR_ATTENTION)
       for (auto& nn : mp.nn)
@@ -392,6 +398,48 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   if (p->ro_in.size() > 1 &&
       ((rc = talloc(t.get(), &t->ro_x, P * p->ro_width)) || (rc = talloc(t.get(), &t->dro, P * p->ro_width))))
     return rc;
+  // readout operations (GM:605-655)
+  t->dT.assign(p->ro_t.size(), nullptr);
+  {
+    int64_t rz_n = 0, rcat_n = 0, ties_n = 0;
+    for (size_t k = 0; k < p->ro_ops.size(); ++k) {
+      const RoOp& op = p->ro_ops[k];
+      const RoBatchOp& bo = b->ro[k];
+      const int nout = op.type == IGN_RO_EXTEND ? 2 : 1;
+      for (int j = 0; j < nout; ++j) {
+        const RoTensor& to = p->ro_t[op.out + j];
+        if ((rc = talloc(t.get(), &t->dT[op.out + j], space_rows(p, b, to) * to.width))) return rc;
+      }
+      const int64_t n = space_rows(p, b, p->ro_t[op.in[0]]);
+      if (op.type == IGN_RO_NEURAL_NETWORK) {
+        int widest = op.in_width, K = op.in_width;
+        for (auto& d : op.layers) {
+          widest = std::max(widest, d.out);
+          need_part(n, K, d.out);
+          K = d.out;
+        }
+        rz_n = std::max(rz_n, n * widest);
+        if (op.in.size() > 1) rcat_n = std::max(rcat_n, n * op.in_width);
+      } else if (op.type == IGN_RO_POOLING) {
+        ties_n = std::max(ties_n, (int64_t)b->G * p->ro_t[op.in[0]].width);
+      } else if (op.type == IGN_RO_EXTEND) {
+        for (int j = 0; j < 2; ++j) {
+          const std::vector<int32_t>& ix = bo.h_idx[j];
+          std::vector<std::pair<int64_t, int32_t>> kv(ix.size());
+          for (size_t e2 = 0; e2 < ix.size(); ++e2) kv[e2] = {ix[e2], (int32_t)e2};
+          std::vector<int32_t> ptr, idx;
+          build_csr(space_rows(p, b, p->ro_t[op.in[j]]), kv, ptr, idx);
+          int32_t *dp = nullptr, *di = nullptr;
+          if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
+          t->rx_ptr.push_back(dp);
+          t->rx_idx.push_back(di);
+        }
+      }
+    }
+    if ((rz_n && ((rc = talloc(t.get(), &t->rz[0], rz_n)) || (rc = talloc(t.get(), &t->rz[1], rz_n)))) ||
+        (rcat_n && (rc = talloc(t.get(), &t->rcat, rcat_n))) || (ties_n && (rc = talloc(t.get(), &t->rties, ties_n))))
+      return rc;
+  }
   if ((rc = talloc(t.get(), &t->part, part_n))) return rc;
   b->train = t.release();
   return IGN_OK;
@@ -456,14 +504,18 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
       t->recs.push_back(rec);
     }
   }
-  // readout with every activation kept (GM:611-629)
+  // readout operations, then the predict stack with every activation kept (GM:605-629)
+  std::vector<const float*> ent(E);
+  for (int e = 0; e < E; ++e) ent[e] = t->ver[e][t->cur[e]];
+  if (!p->ro_ops.empty() && (rc = readout_ops_run(p, b, st, ent.data()))) return rc;
+  auto tensor = [&](int id) -> const float* { return id < E ? ent[id] : b->ro_buf[id]; };
   const int64_t P = b->n_pred;
-  const float* x = t->ver[p->ro_in[0]][t->cur[p->ro_in[0]]];
+  const float* x = tensor(p->ro_in[0]);
   if (p->ro_in.size() > 1) {
     int col = 0;
-    for (int e : p->ro_in) {
-      HIP_TRY(launch_concat_cols(t->ro_x, P, p->ro_width, col, t->ver[e][t->cur[e]], p->ents[e].hidden_dim, st));
-      col += p->ents[e].hidden_dim;
+    for (int id : p->ro_in) {
+      HIP_TRY(launch_concat_cols(t->ro_x, P, p->ro_width, col, tensor(id), p->ro_t[id].width, st));
+      col += p->ro_t[id].width;
     }
     x = t->ro_x;
   }
@@ -499,9 +551,14 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
   for (int e = 0; e < E; ++e)
     HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, b->rows[e] * p->ents[e].hidden_dim * sizeof(float), st));
 
-  // ---- readout (GM:611-629) in reverse
+  // ---- readout (GM:605-629) in reverse: predict, then the operations before it
+  for (size_t id = 0; id < t->dT.size(); ++id)
+    if (t->dT[id])
+      HIP_TRY(hipMemsetAsync(t->dT[id], 0, space_rows(p, b, p->ro_t[id]) * p->ro_t[id].width * sizeof(float), st));
+  auto tensor = [&](int id) -> const float* { return id < E ? t->ver[id][t->cur[id]] : b->ro_buf[id]; };
+  auto grad_of = [&](int id) -> float* { return id < E ? t->dS[0][id] : t->dT[id]; };
   const int L = (int)p->dense.size();
-  const float* X = p->ro_in.size() > 1 ? t->ro_x : t->ver[p->ro_in[0]][t->cur[p->ro_in[0]]];
+  const float* X = p->ro_in.size() > 1 ? t->ro_x : tensor(p->ro_in[0]);
   int zi = 0;
   HIP_TRY(launch_act_bwd(dpred, b->d_pred, P * p->dense[L - 1].out, p->dense[L - 1].act, t->dz[0], st));
   for (int l = L - 1; l >= 0; --l) {
@@ -520,7 +577,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     } else if (p->ro_in.size() > 1) {
       out = t->dro;
     } else {
-      out = t->dS[0][p->ro_in[0]];
+      out = grad_of(p->ro_in[0]);
       acc = 1;
     }
     if (d.pk_wt >= 0)
@@ -529,12 +586,74 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       HIP_TRY(launch_row_gemm_t_generic(t->dz[zi], P, d.out, p->d_params + d.off_w, d.in, out, acc, act, aprev, st));
     zi = 1 - zi;
   }
-  if (p->ro_in.size() > 1) {   // split dX by columns into the input entities (concat axis 1)
+  if (p->ro_in.size() > 1) {   // split dX by columns into the input tensors (concat axis 1)
     int col = 0;
-    for (int e : p->ro_in) {
-      const int h = p->ents[e].hidden_dim;
-      HIP_TRY(launch_split_cols_add(t->dS[0][e], P, h, t->dro, p->ro_width, col, st));
-      col += h;
+    for (int id : p->ro_in) {
+      const int w = p->ro_t[id].width;
+      HIP_TRY(launch_split_cols_add(grad_of(id), P, w, t->dro, p->ro_width, col, st));
+      col += w;
+    }
+  }
+  int xi = (int)t->rx_ptr.size();   // extend CSRs are stored in op order, two per op
+  for (int k = (int)p->ro_ops.size() - 1; k >= 0; --k) {
+    const RoOp& op = p->ro_ops[k];
+    const RoBatchOp& bo = b->ro[k];
+    const RoTensor& t0 = p->ro_t[op.in[0]];
+    const int64_t n = space_rows(p, b, t0);
+    switch (op.type) {
+      case IGN_RO_NEURAL_NETWORK: {   // Readout_nn (AUX:1188-1211): Dense stack on concat(inputs)
+        const int NL = (int)op.layers.size();
+        int rz = 0;
+        HIP_TRY(launch_act_bwd(t->dT[op.out], bo.out[0], n * op.layers[NL - 1].out, op.layers[NL - 1].act, t->rz[0], st));
+        for (int l = NL - 1; l >= 0; --l) {
+          const DenseP& d = op.layers[l];
+          const int K = l == 0 ? op.in_width : op.layers[l - 1].out;
+          const float* A = l > 0 ? bo.tmp[l - 1] : op.in.size() > 1 ? bo.cat : tensor(op.in[0]);
+          HIP_TRY(launch_tsgemm_add(A, K, t->rz[rz], d.out, n, K, d.out, t->part, grads + d.off_w,
+                                    d.use_bias ? grads + d.off_b : nullptr, st));
+          if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)K * d.out, st));
+          if (l > 0) {
+            HIP_TRY(launch_row_gemm_t_generic(t->rz[rz], n, d.out, p->d_params + d.off_w, K, t->rz[1 - rz], 0,
+                                              op.layers[l - 1].act, bo.tmp[l - 1], st));
+            rz = 1 - rz;
+          } else if (op.in.size() > 1) {
+            HIP_TRY(launch_row_gemm_t_generic(t->rz[rz], n, d.out, p->d_params + d.off_w, K, t->rcat, 0, -1, nullptr, st));
+            int col = 0;
+            for (int id : op.in) {
+              const int w = p->ro_t[id].width;
+              HIP_TRY(launch_split_cols_add(grad_of(id), n, w, t->rcat, op.in_width, col, st));
+              col += w;
+            }
+          } else {
+            HIP_TRY(launch_row_gemm_t_generic(t->rz[rz], n, d.out, p->d_params + d.off_w, K, grad_of(op.in[0]), 1, -1,
+                                              nullptr, st));
+          }
+        }
+        break;
+      }
+      case IGN_RO_POOLING:   // Pooling_operation (AUX:1165-1185)
+        HIP_TRY(launch_pool_bwd(tensor(op.in[0]), bo.out[0], t->dT[op.out], t->rties, t0.width, bo.d_inoff, b->G, op.mode,
+                                n, grad_of(op.in[0]), st));
+        break;
+      case IGN_RO_PRODUCT: {   // element_wise (AUX:1081-1088)
+        const RoTensor& t1 = p->ro_t[op.in[1]];
+        const RoTensor& to = p->ro_t[op.out];
+        const int ag = t0.space == RS_GRAPH && to.space != RS_GRAPH, bg = t1.space == RS_GRAPH && to.space != RS_GRAPH;
+        HIP_TRY(launch_product_bwd(t->dT[op.out], tensor(op.in[1]), t0.width, t1.width, to.width, ag, bg, bo.d_seg, b->G,
+                                   n, grad_of(op.in[0]), st));
+        HIP_TRY(launch_product_bwd(t->dT[op.out], tensor(op.in[0]), t1.width, t0.width, to.width, bg, ag, bo.d_seg, b->G,
+                                   space_rows(p, b, t1), grad_of(op.in[1]), st));
+        break;
+      }
+      case IGN_RO_EXTEND: {   // Extend_adjacencies (AUX:1236-1265): gathers, so scatter back per row
+        xi -= 2;
+        for (int j = 0; j < 2; ++j) {
+          const RoTensor& tj = p->ro_t[op.in[j]];
+          HIP_TRY(launch_csr_gather_cols_add(grad_of(op.in[j]), space_rows(p, b, tj), t->rx_ptr[xi + j], t->rx_idx[xi + j],
+                                             t->dT[op.out + j], tj.width, 0, tj.width, 1, st));
+        }
+        break;
+      }
     }
   }
 

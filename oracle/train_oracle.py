@@ -202,19 +202,55 @@ class TorchOracle:
             lname = layer.get("name", "layer_%d_%s_message_creation_%d" % (li, layer["type_layer"], k))
             yield layer, "%s_to_%s_message_creation_0/%s" % (sname, dst, lname)
 
-    def _layers(self, op):
+    def _layers(self, op, counter):
+        """readout_model_<index of the op in the readout list> (GM:352-358), Feed_forward_model names."""
         for li, layer in enumerate(self.nn[op["nn_name"]]["nn_architecture"]):
             name = layer.get("name", "layer_%d_%s_readout" % (li, layer["type_layer"]))
-            yield layer, "readout_model_0/" + name
+            yield layer, "readout_model_%d/%s" % (counter, name)
 
     def _readout(self, state, x):
-        for op in self.d["readout"]:
-            if op["type"] != "predict":
-                continue
-            h = torch.cat([state[i] for i in op["input"]], 1)
-            for layer, pre in self._layers(op):
-                h = _act(h @ self.p[pre + "/kernel"] + self.p[pre + "/bias"], layer.get("activation"))
-            return h
+        """GM:605-655: operations before predict write named tensors (get_global_var_or_input,
+        GM:660-675), then predict.  As the dense oracle, with torch ops."""
+        var = dict(state)
+
+        def get(name):
+            return var[name] if name in var else torch.tensor(np.asarray(x[name], np.float64), dtype=_T)
+
+        for counter, op in enumerate(self.d["readout"]):
+            t = op["type"]
+            if t in ("predict", "neural_network"):                         # GM:612-628
+                h = torch.cat([get(i) for i in op["input"]], 1)
+                for layer, pre in self._layers(op, counter):
+                    h = h @ self.p[pre + "/kernel"]
+                    if pre + "/bias" in self.p:
+                        h = h + self.p[pre + "/bias"]
+                    h = _act(h, layer.get("activation"))
+                if t == "predict":
+                    return h
+                var[op.get("output_name", "None")] = h
+            elif t == "pooling":                                           # AUX:1165-1185
+                v = get(op["input"][0])
+                kind = op["type_pooling"]
+                if kind == "sum":
+                    r = v.sum(0)
+                elif kind == "mean":
+                    r = v.sum(0) / v.shape[0]
+                elif kind == "max":
+                    # tf.reduce_max: the gradient is split equally among the maximal rows
+                    ind = (v == v.max(0).values).to(_T)
+                    r = (v * ind).sum(0) / ind.sum(0)
+                else:
+                    raise OracleError("pooling %r not restated" % kind)
+                var[op["output_name"]] = r.reshape(1, -1)
+            elif t == "product":                                           # AUX:1072-1088
+                if op["type_product"] != "element_wise":
+                    raise OracleError("dot_product (rank-4 tensordot) not restated")
+                var[op["output_name"]] = get(op["input"][0]) * get(op["input"][1])
+            elif t == "extend_adjacencies":                                # AUX:1236-1265
+                var[op["output_name_src"]] = get(op["input"][0])[torch.as_tensor(np.asarray(x["src_" + op["adj_list"]], np.int64))]
+                var[op["output_name_dst"]] = get(op["input"][1])[torch.as_tensor(np.asarray(x["dst_" + op["adj_list"]], np.int64))]
+            else:
+                raise OracleError("readout op %s not restated" % t)
         raise OracleError("no predict operation")
 
     # ---------------------------------------------------------------- loss (GM:745-753)
@@ -232,10 +268,10 @@ class TorchOracle:
                             if "kernel_regularizer" in layer:
                                 W = self.p[pre + "/kernel"]
                                 total = total + float(layer["kernel_regularizer"]) * (W * W).sum()
-        for op in self.d["readout"]:
-            if op["type"] != "predict":
+        for counter, op in enumerate(self.d["readout"]):
+            if op["type"] not in ("predict", "neural_network"):
                 continue
-            for layer, pre in self._layers(op):
+            for layer, pre in self._layers(op, counter):
                 if "kernel_regularizer" in layer:
                     W = self.p[pre + "/kernel"]
                     total = total + float(layer["kernel_regularizer"]) * (W * W).sum()

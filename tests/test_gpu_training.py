@@ -197,3 +197,23 @@ def test_gradients_attention_two_sources():
     graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
     prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
     _check(desc, dims, graphs, labels, prm)
+
+
+@pytest.mark.parametrize("case", ["pool_sum", "pool_mean", "pool_max", "nn_pool_product", "product_width1",
+                                  "extend_nn", "extend_pool", "shadow_entity_name"])
+def test_gradients_readout_operations(case):
+    """Readout operations before predict (GM:605-655): neural_network, pooling (max: tf's
+    gradient split among ties), element-wise product with broadcasting, extend_adjacencies."""
+    from oracle.dense_forward import DenseOracle
+    from tests.readout_cases import READOUT_CASES
+    ops, pin, nets = READOUT_CASES[case]
+    desc = model_examples.routenet_readout(ops, pin, nets, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet" if g % 2 == 0 else "geant2", g)
+                                            for g in range(3)])
+    prm = MPPlan.from_model_info(mi).init_params(11, bias_scale=0.1)
+    ora = DenseOracle(desc, dims, prm)
+    rng = np.random.default_rng(5)   # labels shaped like each graph's predictions
+    labels = [rng.normal(size=ora.forward_graph(g).size).astype(np.float32) for g in graphs]
+    _check(desc, dims, graphs, labels, prm)

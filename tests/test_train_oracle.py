@@ -128,3 +128,19 @@ def test_eval_metrics():
     assert m["mae"] == pytest.approx(0.5)
     assert m["mre"] == pytest.approx((0.5 + 0 + 0.25) / 3)
     assert m["r-squared"] == pytest.approx(1 - 1.25 / (((np.array([1, 2, 4]) - 7 / 3) ** 2).sum()))
+
+
+@pytest.mark.parametrize("case", ["pool_sum", "pool_max", "nn_pool_product", "product_width1", "extend_nn",
+                                  "extend_pool", "shadow_entity_name"])
+def test_torch_forward_readout_operations_match_dense_oracle(case):
+    from tests.readout_cases import READOUT_CASES
+    ops, pin, nets = READOUT_CASES[case]
+    desc = model_examples.routenet_readout(ops, pin, nets, iterations=3)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g) for g in range(2)])
+    prm = MPPlan.from_model_info(mi).init_params(4, bias_scale=0.1)
+    got = TorchOracle(desc, dims, prm).forward(graphs).detach().numpy()
+    exp = DenseOracle(desc, dims, prm).forward(graphs)
+    np.testing.assert_allclose(got, exp, rtol=1e-10, atol=1e-12)
+
