@@ -178,6 +178,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(6, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v) != 0;
+  if (const char* v = getenv("IGN_SUM_SPLIT")) p->sum_split = atoi(v) != 0;
   if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(5, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
@@ -877,7 +878,17 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         for (int g = 0; g < G; ++g)
           max_src_rows = std::max(max_src_rows, b->row_off[mp.src[0].entity][g + 1] - b->row_off[mp.src[0].entity][g]);
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
-      if (p->sum_window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
+      // split sum update (IGN_SUM_SPLIT=1): gather-only kernel, then the GRU step through an identity CSR
+      if (p->sum_split && mp.aggr == IGN_AGGR_SUM && (DIN == 16 || DIN == 32 || DIN == 64)) {
+        std::vector<int32_t> id_ptr(ND + 1);
+        std::vector<uint32_t> id_src(ND);
+        for (int64_t i = 0; i <= ND; ++i) id_ptr[i] = (int32_t)i;
+        for (int64_t i = 0; i < ND; ++i) id_src[i] = (uint32_t)order[i];
+        if ((rc = dev_upload(b.get(), &mb.d_id_ptr, id_ptr)) || (rc = dev_upload(b.get(), &mb.d_id_src, id_src)) ||
+            (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
+          return rc;
+      }
+      if (!p->sum_split && p->sum_window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
         std::vector<int64_t> dstart(ND + 1, 0);
@@ -1151,6 +1162,16 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
       tm.begin(K_SUM, mb.flops, mb.bytes);
       HIP_TRY(launch_sum_win(wa, mp.din, st));
+      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
+      tm.end();
+    } else if (count > 0 && mb.d_id_ptr && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
+      SumGruArgs g{hin, hout, sbases, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, nullptr, nullptr, nullptr, mb.n_dst, 0};
+      SrcBases xb{};
+      xb.base[0] = mb.d_xsum;
+      SumGruArgs a{hin, hout, xb, mb.d_order, mb.d_id_ptr, mb.d_id_src, p->d_packed + cp.pk_w,
+                   p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
+      tm.begin(K_SUM, mb.flops, mb.bytes);
+      HIP_TRY(launch_sum_only(g, mp.din, mb.d_xsum, st));
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
       tm.end();
     } else if (count > 0) {

@@ -110,6 +110,8 @@ struct SumWinArgs {
   int64_t n_wg;
 };
 hipError_t launch_sum_win(const SumWinArgs& args, int din, hipStream_t st);
+// the message gather of a plain sum update alone: xsum[dst row] = sum of its source rows
+hipError_t launch_sum_only(const SumGruArgs& args, int din, float* xsum, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

@@ -820,6 +820,47 @@ __global__ __launch_bounds__(1024) void sum_win_kernel(SumWinArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split sum update, part 1 (IGN_SUM_SPLIT=1): the message gather of sum_gru without the GRU
+// weights, so the kernel is small (≈40 VGPRs, 8 waves/SIMD) and keeps 8 source rows in flight per
+// lane; x[dst row] is written and the GRU step runs on it through an identity CSR.
+template <int DIN>
+__global__ __launch_bounds__(256) void sum_only_kernel(SumGruArgs a, float* __restrict__ xsum) {
+  constexpr int NC = DIN / 16, GU = 8;
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t pos = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + j;
+  const bool valid = pos < a.n_dst;
+  const int row = valid ? a.order[pos] : 0;
+  const int64_t m0 = valid ? a.msg_ptr[pos] : 0, m1 = valid ? a.msg_ptr[pos + 1] : 0;
+  f4 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+  int64_t m = m0;
+  for (; m + GU <= m1; m += GU) {
+    f4 v[GU][NC];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const float* p = src_ptr(a.src, a.msg_src[m + u], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += v[u][c];
+  }
+  for (; m < m1; ++m) {
+    const float* p = src_ptr(a.src, a.msg_src[m], DIN);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+  }
+  if (valid) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) st4(xsum + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+  }
+}
+
 // Attention softmax weights: one wave per (graph, position) group.
 __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63;
@@ -1627,6 +1668,16 @@ hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_
   dim3 grid(grid_for(args.n_dst, 64)), block(256);
   if (h == 32) hipLaunchKernelGGL((seq_gru_kernel<32>), grid, block, 0, st, args);
   else if (h == 16) hipLaunchKernelGGL((seq_gru_kernel<16>), grid, block, 0, st, args);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_only(const SumGruArgs& args, int din, float* xsum, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  const dim3 grid((unsigned)((args.n_dst + 63) / 64)), block(256);
+  if (din == 32) hipLaunchKernelGGL((sum_only_kernel<32>), grid, block, 0, st, args, xsum);
+  else if (din == 16) hipLaunchKernelGGL((sum_only_kernel<16>), grid, block, 0, st, args, xsum);
+  else if (din == 64) hipLaunchKernelGGL((sum_only_kernel<64>), grid, block, 0, st, args, xsum);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
