@@ -179,7 +179,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_SPLIT")) p->sum_split = atoi(v) != 0;
-  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(5, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(7, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -1247,7 +1247,8 @@ int readout(ign_plan* p, ign_batch* b) {
     if (p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0)
       HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
                                 p->readout_variant == 3 ? 9 : p->readout_variant == 4 ? -6 :
-                                p->readout_variant == 5 ? -7 : 6, st));
+                                p->readout_variant == 5 ? -7 : p->readout_variant == 6 ? -8 :
+                                p->readout_variant == 7 ? -9 : 6, st));
     else
       HIP_TRY(launch_readout3(a, l1.in, l1.out, l2.out, st));
     tm.end();

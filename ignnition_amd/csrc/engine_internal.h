@@ -182,7 +182,9 @@ struct ign_plan {
   bool params_set = false;
   bool fused_readout = false;
   int readout_variant = 2;        // fused readout: 1 = f32 MFMA (readout3), 2 / 3 = split-bf16 with 6 / 9
-                                  // piece products (readout_bf); IGN_READOUT_VARIANT
+                                  // piece products (readout_bf); 4-7 = readout_bf layout diagnostics
+                                  // (32-unit chunks, 4-wave blocks, one tile per wave, two blocks per
+                                  // CU); IGN_READOUT_VARIANT
   int ro_width = 0;
   int seq_variant = 4;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves),
                                   // 3 = 2 software-pipelined, 4/5 = split-bf16 h.U (6 / 9 piece products)

@@ -270,7 +270,25 @@ __device__ __forceinline__ f4 split_mfma(const bf8* __restrict__ afrag, int stri
   return acc;
 }
 
-template <int DIN, int ACT, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32)>
+// acc[t] += A . B_t for RT row tiles that share each A (weight) fragment read; b = hf[t][s]
+template <int PASSES, int RT, int KS>
+__device__ __forceinline__ void split_mfma_rt(const bf8* __restrict__ afrag, int stride, const bf8 (&b)[RT][KS][3],
+                                              int s, f4 (&acc)[RT]) {
+  bf8 w[3];
+#pragma unroll
+  for (int pu = 0; pu < 3; ++pu) w[pu] = afrag[pu * stride];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int pu = 2; pu >= 0; --pu)
+#pragma unroll
+      for (int ph = 2; ph >= 0; --ph) {
+        if (PASSES == 6 && pu + ph > 2) continue;
+        acc[t] = MFMA_BF(w[pu], b[t][s][ph], acc[t]);
+      }
+}
+
+template <int DIN, int ACT, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32), int RT = 1>
 __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, const bf8* __restrict__ W1f,
                                                                  const bf8* __restrict__ W2f) {
   constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
@@ -290,41 +308,52 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
   }
   for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
-  const int64_t r = ((int64_t)blockIdx.x * WAVES + wave) * 16 + j;
-  const bool ok = r < a.n_rows;
+  // RT row tiles of 16 per wave: tile t covers rows r0 + 16t .. +16
+  const int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * (16 * RT) + j;
   // layer-1 input fragments: lane (row j, group g) holds x[row][32s + 8g .. +8) (natural k order)
-  bf8 xf[KS1][3];
-  {
+  bf8 xf[RT][KS1][3];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int64_t r = r0 + 16 * t;
+    const bool ok = r < a.n_rows;
     const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
       const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
       const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      split_frag(v, xf[s]);
+      split_frag(v, xf[t][s]);
     }
   }
   __syncthreads();
   // layer 1 -> activations in accumulator layout -> split once into the layer-2 B fragments
-  bf8 hf[KS2][3];
+  bf8 hf[RT][KS2][3];
 #pragma unroll
   for (int s2 = 0; s2 < KS2; ++s2) {
-    float v[8];
+    float v[RT][8];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int u = 2 * s2 + half;
-      f4 acc = ld4(a.b1 + 16 * u + 4 * g);
+      f4 acc[RT];
+      const f4 bias = ld4(a.b1 + 16 * u + 4 * g);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = bias;
 #pragma unroll
       for (int s = 0; s < KS1; ++s) {
         const bf8* af = W1_LDS ? sw1 + ((u * KS1 + s) * 3) * 64 + lane : W1f + ((u * KS1 + s) * 3) * 64 + lane;
-        acc = split_mfma<PASSES>(af, 64, xf[s], acc);
+        split_mfma_rt<PASSES, RT, KS1>(af, 64, xf, s, acc);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[4 * half + q] = act_t<ACT>(acc[q]);
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[t][4 * half + q] = act_t<ACT>(acc[t][q]);
     }
-    split_frag(v, hf[s2]);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) split_frag(v[t], hf[t][s2]);
   }
-  float y = 0.f;
+  float y[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) y[t] = 0.f;
 #pragma unroll 1
   for (int v = 0; v < NCH; ++v) {
     const int cur = v & 1;
@@ -346,18 +375,22 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     // opaque lane offset: the LDS reads must not be hoisted out of the chunk loop (registers)
     int lofs = lane;
     asm volatile("" : "+v"(lofs));
-    f4 acc[CT];
+    f4 acc[CT][RT];
 #pragma unroll
-    for (int c = 0; c < CT; ++c) acc[c] = b[c];
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[c][t] = b[c];
 #pragma unroll
     for (int s = 0; s < KS2; ++s)
 #pragma unroll
       for (int c = 0; c < CT; ++c)
-        acc[c] = split_mfma<PASSES>(sw2[cur] + (c * KS2 + s) * 3 * 64 + lofs, 64, hf[s], acc[c]);
+        split_mfma_rt<PASSES, RT, KS2>(sw2[cur] + (c * KS2 + s) * 3 * 64 + lofs, 64, hf, s, acc[c]);
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) y += w3[c][q] * act_t<ACT>(acc[c][q]);
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[t] += w3[c][q] * act_t<ACT>(acc[c][t][q]);
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + NTH * k;
@@ -365,11 +398,16 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     }
     __syncthreads();
   }
-  y += __shfl_xor(y, 16);
-  y += __shfl_xor(y, 32);
-  if (g == 0 && ok) {
-    const float b3 = a.b3 ? a.b3[0] : 0.f;
-    a.y[r] = act_apply(y + b3, a.act3);
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    float yt = y[t];
+    yt += __shfl_xor(yt, 16);
+    yt += __shfl_xor(yt, 32);
+    const int64_t r = r0 + 16 * t;
+    if (g == 0 && r < a.n_rows) {
+      const float b3 = a.b3 ? a.b3[0] : 0.f;
+      a.y[r] = act_apply(yt + b3, a.act3);
+    }
   }
 }
 
@@ -400,17 +438,17 @@ hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int pref
   return hipGetLastError();
 }
 
-template <int DIN, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32)>
+template <int DIN, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32), int RT = 1>
 static hipError_t readout_bf_din(const Readout3Args& args, const void* W1f, const void* W2f, hipStream_t st) {
-  const dim3 grid((unsigned)((args.n_rows + 16 * WAVES - 1) / (16 * WAVES))), block(64 * WAVES);
+  const dim3 grid((unsigned)((args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES))), block(64 * WAVES);
   const bf8* w1 = static_cast<const bf8*>(W1f);
   const bf8* w2 = static_cast<const bf8*>(W2f);
   switch (args.act1) {
-    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
-    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT, W1L>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
+    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
   }
   return hipGetLastError();
 }
@@ -423,15 +461,20 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
                              hipStream_t st) {
   if (args.n_rows == 0) return hipSuccess;
   if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f) return hipErrorInvalidValue;
-  // 32-unit W2 chunks (two accumulators per wave, 8 barriers per tile); LDS 96 + 48 KB at DIN 32
-  // 16-unit chunks measured faster than 32-unit ones (1.10 vs 1.18 ms, 512 x synth50); passes < 0
-  // selects the 32-unit form (diagnostics)
+  // default (passes 6): two 16-row tiles per wave sharing every W2 fragment read, 8-wave blocks
+  // (246 VGPRs, 2 waves/SIMD): 1.03-1.05 ms against 1.13-1.16 ms for one tile per wave in 12-wave
+  // blocks (-8), 512 x synth50. Diagnostics: -6 = 32-unit W2 chunks (1.18 ms), -7 = 4-wave blocks
+  // with W1 from L2, -9 = two tiles per wave in 4-wave blocks, two blocks per CU (1.39-1.41 ms).
   if (din == 32) {
     if (passes == -6) return readout_bf_din<32, 12, 6, 2>(args, W1f, W2f, st);
-    if (passes == -7) return readout_bf_din<32, 4, 6, 1, false>(args, W1f, W2f, st);   // 3 blocks per CU
-    return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 12, 6, 1>(args, W1f, W2f, st);
+    if (passes == -7) return readout_bf_din<32, 4, 6, 1, false>(args, W1f, W2f, st);
+    if (passes == -8) return readout_bf_din<32, 12, 6, 1>(args, W1f, W2f, st);
+    if (passes == -9) return readout_bf_din<32, 4, 6, 1, false, 2>(args, W1f, W2f, st);
+    return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2>(args, W1f, W2f, st);
   }
-  return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
+  if (passes == -8) return readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
+  if (passes == -9) return readout_bf_din<64, 4, 6, 1, false, 2>(args, W1f, W2f, st);
+  return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 8, 6, 1, false, 2>(args, W1f, W2f, st);
 }
 
 hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st) {
