@@ -200,6 +200,7 @@ struct ign_plan {
                                   // (keeps id locality), 2 id order, 3 per-graph sort + XCD-aware
                                   // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
+  bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
   bool sum_split = false;         // plain sums as a gather-only kernel + the GRU step (IGN_SUM_SPLIT=1)
   bool sum_window = false;        // windowed sum aggregation where eligible (IGN_SUM_WINDOW=1): measured
                                   // 0.120 vs 0.112 ms (RouteNet link update), 0.156 vs 0.206 (Q-size)

@@ -277,6 +277,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       ga_n = std::max(ga_n, mb.n_steps * 3 * H);
       gu_n = std::max(gu_n, mt.hs_rows * 3 * H);
       need_part(mt.hs_rows, H, 3 * H);
+      if (p->bwd_fuse && seq_bwd_fused_supported(H)) part_n = std::max(part_n, seq_bwd_partial_floats(H));
       for (int s = 0; s < S; ++s) {
         dtab_n = std::max(dtab_n, mb.src_rows[s] * 3 * H);
         need_part(mb.src_rows[s], mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : DIN, 3 * H);
@@ -686,8 +687,18 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       SeqBwdArgs a{mt.hs[rec.it], mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
                    t->ga, t->gu, mb.n_dst};
-      HIP_TRY(launch_seq_gru_bwd(a, H, st));
-      HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, gb + H3, st));
+      if (p->bwd_fuse && seq_bwd_fused_supported(H)) {
+        // dU and the du_h bias sums inside the kernel; the z / r recurrent-bias sums equal ga's
+        a.gu = nullptr;
+        a.part = t->part;
+        a.dU = grk;
+        a.db_rec = gb + H3;
+        HIP_TRY(launch_seq_gru_bwd(a, H, st));
+        HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, 2 * H, t->part, gb + H3, st));
+      } else {
+        HIP_TRY(launch_seq_gru_bwd(a, H, st));
+        HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, gb + H3, st));
+      }
       HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, gb, st));
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const int se = mp.src[s].entity;

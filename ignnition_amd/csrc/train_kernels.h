@@ -19,8 +19,14 @@ struct SeqBwdArgs {
   float* dh_out;             // [rows][H] dLoss/d(state before the MP), GRU part
   float* ga;                 // [n_steps][3H]  dLoss/d(x.W + b_in) per step
   float* gu;                 // [n_steps + n_dst][3H] dLoss/d(h.U + b_rec), rows aligned with hs
-                             // (the kernel zeroes each sequence's final-state row)
+                             // (the kernel zeroes each sequence's final-state row); unused when fused
   int64_t n_dst;
+  // fused form (part != nullptr, H 16 / 32): dU += sum h_prev^T du and db_rec[2H..3H) += sum du_h are
+  // formed in the kernel (per-wave partials in part, reduced in a fixed order); gu is not written and
+  // the z / r parts of db_rec (= column sums of ga) are left to the caller
+  float* part = nullptr;     // seq_bwd_partial_floats(H)
+  float* dU = nullptr;       // [H][3H] recurrent-kernel gradient (accumulated)
+  float* db_rec = nullptr;   // [3H] recurrent-bias gradient (accumulated)
 };
 
 // Backward of the sum update (AUX:752-765): one GRU step per destination row.
@@ -43,6 +49,8 @@ struct SumBwdArgs {
 hipError_t launch_pack_a(const float* M, int rows, int cols, float* out, hipStream_t st);
 bool bwd_shape_supported(int din, int h);
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st);
+bool seq_bwd_fused_supported(int h);
+int64_t seq_bwd_partial_floats(int h);
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);
 // out[r][:cols] (+)= sum over k in [ptr[r], ptr[r+1]) of in[idx[k]][:cols]   (cols % 4 == 0)
 // attention backward (AUX:287-343; see train_kernels.hip): per-message dw / dv, then per source row
@@ -81,6 +89,9 @@ hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, f
 // C[M][N] += sum_r A[r][:M]^T B[r][:N] and, if Cb, Cb[N] += sum_r B[r][:N] (a virtual ones column);
 // partial sums per row chunk, reduced in a fixed order (deterministic)
 int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N);
+// C[m][n] (row m = M: Cb[n]) += sum of nchunks partial tiles part[c][M + ones][N], in chunk order
+hipError_t launch_partials_reduce_add(float* part, int64_t nchunks, int M, int N, int ones, float* C, float* Cb,
+                                      hipStream_t st);
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
                              float* part, float* C, float* Cb, hipStream_t st);
 // forward Dense layer for the training readout: y = act(x W + b), MFMA when packed fragments exist

@@ -63,13 +63,22 @@ __global__ void pack_a_kernel(const float* __restrict__ M, int rows, int cols, f
 // Lanes whose sequence is shorter skip the step (mask): their gradient passes through.
 // H <= 32: the U and U^T fragments (2 x 12 KB at H = 32) are staged in LDS per block; read from L2
 // per MFMA they cost 24 KB of L2 reads per wave-step (measured 1.34 ms per launch at 512 x synth50).
-template <int H>
+// FUSE (H 16 / 32): persistent waves also form the recurrent-kernel gradient dU = sum h_prev^T du
+// on the MFMA instead of writing du per step for a separate row contraction: each step, h_prev and
+// du are transposed through a per-wave LDS tile ([unit][row], 4-row groups XOR-swizzled by unit so
+// a lane reads its 4 rows as one b128), rows on the MFMA k axis (row 4kk + ks for lane group kk,
+// k-step ks).  Each wave writes one (H + 1) x 3H partial (row H: the column sums of du_h; the z / r
+// column sums equal those of ga); launch_seq_gru_bwd reduces the partials in a fixed order.
+template <int H, bool FUSE>
 __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   constexpr int NT = H / 16, KH = H / 4, K3 = 3 * H / 4;
   constexpr bool LDSU = H <= 32;
+  static_assert(!FUSE || LDSU, "fused dU: H 16 / 32");
   constexpr int NUP = LDSU ? 3 * NT * KH * 64 : 1, NUT = LDSU ? NT * K3 * 64 : 1;
+  constexpr int NTR = FUSE ? 4 * 3 * H * 16 : 1;   // per-wave transpose tiles
   __shared__ float sUp[NUP];
   __shared__ float sUt[NUT];
+  __shared__ float sT[NTR];
   if constexpr (LDSU) {
     for (int e = threadIdx.x; e < NUP / 4; e += blockDim.x)
       reinterpret_cast<f4*>(sUp)[e] = reinterpret_cast<const f4*>(a.Up)[e];
@@ -82,109 +91,178 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int64_t pos = ((int64_t)blockIdx.x * 4 + wave) * 16 + j;
-  const bool valid = pos < a.n_dst;
-  const int row = valid ? a.order[pos] : 0;
-  const int L = valid ? a.len[pos] : 0;
-  const int64_t sp = valid ? a.step_ptr[pos] : 0;
-  const int64_t hbase = valid ? sp + pos : 0;
-  f4 dh[NT];
+  f4 dU[NT][3 * NT], bsum[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) dh[t] = valid ? ld4(a.dh_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-  int Lmax = L;
+  for (int mt = 0; mt < NT; ++mt) {
+    bsum[mt] = f4{0, 0, 0, 0};
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
-  f4 bh[NT];
+    for (int nt = 0; nt < 3 * NT; ++nt) dU[mt][nt] = f4{0, 0, 0, 0};
+  }
+  float* R = sT + (FUSE ? wave * (3 * H * 16) : 0);
+  // transpose-tile offsets: write (unit 16t + 4g + q, row j); read (unit 16x + j, rows 4g .. 4g+3)
+  const int wofs = j ^ (4 * g), rofs = j * 16 + 4 * (g ^ ((j >> 2) & 3));
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  // FUSE: persistent waves (static tile order: deterministic partials); otherwise one tile per wave
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += FUSE ? (int64_t)gridDim.x * 4 : n_tiles) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int L = valid ? a.len[pos] : 0;
+    const int64_t sp = valid ? a.step_ptr[pos] : 0;
+    const int64_t hbase = valid ? sp + pos : 0;
+    f4 dh[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) bh[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+    for (int t = 0; t < NT; ++t) dh[t] = valid ? ld4(a.dh_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    int Lmax = L;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+    f4 bh[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bh[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
 
-  for (int step = Lmax - 1; step >= 0; --step) {
-    const bool act = step < L;
-    const int64_t tt = act ? step : 0;
-    const int64_t i = sp + tt;
-    const int64_t hr = hbase + tt;
-    f4 hp[NT];
+    for (int step = Lmax - 1; step >= 0; --step) {
+      const bool act = step < L;
+      const int64_t tt = act ? step : 0;
+      const int64_t i = sp + tt;
+      const int64_t hr = hbase + tt;
+      f4 hp[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
-    const uint32_t code = a.step_code[i];
-    f4 x[3][NT];
+      for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
+      const uint32_t code = a.step_code[i];
+      f4 x[3][NT];
 #pragma unroll
-    for (int G = 0; G < 3; ++G)
+      for (int G = 0; G < 3; ++G)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
-    // opaque lane offset: keeps the loop-invariant fragment reads inside the step loop (registers)
-    int lofs = lane;
-    asm volatile("" : "+v"(lofs));
-    f4 az[NT], ar[NT], ah[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      az[t] = f4{0, 0, 0, 0};
-      ar[t] = f4{0, 0, 0, 0};
-      ah[t] = bh[t];
-    }
-#pragma unroll
-    for (int s = 0; s < KH; ++s) {
-      const float hb = hp[s >> 2][s & 3];
+        for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
+      // opaque lane offset: keeps the loop-invariant fragment reads inside the step loop (registers)
+      int lofs = lane;
+      asm volatile("" : "+v"(lofs));
+      f4 az[NT], ar[NT], ah[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        az[t] = MFMA(Up[frag_idx(0 * NT + t, s, KH, lofs)], hb, az[t]);
-        ar[t] = MFMA(Up[frag_idx(1 * NT + t, s, KH, lofs)], hb, ar[t]);
-        ah[t] = MFMA(Up[frag_idx(2 * NT + t, s, KH, lofs)], hb, ah[t]);
+        az[t] = f4{0, 0, 0, 0};
+        ar[t] = f4{0, 0, 0, 0};
+        ah[t] = bh[t];
       }
-    }
-    f4 gz[NT], gr[NT], gh[NT], guh[NT], acc[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
+      for (int s = 0; s < KH; ++s) {
+        const float hb = hp[s >> 2][s & 3];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = sig2_(az[t][r] + x[0][t][r]);
-        const float rr = sig2_(ar[t][r] + x[1][t][r]);
-        const float c = tanh2_(x[2][t][r] + rr * ah[t][r]);
-        const float uh = ah[t][r] * kInv2Log2e;
-        const float d = act ? dh[t][r] : 0.f;
-        const float dzp = d * (hp[t][r] - c) * z * (1.f - z);
-        const float dcp = d * (1.f - z) * (1.f - c * c);
-        const float drp = dcp * uh * rr * (1.f - rr);
-        gz[t][r] = dzp;
-        gr[t][r] = drp;
-        gh[t][r] = dcp;
-        guh[t][r] = dcp * rr;
-        acc[t][r] = dh[t][r] * z;
+        for (int t = 0; t < NT; ++t) {
+          az[t] = MFMA(Up[frag_idx(0 * NT + t, s, KH, lofs)], hb, az[t]);
+          ar[t] = MFMA(Up[frag_idx(1 * NT + t, s, KH, lofs)], hb, ar[t]);
+          ah[t] = MFMA(Up[frag_idx(2 * NT + t, s, KH, lofs)], hb, ah[t]);
+        }
       }
-    }
-    if (act) {
+      f4 gz[NT], gr[NT], gh[NT], guh[NT], acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        float* pa = a.ga + i * (3 * H) + 16 * t + 4 * g;
-        st4(pa, gz[t]);
-        st4(pa + H, gr[t]);
-        st4(pa + 2 * H, gh[t]);
-        float* pu = a.gu + hr * (3 * H) + 16 * t + 4 * g;
-        st4(pu, gz[t]);
-        st4(pu + H, gr[t]);
-        st4(pu + 2 * H, guh[t]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = sig2_(az[t][r] + x[0][t][r]);
+          const float rr = sig2_(ar[t][r] + x[1][t][r]);
+          const float c = tanh2_(x[2][t][r] + rr * ah[t][r]);
+          const float uh = ah[t][r] * kInv2Log2e;
+          const float d = act ? dh[t][r] : 0.f;
+          const float dzp = d * (hp[t][r] - c) * z * (1.f - z);
+          const float dcp = d * (1.f - z) * (1.f - c * c);
+          const float drp = dcp * uh * rr * (1.f - rr);
+          gz[t][r] = dzp;
+          gr[t][r] = drp;
+          gh[t][r] = dcp;
+          guh[t][r] = dcp * rr;
+          acc[t][r] = dh[t][r] * z;
+        }
+      }
+      if (act) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          float* pa = a.ga + i * (3 * H) + 16 * t + 4 * g;
+          st4(pa, gz[t]);
+          st4(pa + H, gr[t]);
+          st4(pa + 2 * H, gh[t]);
+          if constexpr (!FUSE) {
+            float* pu = a.gu + hr * (3 * H) + 16 * t + 4 * g;
+            st4(pu, gz[t]);
+            st4(pu + H, gr[t]);
+            st4(pu + 2 * H, guh[t]);
+          }
+        }
+      }
+      if constexpr (FUSE) {   // dU += h_prev^T du over the tile's 16 rows (inactive rows: du = 0)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) R[(16 * t + 4 * g + q) * 16 + wofs] = hp[t][q];
+        f4 af[NT];
+#pragma unroll
+        for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            R[(16 * t + 4 * g + q) * 16 + wofs] = gz[t][q];
+            R[(H + 16 * t + 4 * g + q) * 16 + wofs] = gr[t][q];
+            R[(2 * H + 16 * t + 4 * g + q) * 16 + wofs] = guh[t][q];
+          }
+#pragma unroll
+        for (int nt = 0; nt < 3 * NT; ++nt) {
+          const f4 bf = ld4(R + nt * 256 + rofs);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int mt = 0; mt < NT; ++mt) dU[mt][nt] = MFMA(af[mt][ks], bf[ks], dU[mt][nt]);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bsum[t] += guh[t];
+      }
+      // dh_prev = dh' z + du . U^T   (k over the 3H gate units, gate-major)
+#pragma unroll
+      for (int s = 0; s < K3; ++s) {
+        const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
+        const float b = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = MFMA(Ut[frag_idx(t, s, K3, lofs)], b, acc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dh[t][r] = act ? acc[t][r] : dh[t][r];
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.dh_out + (int64_t)row * H + 16 * t + 4 * g, dh[t]);
+      if constexpr (!FUSE) {
+        // the final state's row of gu has no step (no memset of the whole buffer needed)
+        float* pz = a.gu + (hbase + L) * (3 * H) + 4 * g;
+#pragma unroll
+        for (int t = 0; t < 3 * NT; ++t) st4(pz + 16 * t, f4{0, 0, 0, 0});
       }
     }
-    // dh_prev = dh' z + du . U^T   (k over the 3H gate units, gate-major)
+  }  // tile loop
+  if constexpr (FUSE) {
+    // this wave's partial: rows 0..H-1 = dU (lane: D[16mt + 4g + q][16nt + j]), row H = [0, 0, sum du_h]
+    float* P = a.part + ((int64_t)blockIdx.x * 4 + wave) * (H + 1) * (3 * H);
 #pragma unroll
-    for (int s = 0; s < K3; ++s) {
-      const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
-      const float b = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+    for (int mt = 0; mt < NT; ++mt)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = MFMA(Ut[frag_idx(t, s, K3, lofs)], b, acc[t]);
-    }
+      for (int nt = 0; nt < 3 * NT; ++nt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) P[(16 * mt + 4 * g + q) * (3 * H) + 16 * nt + j] = dU[mt][nt][q];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dh[t][r] = act ? acc[t][r] : dh[t][r];
-  }
-  if (valid) {
+      for (int q = 0; q < 4; ++q) {
+        float s = bsum[t][q];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) st4(a.dh_out + (int64_t)row * H + 16 * t + 4 * g, dh[t]);
-    // the final state's row of gu has no step (no memset of the whole buffer needed)
-    float* pz = a.gu + (hbase + L) * (3 * H) + 4 * g;
+        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);   // over the 16 rows j of group g
+        bsum[t][q] = s;
+      }
+    for (int e = lane; e < 2 * H; e += 64) P[H * (3 * H) + e] = 0.f;
+    if (j == 0) {
 #pragma unroll
-    for (int t = 0; t < 3 * NT; ++t) st4(pz + 16 * t, f4{0, 0, 0, 0});
+      for (int t = 0; t < NT; ++t) st4(P + H * (3 * H) + 2 * H + 16 * t + 4 * g, bsum[t]);
+    }
   }
 }
 
@@ -516,6 +594,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __rest
 // iteration (32 loads in flight), and writes its partial tile.  Chunks are sized so the grid
 // holds ~8k waves; two reduction passes (segments, then final) sum the partials in a fixed order.
 constexpr int kTsWaves = 8192;
+constexpr int kBwdMaxWaves = 4096;   // fused ordered backward: partial slots
 constexpr int kTsSegs = 64;
 
 struct TsPlan {
@@ -752,12 +831,44 @@ bool bwd_shape_supported(int din, int h) {
          (din != 64 || h == 64);
 }
 
+bool seq_bwd_fused_supported(int h) { return h == 16 || h == 32; }
+
+int64_t seq_bwd_partial_floats(int h) { return (int64_t)(kBwdMaxWaves + kTsSegs) * (h + 1) * 3 * h; }
+
+template <int H>
+static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, seq_gru_bwd_kernel<H, true>, 256, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  const int64_t tiles = (a.n_dst + 15) / 16;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>({(tiles + 3) / 4, (int64_t)per_cu * cus, kBwdMaxWaves / 4}));
+  hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_partials_reduce_add(a.part, blocks * 4, H, 3 * H, 1, a.dU, a.db_rec, st);
+}
+
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
   if (a.n_dst == 0) return hipSuccess;
+  if (a.part) {   // fused dU / b_rec(h) gradients
+    if (!a.dU || !a.db_rec) return hipErrorInvalidValue;
+    if (h == 16) return seq_bwd_fused<16>(a, st);
+    if (h == 32) return seq_bwd_fused<32>(a, st);
+    return hipErrorInvalidValue;
+  }
+  if (!a.gu) return hipErrorInvalidValue;
   dim3 grid((unsigned)((a.n_dst + 63) / 64));
-  if (h == 16) hipLaunchKernelGGL((seq_gru_bwd_kernel<16>), grid, dim3(256), 0, st, a);
-  else if (h == 32) hipLaunchKernelGGL((seq_gru_bwd_kernel<32>), grid, dim3(256), 0, st, a);
-  else if (h == 64) hipLaunchKernelGGL((seq_gru_bwd_kernel<64>), grid, dim3(256), 0, st, a);
+  if (h == 16) hipLaunchKernelGGL((seq_gru_bwd_kernel<16, false>), grid, dim3(256), 0, st, a);
+  else if (h == 32) hipLaunchKernelGGL((seq_gru_bwd_kernel<32, false>), grid, dim3(256), 0, st, a);
+  else if (h == 64) hipLaunchKernelGGL((seq_gru_bwd_kernel<64, false>), grid, dim3(256), 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -901,12 +1012,20 @@ hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, i
   hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int64_t size = (int64_t)p.Mx * N;
-  float* seg = part + p.chunks * size;
-  const int S = (int)std::min<int64_t>(kTsSegs, p.chunks);
+  return launch_partials_reduce_add(part, p.chunks, M, N, ones, C, Cb, st);
+}
+
+// C[m][n] (+ Cb[n] for the ones row m = M) += sum over chunks c of part[c][m][n], in chunk order
+// (segment sums, then the segments in order); part holds kTsSegs more chunk slots as scratch
+hipError_t launch_partials_reduce_add(float* part, int64_t nchunks, int M, int N, int ones, float* C, float* Cb,
+                                      hipStream_t st) {
+  const int64_t size = (int64_t)(M + ones) * N;
+  float* seg = part + nchunks * size;
+  const int S = (int)std::min<int64_t>(kTsSegs, nchunks);
   hipLaunchKernelGGL(reduce_seg_kernel, dim3((unsigned)((size + 255) / 256), (unsigned)S), dim3(256), 0, st, part,
-                     p.chunks, size, S, seg);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+                     nchunks, size, S, seg);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(reduce_final_kernel, dim3(blocks_for(size)), dim3(256), 0, st, seg, S, M, N, ones, C, Cb);
   return hipGetLastError();
 }
