@@ -217,3 +217,17 @@ def test_gradients_readout_operations(case):
     rng = np.random.default_rng(5)   # labels shaped like each graph's predictions
     labels = [rng.normal(size=ora.forward_graph(g).size).astype(np.float32) for g in graphs]
     _check(desc, dims, graphs, labels, prm)
+
+
+def test_fused_backward_is_deterministic_and_matches_unfused(monkeypatch):
+    """The ordered backward forms dU from per-wave partials reduced in a fixed order: two runs are
+    bitwise equal, and the result agrees with the du-buffer + row-contraction form (IGN_BWD_FUSE=0)
+    to fp32 reassociation."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "synth50", 24)
+    prm = MPPlan.from_model_info(mi).init_params(11, bias_scale=0.1)
+    g1 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    g2 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    np.testing.assert_array_equal(g1, g2)
+    monkeypatch.setenv("IGN_BWD_FUSE", "0")
+    g3 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    assert np.linalg.norm(g1.astype(np.float64) - g3) <= 1e-5 * np.linalg.norm(g3)
