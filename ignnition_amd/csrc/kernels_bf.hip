@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + NTH * k;
-      if (i < CHF) stage[k] = W2v[(int64_t)nv * CHF + i];
+      if (CHF % NTH == 0 || i < CHF) stage[k] = W2v[(int64_t)nv * CHF + i];   // (no branch when it divides)
     }
     __builtin_amdgcn_sched_barrier(0);
     // opaque lane offset: the LDS reads must not be hoisted out of the chunk loop (registers)
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + NTH * k;
-      if (i < CHF) reinterpret_cast<u4v*>(sw2[cur ^ 1])[i] = stage[k];
+      if (CHF % NTH == 0 || i < CHF) reinterpret_cast<u4v*>(sw2[cur ^ 1])[i] = stage[k];
     }
     __syncthreads();
   }
