@@ -143,6 +143,8 @@ int ign::repack(ign_plan* p) {
     if (dp.pk_bf >= 0)   // layer 1 reads its input from memory (natural k), layer 2 chains from registers
       HIP_TRY(launch_pack_dense_bf16(p->d_params + dp.off_w, p->d_packed + dp.pk_bf, dp.in, dp.out, &dp != &p->dense[0],
                                      p->stream));
+    if (dp.pk_bfn >= 0)
+      HIP_TRY(launch_pack_dense_bf16(p->d_params + dp.off_w, p->d_packed + dp.pk_bfn, dp.in, dp.out, 0, p->stream));
   }
   for (auto& dp : p->dense)
     if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
@@ -180,6 +182,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_SPLIT")) p->sum_split = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
+  if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(7, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
@@ -371,6 +374,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (p->fused_readout && l < 2 && dp.in % 32 == 0 && dp.out % 16 == 0 &&
         readout_bf_supported(p->dense[0].in, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act)) {
       dp.pk_bf = pk;
+      pk = align(pk + 3LL * dp.in * dp.out / 2);
+    }
+    if (dense_bf_supported(dp.in, dp.out)) {
+      dp.pk_bfn = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
     }
   }

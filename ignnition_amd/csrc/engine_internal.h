@@ -47,6 +47,7 @@ struct DenseP {
   int64_t off_w, off_b, pk_w = -1;   // pk_w: forward fragments (fused readout, training readout)
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
   int64_t pk_bf = -1;             // fused readout: split-bf16 A fragments (readout variants 2/3)
+  int64_t pk_bfn = -1;            // training forward: split-bf16 pieces, natural k (dense_bf)
 };
 
 struct MsgNN {                    // message-creation network of one MP source (GM:440-475)
@@ -200,6 +201,7 @@ struct ign_plan {
                                   // (keeps id locality), 2 id order, 3 per-graph sort + XCD-aware
                                   // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
+  bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
   bool sum_split = false;         // plain sums as a gather-only kernel + the GRU step (IGN_SUM_SPLIT=1)
   bool sum_window = false;        // windowed sum aggregation where eligible (IGN_SUM_WINDOW=1): measured

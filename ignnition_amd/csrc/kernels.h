@@ -120,6 +120,11 @@ bool readout_bf_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
                              hipStream_t st);
 hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st);
+// y[r][0..M) = act(x[r] . W + b), split-bf16 (x6) with fp32 accumulation; W packed by
+// launch_pack_dense_bf16 with chained = 0.  K in {32, 64, 128, 256}, M a multiple of 128.
+bool dense_bf_supported(int K, int M);
+hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const void* Wbf, const float* bias, int M,
+                           int act, float* y, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
                                 int out, int act, float* y, hipStream_t st);
 hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,

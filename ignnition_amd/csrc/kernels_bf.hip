@@ -411,6 +411,86 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Row GEMM y[r] = act(x[r] . W + b) on the split-bf16 path (the training forward's Dense layers,
+// whose activations are kept for the backward).  readout_bf's layer-2 loop with the input read
+// from memory: W (packed non-chained, natural k) is staged through LDS in groups of G 16-unit
+// tiles (<= 24 KB), double-buffered; each wave owns two 16-row tiles whose input pieces stay in
+// registers (K / 32 x 3 fragments per tile) and writes act(acc) as 16 B per lane.
+template <int KS, int G, int ACT>
+__global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__ x, int64_t n, int x_stride,
+                                                       const bf8* __restrict__ Wf, const float* __restrict__ bias,
+                                                       int M, float* __restrict__ y) {
+  constexpr int WAVES = 8, RT = 2, NTH = 64 * WAVES;
+  constexpr int CHF = G * KS * 3 * 64;   // bf8 per stage
+  constexpr int PER = (CHF + NTH - 1) / NTH;
+  __shared__ bf8 sw[2][CHF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int j = lane & 15, g = lane >> 4;
+  const u4v* Wv = reinterpret_cast<const u4v*>(Wf);
+  const int NV = M / (16 * G);
+  for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw[0])[i] = Wv[i];
+  const int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * (16 * RT) + j;
+  bf8 xf[RT][KS][3];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int64_t r = r0 + 16 * t;
+    const bool ok = r < n;
+    const float* xr = x + (ok ? r : 0) * (int64_t)x_stride;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+      const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      split_frag(v, xf[t][s]);
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int v = 0; v < NV; ++v) {
+    const int cur = v & 1;
+    const bool more = v + 1 < NV;
+    u4v stage[PER];
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int i = tid + NTH * q;
+        if (CHF % NTH == 0 || i < CHF) stage[q] = Wv[(int64_t)(v + 1) * CHF + i];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int lofs = lane;   // opaque: keeps the LDS reads inside the loop
+    asm volatile("" : "+v"(lofs));
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      const int u = v * G + c;
+      const f4 b = bias ? ld4(bias + 16 * u + 4 * g) : f4{0, 0, 0, 0};
+      f4 acc[RT];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = b;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) split_mfma_rt<6, RT, KS>(sw[cur] + (c * KS + s) * 3 * 64 + lofs, 64, xf, s, acc);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int64_t r = r0 + 16 * t;
+        f4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = act_t<ACT>(acc[t][q]);
+        if (r < n) st4(y + r * M + 16 * u + 4 * g, o);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int i = tid + NTH * q;
+        if (CHF % NTH == 0 || i < CHF) reinterpret_cast<u4v*>(sw[cur ^ 1])[i] = stage[q];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int prefetch, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
   if (!args.Ubf || (h != 32 && h != 64)) return hipErrorInvalidValue;
@@ -475,6 +555,39 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   if (passes == -8) return readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
   if (passes == -9) return readout_bf_din<64, 4, 6, 1, false, 2>(args, W1f, W2f, st);
   return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 8, 6, 1, false, 2>(args, W1f, W2f, st);
+}
+
+
+bool dense_bf_supported(int K, int M) {
+  return (K == 32 || K == 64 || K == 128 || K == 256) && M % 128 == 0 && M > 0;
+}
+
+template <int KS, int G>
+static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const bf8* W, const float* bias, int M, int act,
+                              float* y, hipStream_t st) {
+  const dim3 grid((unsigned)((n + 255) / 256)), block(512);
+  switch (act) {
+    case IGN_K_ACT_SELU: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_SELU>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
+    case IGN_K_ACT_RELU: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_RELU>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
+    case IGN_K_ACT_TANH: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_TANH>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
+    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_SIGMOID>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
+    default: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_LINEAR>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const void* Wbf, const float* bias, int M,
+                           int act, float* y, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!dense_bf_supported(K, M) || x_stride % 4 || !Wbf) return hipErrorInvalidValue;
+  const bf8* W = static_cast<const bf8*>(Wbf);
+  // stages of <= 24 KB: G 16-unit tiles of K x 16 x 3 pieces (M % 128 == 0: G divides M / 16)
+  switch (K) {
+    case 32: return dense_bf_ks<1, 8>(x, n, x_stride, W, bias, M, act, y, st);
+    case 64: return dense_bf_ks<2, 4>(x, n, x_stride, W, bias, M, act, y, st);
+    case 128: return dense_bf_ks<4, 2>(x, n, x_stride, W, bias, M, act, y, st);
+    default: return dense_bf_ks<8, 1>(x, n, x_stride, W, bias, M, act, y, st);
+  }
 }
 
 hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st) {

@@ -63,6 +63,7 @@ struct TrainState {
   std::vector<float*> act;                // readout activations of layers 0 .. L-2
   float* dz[2] = {nullptr, nullptr};
   float* part = nullptr;
+  float* bsum = nullptr;                  // [192]: column sums of ga (fused ordered backward)
   float* ro_x = nullptr;                  // concatenated readout input (several input entities)
   float* dro = nullptr;
   float* dmsg = nullptr;                  // message networks: d(messages) [edges][out]
@@ -441,7 +442,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         (rcat_n && (rc = talloc(t.get(), &t->rcat, rcat_n))) || (ties_n && (rc = talloc(t.get(), &t->rties, ties_n))))
       return rc;
   }
-  if ((rc = talloc(t.get(), &t->part, part_n))) return rc;
+  if ((rc = talloc(t.get(), &t->part, part_n)) || (rc = talloc(t.get(), &t->bsum, 3 * 64))) return rc;
   b->train = t.release();
   return IGN_OK;
 }
@@ -525,8 +526,12 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
   for (size_t l = 0; l < p->dense.size(); ++l) {
     const DenseP& d = p->dense[l];
     float* o = l + 1 == p->dense.size() ? b->d_pred : t->act[l];
-    HIP_TRY(launch_dense_fwd(in, P, d.in, in_stride, d.pk_w >= 0 ? p->d_packed + d.pk_w : nullptr,
-                             p->d_params + d.off_w, d.use_bias ? p->d_params + d.off_b : nullptr, d.out, d.act, o, st));
+    if (p->train_dense_bf && d.pk_bfn >= 0 && in_stride % 4 == 0)   // split-bf16, fp32-exact operands
+      HIP_TRY(launch_dense_bf(in, P, d.in, in_stride, p->d_packed + d.pk_bfn, d.use_bias ? p->d_params + d.off_b : nullptr,
+                              d.out, d.act, o, st));
+    else
+      HIP_TRY(launch_dense_fwd(in, P, d.in, in_stride, d.pk_w >= 0 ? p->d_packed + d.pk_w : nullptr,
+                               p->d_params + d.off_w, d.use_bias ? p->d_params + d.off_b : nullptr, d.out, d.act, o, st));
     in = o;
     in_stride = d.out;
   }
@@ -694,12 +699,16 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
         a.dU = grk;
         a.db_rec = gb + H3;
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
-        HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, 2 * H, t->part, gb + H3, st));
+        // one pass of column sums over ga feeds b_in and the z / r parts of b_rec
+        HIP_TRY(hipMemsetAsync(t->bsum, 0, H3 * sizeof(float), st));
+        HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, t->bsum, st));
+        HIP_TRY(launch_axpy(gb, t->bsum, 1.f, H3, st));
+        HIP_TRY(launch_axpy(gb + H3, t->bsum, 1.f, 2 * H, st));
       } else {
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
         HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, gb + H3, st));
+        HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, gb, st));
       }
-      HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, gb, st));
       for (size_t s = 0; s < mp.src.size(); ++s) {
         const int se = mp.src[s].entity;
         HIP_TRY(launch_csr_gather_add(t->dtab, mt.trows[s], mt.tptr[s], mt.tidx[s], t->ga, H3, 0, st));
