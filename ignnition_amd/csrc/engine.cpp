@@ -145,6 +145,8 @@ int ign::repack(ign_plan* p) {
                                      p->stream));
     if (dp.pk_bfn >= 0)
       HIP_TRY(launch_pack_dense_bf16(p->d_params + dp.off_w, p->d_packed + dp.pk_bfn, dp.in, dp.out, 0, p->stream));
+    if (dp.pk_bft >= 0)
+      HIP_TRY(launch_pack_dense_bf16_t(p->d_params + dp.off_w, p->d_packed + dp.pk_bft, dp.in, dp.out, p->stream));
   }
   for (auto& dp : p->dense)
     if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
@@ -378,6 +380,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     }
     if (dense_bf_supported(dp.in, dp.out)) {
       dp.pk_bfn = pk;
+      pk = align(pk + 3LL * dp.in * dp.out / 2);
+    }
+    if (dense_bf_supported(dp.out, dp.in)) {
+      dp.pk_bft = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
     }
   }

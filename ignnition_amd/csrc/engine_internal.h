@@ -48,6 +48,7 @@ struct DenseP {
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
   int64_t pk_bf = -1;             // fused readout: split-bf16 A fragments (readout variants 2/3)
   int64_t pk_bfn = -1;            // training forward: split-bf16 pieces, natural k (dense_bf)
+  int64_t pk_bft = -1;            // training backward: split-bf16 pieces of W^T (dense_bf_t)
 };
 
 struct MsgNN {                    // message-creation network of one MP source (GM:440-475)

@@ -125,6 +125,11 @@ hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, in
 bool dense_bf_supported(int K, int M);
 hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const void* Wbf, const float* bias, int M,
                            int act, float* y, hipStream_t st);
+// the backward row GEMM out[r][0..M) (+)= (dz[r] . W^T) * act'(aprev[r]) (act < 0: no act'), dz [n][K]
+// dense; W^T packed by launch_pack_dense_bf16_t(W [M][K])
+hipError_t launch_dense_bf_t(const float* dz, int64_t n, int K, const void* Wtbf, int M, float* out, int accumulate,
+                             int act, const float* aprev, hipStream_t st);
+hipError_t launch_pack_dense_bf16_t(const float* W, void* out, int IN, int OUT, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
                                 int out, int act, float* y, hipStream_t st);
 hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,

@@ -220,8 +220,9 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 // = 32: 48 KB) stays in LDS for the block.  One wave = 16 rows: the layer-1 activations are
 // split once into 3 x 8 B fragments (96 VGPRs, accumulator layout = chained k order) and feed
 // all 16 chunks; layer 2 is contracted with w3 per chunk and never stored.
+// trans: the packed matrix is W^T of a row-major W [OUT][IN] (element (k, n) = W[n][k])
 __global__ void pack_dense_bf16_kernel(const float* __restrict__ W, uint16_t* __restrict__ out, int IN, int OUT,
-                                       int chained) {
+                                       int chained, int trans) {
   const int KS = IN / 32;
   const int64_t total = (int64_t)(OUT / 16) * KS * 3 * 512;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -233,7 +234,8 @@ __global__ void pack_dense_bf16_kernel(const float* __restrict__ W, uint16_t* __
     const int g = lane >> 4;
     const int k = chained ? 16 * (2 * s + (j >> 2)) + 4 * g + (j & 3) : 32 * s + 8 * g + j;
     float p[3];
-    split3(W[(int64_t)k * OUT + 16 * u + (lane & 15)], p[0], p[1], p[2]);
+    const int n = 16 * u + (lane & 15);
+    split3(trans ? W[(int64_t)n * IN + k] : W[(int64_t)k * OUT + n], p[0], p[1], p[2]);
     out[e] = (uint16_t)(__float_as_uint(p[piece]) >> 16);
   }
 }
@@ -412,16 +414,32 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 }
 
 
+__device__ __forceinline__ float act_grad_out(float a, int act) {   // act' through the output a
+  switch (act) {
+    case IGN_K_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case IGN_K_ACT_SELU: {
+      const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
+      return a > 0.f ? lam : a + la;
+    }
+    case IGN_K_ACT_SIGMOID: return a * (1.f - a);
+    case IGN_K_ACT_TANH: return 1.f - a * a;
+    default: return 1.f;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Row GEMM y[r] = act(x[r] . W + b) on the split-bf16 path (the training forward's Dense layers,
 // whose activations are kept for the backward).  readout_bf's layer-2 loop with the input read
 // from memory: W (packed non-chained, natural k) is staged through LDS in groups of G 16-unit
 // tiles (<= 24 KB), double-buffered; each wave owns two 16-row tiles whose input pieces stay in
 // registers (K / 32 x 3 fragments per tile) and writes act(acc) as 16 B per lane.
-template <int KS, int G, int ACT>
+// BWD: the backward row GEMM instead, y[r] (+)= (x[r] . W^T) * act'(aprev[r]) with W^T packed
+// (row_gemm_t's contract; bias unused, ACT = the activation whose derivative is applied).
+template <int KS, int G, int ACT, bool BWD = false>
 __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__ x, int64_t n, int x_stride,
                                                        const bf8* __restrict__ Wf, const float* __restrict__ bias,
-                                                       int M, float* __restrict__ y) {
+                                                       int M, float* __restrict__ y, const float* __restrict__ aprev,
+                                                       int accumulate) {
   constexpr int WAVES = 8, RT = 2, NTH = 64 * WAVES;
   constexpr int CHF = G * KS * 3 * 64;   // bf8 per stage
   constexpr int PER = (CHF + NTH - 1) / NTH;
@@ -474,10 +492,19 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         const int64_t r = r0 + 16 * t;
+        if (r >= n) continue;
+        float* po = y + r * M + 16 * u + 4 * g;
         f4 o;
+        if constexpr (BWD) {
+          const f4 av = aprev ? ld4(aprev + r * M + 16 * u + 4 * g) : f4{0, 0, 0, 0};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = act_t<ACT>(acc[t][q]);
-        if (r < n) st4(y + r * M + 16 * u + 4 * g, o);
+          for (int q = 0; q < 4; ++q) o[q] = aprev ? acc[t][q] * act_grad_out(av[q], ACT) : acc[t][q];
+          if (accumulate) o += ld4(po);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = act_t<ACT>(acc[t][q]);
+        }
+        st4(po, o);
       }
     }
     if (more) {
@@ -562,38 +589,60 @@ bool dense_bf_supported(int K, int M) {
   return (K == 32 || K == 64 || K == 128 || K == 256) && M % 128 == 0 && M > 0;
 }
 
-template <int KS, int G>
+template <int KS, int G, bool BWD>
 static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const bf8* W, const float* bias, int M, int act,
-                              float* y, hipStream_t st) {
+                              float* y, const float* aprev, int accumulate, hipStream_t st) {
   const dim3 grid((unsigned)((n + 255) / 256)), block(512);
+#define DBF(A) hipLaunchKernelGGL((dense_bf_kernel<KS, G, A, BWD>), grid, block, 0, st, x, n, x_stride, W, bias, M, y, aprev, accumulate)
   switch (act) {
-    case IGN_K_ACT_SELU: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_SELU>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
-    case IGN_K_ACT_RELU: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_RELU>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
-    case IGN_K_ACT_TANH: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_TANH>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
-    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_SIGMOID>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
-    default: hipLaunchKernelGGL((dense_bf_kernel<KS, G, IGN_K_ACT_LINEAR>), grid, block, 0, st, x, n, x_stride, W, bias, M, y); break;
+    case IGN_K_ACT_SELU: DBF(IGN_K_ACT_SELU); break;
+    case IGN_K_ACT_RELU: DBF(IGN_K_ACT_RELU); break;
+    case IGN_K_ACT_TANH: DBF(IGN_K_ACT_TANH); break;
+    case IGN_K_ACT_SIGMOID: DBF(IGN_K_ACT_SIGMOID); break;
+    default: DBF(IGN_K_ACT_LINEAR); break;
   }
+#undef DBF
   return hipGetLastError();
+}
+
+template <bool BWD>
+static hipError_t dense_bf_any(const float* x, int64_t n, int K, int x_stride, const bf8* W, const float* bias, int M,
+                               int act, float* y, const float* aprev, int accumulate, hipStream_t st) {
+  // stages of <= 24 KB: G 16-unit tiles of K x 16 x 3 pieces (M % 128 == 0: G divides M / 16)
+  switch (K) {
+    case 32: return dense_bf_ks<1, 8, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    case 64: return dense_bf_ks<2, 4, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    case 128: return dense_bf_ks<4, 2, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    default: return dense_bf_ks<8, 1, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+  }
 }
 
 hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const void* Wbf, const float* bias, int M,
                            int act, float* y, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (!dense_bf_supported(K, M) || x_stride % 4 || !Wbf) return hipErrorInvalidValue;
-  const bf8* W = static_cast<const bf8*>(Wbf);
-  // stages of <= 24 KB: G 16-unit tiles of K x 16 x 3 pieces (M % 128 == 0: G divides M / 16)
-  switch (K) {
-    case 32: return dense_bf_ks<1, 8>(x, n, x_stride, W, bias, M, act, y, st);
-    case 64: return dense_bf_ks<2, 4>(x, n, x_stride, W, bias, M, act, y, st);
-    case 128: return dense_bf_ks<4, 2>(x, n, x_stride, W, bias, M, act, y, st);
-    default: return dense_bf_ks<8, 1>(x, n, x_stride, W, bias, M, act, y, st);
-  }
+  return dense_bf_any<false>(x, n, K, x_stride, static_cast<const bf8*>(Wbf), bias, M, act, y, nullptr, 0, st);
+}
+
+hipError_t launch_dense_bf_t(const float* dz, int64_t n, int K, const void* Wtbf, int M, float* out, int accumulate,
+                             int act, const float* aprev, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!dense_bf_supported(K, M) || !Wtbf) return hipErrorInvalidValue;
+  return dense_bf_any<true>(dz, n, K, K, static_cast<const bf8*>(Wtbf), nullptr, M, act < 0 ? IGN_K_ACT_LINEAR : act,
+                            out, act < 0 ? nullptr : aprev, accumulate, st);
+}
+
+hipError_t launch_pack_dense_bf16_t(const float* W, void* out, int IN, int OUT, hipStream_t st) {
+  // pieces of W^T ([OUT][IN] contraction over OUT) for launch_dense_bf_t; W is [IN][OUT]
+  if (OUT % 32 || IN % 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_dense_bf16_kernel, dim3(128), dim3(256), 0, st, W, static_cast<uint16_t*>(out), OUT, IN, 0, 1);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st) {
   if (IN % 32 || OUT % 16) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pack_dense_bf16_kernel, dim3(128), dim3(256), 0, st, W, static_cast<uint16_t*>(out), IN, OUT,
-                     chained);
+                     chained, 0);
   return hipGetLastError();
 }
 

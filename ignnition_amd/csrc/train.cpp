@@ -586,7 +586,9 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       out = grad_of(p->ro_in[0]);
       acc = 1;
     }
-    if (d.pk_wt >= 0)
+    if (p->train_dense_bf && d.pk_bft >= 0)   // split-bf16, fp32-exact operands
+      HIP_TRY(launch_dense_bf_t(t->dz[zi], P, d.out, p->d_packed + d.pk_bft, d.in, out, acc, act, aprev, st));
+    else if (d.pk_wt >= 0)
       HIP_TRY(launch_row_gemm_t(t->dz[zi], P, d.out, p->d_packed + d.pk_wt, d.in, out, acc, act, aprev, st));
     else
       HIP_TRY(launch_row_gemm_t_generic(t->dz[zi], P, d.out, p->d_params + d.off_w, d.in, out, acc, act, aprev, st));
