@@ -583,6 +583,30 @@ __global__ void row_gemm_t_generic_kernel(const float* __restrict__ in, int64_t 
   }
 }
 
+// K = 1 (the backward of a 1-unit output layer): out[r][m] (+)= in[r] Mat[m] act'(aprev[r][m]),
+// four columns per thread (16-B accesses); the same per-element arithmetic as the generic kernel
+__global__ void row_outer_t_kernel(const float* __restrict__ in, int64_t n, const float* __restrict__ Mat, int M,
+                                   float* __restrict__ out, int accumulate, int act, const float* __restrict__ aprev) {
+  const int M4 = M >> 2;
+  const int64_t total = n * M4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / M4;
+    const int m = (int)(e - r * M4) * 4;
+    const float x = in[r];
+    const f4 w = ld4(Mat + m);
+    const f4 av = act >= 0 ? ld4(aprev + r * M + m) : f4{0, 0, 0, 0};
+    f4 o = accumulate ? ld4(out + r * M + m) : f4{0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float s = 0.f;
+      s += x * w[q];
+      if (act >= 0) s *= act_grad(av[q], act);
+      o[q] = accumulate ? o[q] + s : s;
+    }
+    st4(out + r * M + m, o);
+  }
+}
+
 __global__ void split_cols_add_kernel(float* __restrict__ dst, int64_t n, int width, const float* __restrict__ src,
                                       int src_stride, int col0) {
   const int64_t total = n * width;
@@ -989,6 +1013,11 @@ hipError_t launch_row_gemm_t(const float* in, int64_t n, int K, const float* Ap,
 hipError_t launch_row_gemm_t_generic(const float* in, int64_t n, int K, const float* Mat, int M, float* out,
                                      int accumulate, int act, const float* aprev, hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (K == 1 && M % 4 == 0) {
+    hipLaunchKernelGGL(row_outer_t_kernel, dim3(blocks_for(n * (M / 4))), dim3(256), 0, st, in, n, Mat, M, out,
+                       accumulate, act, aprev);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(row_gemm_t_generic_kernel, dim3(blocks_for(n * M)), dim3(256), 0, st, in, n, K, Mat, M, out,
                      accumulate, act, aprev);
   return hipGetLastError();
