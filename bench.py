@@ -242,14 +242,17 @@ def main():
             cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
     seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "4"))
     ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "2"))
+    sum_v = int(os.environ.get("IGN_SUM_VARIANT", "7"))
     split = lambda v, six: ("split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
                             % (6 if six else 9)) if v else "f32 MFMA"
     contraction = {"ordered_update_hU": split(seq_v >= 4, seq_v == 4),
                    "readout": split(ro_v in (2, 3, 4), ro_v != 3),
-                   "sum_update_and_projection": "f32 MFMA"}
+                   # sum variant 7 (default): split-bf16 x.W / h.U when DIN = H = 64 (the synthetic graph)
+                   "sum_update": split(plan.hidden[0] == 64 and sum_v == 7, True),
+                   "projection": "f32 MFMA"}
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,
-                                                                                              "sum_update_and_projection")]
+                                                                                              "sum_update")]
     line = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,

@@ -114,6 +114,8 @@ int ign::repack(ign_plan* p) {
                             p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
                             p->stream));
     if (cp.pk_ubf >= 0) HIP_TRY(launch_pack_u_bf16(p->d_params + cp.off_rk, p->d_packed + cp.pk_ubf, cp.H, p->stream));
+    if (cp.pk_wbf >= 0)
+      HIP_TRY(launch_pack_w_bf16(p->d_params + cp.off_k, p->d_packed + cp.pk_wbf, cp.din, cp.H, p->stream));
     if (cp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
     if (cp.pk_ut >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
   }
@@ -174,12 +176,12 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(6, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(7, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
   if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
-  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(6, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(7, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_SPLIT")) p->sum_split = atoi(v) != 0;
@@ -366,6 +368,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.pk_u = pk; pk = align(pk + 3LL * cp.H * cp.H);
     cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
     if (pack_u_bf16_floats(cp.H)) { cp.pk_ubf = pk; pk = align(pk + pack_u_bf16_floats(cp.H)); }
+    if (cp.din == 64 && cp.H == 64) { cp.pk_wbf = pk; pk = align(pk + pack_w_bf16_floats(cp.din, cp.H)); }
   }
   for (size_t l = 0; l < p->dense.size(); ++l) {
     DenseP& dp = p->dense[l];
@@ -1193,6 +1196,10 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count,
                    p->xcd_remap || p->sum_order == 3};
       if (mp.aggr == IGN_AGGR_ATTENTION) a.msg_w = mb.d_msg_w;
+      if (mp.aggr == IGN_AGGR_SUM && cp.pk_wbf >= 0 && cp.pk_ubf >= 0 && mp.din == cp.din && !mp.feature_concat) {
+        a.Wbf = p->d_packed + cp.pk_wbf;
+        a.Ubf = p->d_packed + cp.pk_ubf;
+      }
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
         a.conv_kp = p->d_packed + p->pk_conv;
         a.conv_act = mp.act;

@@ -37,6 +37,7 @@ struct CellP {
   int64_t off_k, off_rk, off_b;   // raw Keras-layout params
   int64_t pk_w, pk_u, pk_b;       // packed fragments (in d_packed)
   int64_t pk_wt = -1, pk_ut = -1; // backward: unscaled W^T / U^T fragments (pack_a)
+  int64_t pk_wbf = -1;            // split-bf16 input-kernel fragments (sum variant 7, DIN = H = 64)
   int64_t pk_ubf = -1;            // split-bf16 recurrent-kernel fragments (seq variants 4/5)
   bool used = false;
 };
@@ -194,7 +195,8 @@ struct ign_plan {
   // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
   bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
-  int sum_variant = 3;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS,
+  int sum_variant = 7;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS,
+                                  // 7 = LDS + split-bf16 x.W / h.U (kernels_bf.hip),
                                   // 3 = LDS + 4 messages in flight per lane, 4 = warp-specialised
                                   // (producer waves gather, consumer waves MFMA), 5 = LDS + header /
                                   // index prefetch one tile ahead; IGN_SUM_VARIANT

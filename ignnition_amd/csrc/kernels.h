@@ -50,6 +50,8 @@ struct SumGruArgs {
   const float* conv_kp = nullptr;  // convolution: packed kernel; x = act((sum h_src . K + h) / deg)
   int conv_act = 0;
   float* sum_save = nullptr;       // training, convolution: [rows][DIN] message sums before K
+  const void* Wbf = nullptr;       // split-bf16 pieces of W / U (pack_w_bf16 / pack_u_bf16): variant 7
+  const void* Ubf = nullptr;
 };
 
 // Attention weights (AUX:287-343): per (graph, position) group of dense cells, the axis-0 softmax
@@ -94,6 +96,11 @@ hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int pref
 // recurrent kernel -> split-bf16 A fragments for seq variants 4/5 (H = 32 or 64); floats used: 9 H^2 / 2
 hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H * H / 2 : 0; }
+// pieces of a [K][3H] input kernel (K % 32 == 0) for the split-bf16 sum update
+hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream_t st);
+inline int64_t pack_w_bf16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 9LL * K * H / 2 : 0; }
+// split-bf16 sum update (DIN = H = 64, no message weights / convolution); hipErrorInvalidValue otherwise
+hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 
 // Windowed sum (AUX:254-262 for single-source sum MPs of graph-local batches): one workgroup per

@@ -1723,6 +1723,8 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
 #undef SUM_CASE
   if (din == 64 && h == 64) {
     if (mode != 0) return hipErrorInvalidValue;
+    if (variant == 7 && args.Wbf && args.Ubf) return launch_sum_gru_bf(args, din, h, st);
+    if (variant == 7) variant = 3;
     if (variant == 5) {
       constexpr int WV = 12;
       auto kern = sum_gru_pf_kernel<64, 64, WV, 4, 16>;

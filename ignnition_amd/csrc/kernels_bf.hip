@@ -43,8 +43,9 @@ int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) {
 // B[k][n = l&15].  The k order is permuted, kperm(s, g, j) = 16 (2s + (j>>2)) + 4g + (j&3), so
 // the B fragment of k-step s is exactly registers (2s .. 2s+1) of the lane's accumulator tiles:
 // the state still never leaves the lane.
-__global__ void pack_u_bf16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out, int H) {
-  const int NT = H / 16, KS = H / 32;
+// K: rows of the matrix (H for the recurrent kernel U, DIN for the input kernel W of the sum update)
+__global__ void pack_u_bf16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out, int K, int H) {
+  const int NT = H / 16, KS = K / 32;
   const int64_t total = 9LL * NT * KS * 64 * 8;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
@@ -209,6 +210,168 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
     }
   }  // tile loop
+}
+
+// ---------------------------------------------------------------------------------------------
+// Variant 7 of the sum update (kernels.hip sum_gru_lds, DIN = H = 64): the same persistent,
+// in-degree-sorted tiles and message gather, with x.W and h.U on the bf16 matrix path,
+// fp32-exact (6 piece products).  At 64/64 the f32 form issues 384 f32 MFMAs per
+// 16 rows (12.3k cycles); this one 288 bf16 MFMAs (~4.6k) plus the splits of x and h.
+// W and U pieces (147 KB) are staged once per block in LDS: one 12-wave block per CU.
+__device__ __forceinline__ const float* src_row_bf(const SrcBases& sb, uint32_t code, int din) {
+  const uint32_t slot = code >> IGN_SLOT_SHIFT;
+  const float* b = sb.base[0];
+  if (slot == 1) b = sb.base[1];
+  if (slot == 2) b = sb.base[2];
+  if (slot == 3) b = sb.base[3];
+  return b + (int64_t)(code & IGN_ROW_MASK) * din;
+}
+
+// B fragments of a lane's values v[2 * KS] (chained k order): the three exact bf16 pieces
+template <int KS>
+__device__ __forceinline__ void split_frags(const f4* v, bf8 (&f)[3][KS]) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    u4v w0, w1, w2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e0 = 2 * q, e1 = 2 * q + 1;
+      float a0, a1, a2, b0, b1, b2;
+      split3(v[2 * s + (e0 >> 2)][e0 & 3], a0, a1, a2);
+      split3(v[2 * s + (e1 >> 2)][e1 & 3], b0, b1, b2);
+      w0[q] = pack_hi16(a0, b0);
+      w1[q] = pack_hi16(a1, b1);
+      w2[q] = pack_hi16(a2, b2);
+    }
+    f[0][s] = __builtin_bit_cast(bf8, w0);
+    f[1][s] = __builtin_bit_cast(bf8, w1);
+    f[2][s] = __builtin_bit_cast(bf8, w2);
+  }
+}
+
+template <int DIN, int H, int WAVES, int GU>
+__global__ __launch_bounds__(64 * WAVES) void sum_gru_bf_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, KX = DIN / 32, KH = H / 32;
+  constexpr int WF = 9 * NT * KX * 64, UF = 9 * NT * KH * 64;   // bf8 fragments (16 B)
+  __shared__ bf8 sW[WF];
+  __shared__ bf8 sU[UF];
+  __shared__ float sbias[4 * H];
+  {
+    const u4v* gW = static_cast<const u4v*>(a.Wbf);
+    const u4v* gU = static_cast<const u4v*>(a.Ubf);
+    u4v* dW = reinterpret_cast<u4v*>(sW);
+    u4v* dU = reinterpret_cast<u4v*>(sU);
+    for (int i = threadIdx.x; i < WF; i += 64 * WAVES) dW[i] = gW[i];
+    for (int i = threadIdx.x; i < UF; i += 64 * WAVES) dU[i] = gU[i];
+    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) sbias[i] = a.bias[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * WAVES + wave; tile < n_tiles; tile += (int64_t)gridDim.x * WAVES) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+    const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    f4 x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+    // the same summation order as sum_gru_lds (GU at a time, then pairs, then singles)
+    int64_t m = m0;
+    for (; m + GU <= m1; m += GU) {
+      f4 v[GU][NC];
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const float* p = src_row_bf(a.src, a.msg_src[m + u], DIN);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] += v[u][c];
+    }
+    for (; m + 2 <= m1; m += 2) {
+      const float* p0 = src_row_bf(a.src, a.msg_src[m], DIN);
+      const float* p1 = src_row_bf(a.src, a.msg_src[m + 1], DIN);
+      f4 v0[NC], v1[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        v0[c] = ld4(p0 + 16 * c + 4 * g);
+        v1[c] = ld4(p1 + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
+    }
+    for (; m < m1; ++m) {
+      const float* p = src_row_bf(a.src, a.msg_src[m], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+    }
+    if (a.x_save && valid) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+    }
+    bf8 xf[3][KX], hf[3][KH];
+    split_frags<KX>(x, xf);
+    split_frags<KH>(h, hf);
+    int lofs = lane;                    // opaque: keeps the fragment reads inside the tile loop
+    asm volatile("" : "+v"(lofs));
+    f4 hn[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int u0 = 16 * t + 4 * g;
+      f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
+      f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
+      f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
+      f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
+      // piece products grouped by weight piece, small first; x6 drops pu + ph > 2
+#pragma unroll
+      for (int pu = 2; pu >= 0; --pu) {
+#pragma unroll
+        for (int s = 0; s < KX; ++s) {
+          const bf8 wz = sW[(((pu * 3 + 0) * NT + t) * KX + s) * 64 + lofs];
+          const bf8 wr = sW[(((pu * 3 + 1) * NT + t) * KX + s) * 64 + lofs];
+          const bf8 wh = sW[(((pu * 3 + 2) * NT + t) * KX + s) * 64 + lofs];
+#pragma unroll
+          for (int ph = 2 - pu; ph >= 0; --ph) {
+            az = MFMA_BF(wz, xf[ph][s], az);
+            ar = MFMA_BF(wr, xf[ph][s], ar);
+            ax = MFMA_BF(wh, xf[ph][s], ax);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < KH; ++s) {
+          const bf8 wz = sU[(((pu * 3 + 0) * NT + t) * KH + s) * 64 + lofs];
+          const bf8 wr = sU[(((pu * 3 + 1) * NT + t) * KH + s) * 64 + lofs];
+          const bf8 wh = sU[(((pu * 3 + 2) * NT + t) * KH + s) * 64 + lofs];
+#pragma unroll
+          for (int ph = 2 - pu; ph >= 0; --ph) {
+            az = MFMA_BF(wz, hf[ph][s], az);
+            ar = MFMA_BF(wr, hf[ph][s], ar);
+            ah = MFMA_BF(wh, hf[ph][s], ah);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[r]);
+        const float rr = sig2_(ar[r]);
+        const float c = tanh2_(ax[r] + rr * ah[r]);
+        hn[t][r] = c + z * (h[t][r] - c);
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -648,7 +811,23 @@ hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, in
 
 hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st) {
   if (H != 32 && H != 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_u_bf16_kernel, dim3(64), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H);
+  hipLaunchKernelGGL(pack_u_bf16_kernel, dim3(64), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H, H);
   return hipGetLastError();
 }
 
+hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream_t st) {
+  if ((H != 32 && H != 64) || K % 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_u_bf16_kernel, dim3(64), dim3(256), 0, st, W, static_cast<uint16_t*>(out), K, H);
+  return hipGetLastError();
+}
+
+
+hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  if (din != 64 || h != 64 || !args.Wbf || !args.Ubf || args.msg_w || args.conv_kp) return hipErrorInvalidValue;
+  constexpr int WV = 12;
+  auto kern = sum_gru_bf_kernel<64, 64, WV, 4>;
+  const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
+  hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
+  return hipGetLastError();
+}

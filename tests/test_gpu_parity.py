@@ -294,6 +294,32 @@ def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
         assert v <= max(4 * errs["2/1"], 1e-6), errs
 
 
+def test_split_bf16_sum_update_is_fp32_accurate(monkeypatch):
+    """Sum-update variant 7 (x.W and h.U from exact 3-piece bf16 splits, 6 piece products, the
+    default at DIN = H = 64) vs the f32-MFMA variant 3 on the synthetic graph's model: both
+    inside the parity tolerance vs the float64 oracle, the split form within 4x of the f32 error
+    (or 1e-6); same summation order of the messages, so repeated runs are bitwise equal."""
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=3000, iterations=4, window=64)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(7, bias_scale=0.2)
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    errs, outs = {}, {}
+    for v in ("3", "7"):
+        monkeypatch.setenv("IGN_SUM_VARIANT", v)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        out = b.forward().reshape(-1)
+        np.testing.assert_array_equal(out, b.forward().reshape(-1))
+        b.close()
+        eng.close()
+        _close(out, ref)
+        errs[v], outs[v] = _scaled_err(out, ref), out
+    print("max scaled error vs float64 oracle (sum variant):", errs)
+    assert not np.array_equal(outs["3"], outs["7"])   # the variant switch took effect
+    assert errs["7"] <= max(4 * errs["3"], 1e-6), errs
+
+
 def test_timing_kinds_mask():
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
     plan = MPPlan.from_model_info(mi)
