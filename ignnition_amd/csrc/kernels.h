@@ -101,6 +101,9 @@ hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream
 inline int64_t pack_w_bf16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 9LL * K * H / 2 : 0; }
 // split-bf16 sum update (DIN = H = 64, no message weights / convolution); hipErrorInvalidValue otherwise
 hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t st);
+// split-bf16 form of the training row contraction (train_kernels.hip tsgemm; same grid and partials)
+hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
+                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 
 // Windowed sum (AUX:254-262 for single-source sum MPs of graph-local batches): one workgroup per

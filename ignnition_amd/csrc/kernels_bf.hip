@@ -375,6 +375,120 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_bf_kernel(SumGruArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Weight-gradient row contraction part[chunk] = sum_r A[r]^T B[r] (train_kernels.hip tsgemm) on
+// the bf16 matrix path, fp32-exact (x6 piece products).  Rows sit on the k axis of
+// v_mfma_f32_16x16x32_bf16: lane (c = l&15, g = l>>4) holds rows r + 8g .. r + 8g + 7 of column
+// m0 + 16x + c (A) / n0 + 16y + c (B), so the loads stay 64-B row segments as in tsgemm.
+// One wave = one 64x64 output tile; the ones column (bias gradient) is a VALU column sum of B.
+__global__ __launch_bounds__(256) void tsgemm_bf_kernel(const float* __restrict__ A, int lda,
+                                                        const float* __restrict__ B, int ldb, int64_t n_rows, int M,
+                                                        int N, int ones, int64_t chunk, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int Mx = M + ones;
+  const int tiles_m = (Mx + 63) / 64, tiles_n = (N + 63) / 64;
+  const int tile = blockIdx.y * (blockDim.x >> 6) + wave;
+  if (tile >= tiles_m * tiles_n) return;
+  const int m0 = (tile / tiles_n) * 64, n0 = (tile % tiles_n) * 64;
+  const int na = max(0, min(4, (M - m0 + 15) / 16)), nb = min(4, (N - n0 + 15) / 16);
+  const bool has_ones = ones && M >= m0 && M < m0 + 64;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  const int64_t r1 = std::min<int64_t>(n_rows, r0 + chunk);
+  const int g = lane >> 4, c = lane & 15;
+  f4 acc[4][4];
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f4{0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; r += 32) {
+    float bv[4][8];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int n = n0 + 16 * y + c;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int64_t rr = r + 8 * g + jj;
+        bv[y][jj] = (y < nb && rr < r1 && n < N) ? B[rr * ldb + n] : 0.f;
+      }
+    }
+    float av[4][8];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int m = m0 + 16 * x + c;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int64_t rr = r + 8 * g + jj;
+        av[x][jj] = (x < na && rr < r1 && m < M) ? A[rr * lda + m] : 0.f;
+      }
+    }
+    bf8 bp[4][3];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      u4v w0, w1, w2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a0, a1, a2, b0, b1, b2;
+        split3(bv[y][2 * q], a0, a1, a2);
+        split3(bv[y][2 * q + 1], b0, b1, b2);
+        w0[q] = pack_hi16(a0, b0);
+        w1[q] = pack_hi16(a1, b1);
+        w2[q] = pack_hi16(a2, b2);
+      }
+      bp[y][0] = __builtin_bit_cast(bf8, w0);
+      bp[y][1] = __builtin_bit_cast(bf8, w1);
+      bp[y][2] = __builtin_bit_cast(bf8, w2);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) csum[y] += bv[y][jj];
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      if (x >= na) continue;
+      u4v w0, w1, w2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a0, a1, a2, b0, b1, b2;
+        split3(av[x][2 * q], a0, a1, a2);
+        split3(av[x][2 * q + 1], b0, b1, b2);
+        w0[q] = pack_hi16(a0, b0);
+        w1[q] = pack_hi16(a1, b1);
+        w2[q] = pack_hi16(a2, b2);
+      }
+      const bf8 ap[3] = {__builtin_bit_cast(bf8, w0), __builtin_bit_cast(bf8, w1), __builtin_bit_cast(bf8, w2)};
+#pragma unroll
+      for (int pa = 2; pa >= 0; --pa)
+#pragma unroll
+        for (int pb = 2 - pa; pb >= 0; --pb)
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+            if (y < nb) acc[x][y] = MFMA_BF(ap[pa], bp[y][pb], acc[x][y]);
+    }
+  }
+  float* P = part + (int64_t)blockIdx.x * Mx * N;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int n = n0 + 16 * y + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m0 + 16 * x + 4 * g + q;
+        if (x < na && y < nb && m < M && n < N) P[(int64_t)m * N + n] = acc[x][y][q];
+      }
+    }
+  if (has_ones) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {      // sum over the 4 row groups g (lanes c, c+16, c+32, c+48)
+      float sm = csum[y];
+      sm += __shfl_xor(sm, 16);
+      sm += __shfl_xor(sm, 32);
+      const int n = n0 + 16 * y + c;
+      if (g == 0 && n < N) P[(int64_t)M * N + n] = sm;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Fused readout MLP on the bf16 matrix path, fp32-exact operands (device_common.h, split-bf16):
 // y = act2(act1(X W1 + b1) W2 + b2) . w3 + b3 with every contraction formed from exact 3-piece
 // bf16 splits of both operands (PASSES = 6 or 9 piece products, fp32 accumulation).
@@ -829,5 +943,12 @@ hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t
   auto kern = sum_gru_bf_kernel<64, 64, WV, 4>;
   const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
   hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
+  return hipGetLastError();
+}
+
+hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
+                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st) {
+  dim3 grid((unsigned)chunks, (unsigned)((tiles + wpb - 1) / wpb));
+  hipLaunchKernelGGL(tsgemm_bf_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, part);
   return hipGetLastError();
 }

@@ -63,7 +63,7 @@ struct TrainState {
   std::vector<float*> act;                // readout activations of layers 0 .. L-2
   float* dz[2] = {nullptr, nullptr};
   float* part = nullptr;
-  float* bsum = nullptr;                  // [192]: column sums of ga (fused ordered backward)
+  float* bsum = nullptr;                  // [(H + 1) 3H], H <= 32: fused ordered backward's reduction
   float* ro_x = nullptr;                  // concatenated readout input (several input entities)
   float* dro = nullptr;
   float* dmsg = nullptr;                  // message networks: d(messages) [edges][out]
@@ -442,7 +442,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         (rcat_n && (rc = talloc(t.get(), &t->rcat, rcat_n))) || (ties_n && (rc = talloc(t.get(), &t->rties, ties_n))))
       return rc;
   }
-  if ((rc = talloc(t.get(), &t->part, part_n)) || (rc = talloc(t.get(), &t->bsum, 3 * 64))) return rc;
+  if ((rc = talloc(t.get(), &t->part, part_n)) || (rc = talloc(t.get(), &t->bsum, (32 + 1) * 3 * 32))) return rc;
   b->train = t.release();
   return IGN_OK;
 }
@@ -695,17 +695,14 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
                    t->ga, t->gu, mb.n_dst};
       if (p->bwd_fuse && seq_bwd_fused_supported(H)) {
-        // dU and the du_h bias sums inside the kernel; the z / r recurrent-bias sums equal ga's
+        // dU and both bias gradients (column sums of da and du) inside the kernel
         a.gu = nullptr;
         a.part = t->part;
         a.dU = grk;
         a.db_rec = gb + H3;
+        a.db_in = gb;
+        a.scratch = t->bsum;
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
-        // one pass of column sums over ga feeds b_in and the z / r parts of b_rec
-        HIP_TRY(hipMemsetAsync(t->bsum, 0, H3 * sizeof(float), st));
-        HIP_TRY(launch_colsum_add(t->ga, H3, mb.n_steps, H3, t->part, t->bsum, st));
-        HIP_TRY(launch_axpy(gb, t->bsum, 1.f, H3, st));
-        HIP_TRY(launch_axpy(gb + H3, t->bsum, 1.f, 2 * H, st));
       } else {
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
         HIP_TRY(launch_tsgemm_add(mt.hs[rec.it], H, t->gu, H3, mt.hs_rows, H, H3, t->part, grk, gb + H3, st));

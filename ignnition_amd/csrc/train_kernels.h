@@ -21,12 +21,14 @@ struct SeqBwdArgs {
   float* gu;                 // [n_steps + n_dst][3H] dLoss/d(h.U + b_rec), rows aligned with hs
                              // (the kernel zeroes each sequence's final-state row); unused when fused
   int64_t n_dst;
-  // fused form (part != nullptr, H 16 / 32): dU += sum h_prev^T du and db_rec[2H..3H) += sum du_h are
-  // formed in the kernel (per-wave partials in part, reduced in a fixed order); gu is not written and
-  // the z / r parts of db_rec (= column sums of ga) are left to the caller
+  // fused form (part != nullptr, H 16 / 32): dU += sum h_prev^T du, db_rec += sum du and
+  // db_in += sum da are formed in the kernel (per-wave partials in part, reduced in a fixed order);
+  // gu is not written
   float* part = nullptr;     // seq_bwd_partial_floats(H)
   float* dU = nullptr;       // [H][3H] recurrent-kernel gradient (accumulated)
   float* db_rec = nullptr;   // [3H] recurrent-bias gradient (accumulated)
+  float* db_in = nullptr;    // [3H] input-bias gradient (accumulated)
+  float* scratch = nullptr;  // [(H + 1) * 3H] reduction target
 };
 
 // Backward of the sum update (AUX:752-765): one GRU step per destination row.

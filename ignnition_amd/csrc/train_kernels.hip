@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <stdlib.h>
 
 #include "device_common.h"
 #include "kernels.h"
@@ -67,8 +68,9 @@ __global__ void pack_a_kernel(const float* __restrict__ M, int rows, int cols, f
 // on the MFMA instead of writing du per step for a separate row contraction: each step, h_prev and
 // du are transposed through a per-wave LDS tile ([unit][row], 4-row groups XOR-swizzled by unit so
 // a lane reads its 4 rows as one b128), rows on the MFMA k axis (row 4kk + ks for lane group kk,
-// k-step ks).  Each wave writes one (H + 1) x 3H partial (row H: the column sums of du_h; the z / r
-// column sums equal those of ga); launch_seq_gru_bwd reduces the partials in a fixed order.
+// k-step ks).  Each wave writes one (H + 2) x 3H partial (row H: the column sums of da = b_in's
+// gradient, row H + 1: those of du = b_rec's; they differ in the h gate only, dc vs dc r), so no
+// separate column-sum pass over ga is needed; launch_seq_gru_bwd reduces the partials in a fixed order.
 template <int H, bool FUSE>
 __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   constexpr int NT = H / 16, KH = H / 4, K3 = 3 * H / 4;
@@ -91,10 +93,13 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  f4 dU[NT][3 * NT], bsum[NT];
+  f4 dU[NT][3 * NT], bsum[NT], bz[NT], br[NT], bc[NT];
 #pragma unroll
   for (int mt = 0; mt < NT; ++mt) {
     bsum[mt] = f4{0, 0, 0, 0};
+    bz[mt] = f4{0, 0, 0, 0};
+    br[mt] = f4{0, 0, 0, 0};
+    bc[mt] = f4{0, 0, 0, 0};
 #pragma unroll
     for (int nt = 0; nt < 3 * NT; ++nt) dU[mt][nt] = f4{0, 0, 0, 0};
   }
@@ -214,7 +219,12 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
             for (int mt = 0; mt < NT; ++mt) dU[mt][nt] = MFMA(af[mt][ks], bf[ks], dU[mt][nt]);
         }
 #pragma unroll
-        for (int t = 0; t < NT; ++t) bsum[t] += guh[t];
+        for (int t = 0; t < NT; ++t) {
+          bsum[t] += guh[t];
+          bz[t] += gz[t];
+          br[t] += gr[t];
+          bc[t] += gh[t];
+        }
       }
       // dh_prev = dh' z + du . U^T   (k over the 3H gate units, gate-major)
 #pragma unroll
@@ -241,8 +251,9 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
     }
   }  // tile loop
   if constexpr (FUSE) {
-    // this wave's partial: rows 0..H-1 = dU (lane: D[16mt + 4g + q][16nt + j]), row H = [0, 0, sum du_h]
-    float* P = a.part + ((int64_t)blockIdx.x * 4 + wave) * (H + 1) * (3 * H);
+    // this wave's partial: rows 0..H-1 = dU (lane: D[16mt + 4g + q][16nt + j]),
+    // row H = [sum da_z, sum da_r, sum da_h], row H + 1 = [sum du_z, sum du_r, sum du_h]
+    float* P = a.part + ((int64_t)blockIdx.x * 4 + wave) * (H + 2) * (3 * H);
 #pragma unroll
     for (int mt = 0; mt < NT; ++mt)
 #pragma unroll
@@ -253,15 +264,32 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float s = bsum[t][q];
+        float s = bsum[t][q], sz = bz[t][q], sr = br[t][q], sc = bc[t][q];
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);   // over the 16 rows j of group g
+        for (int o = 1; o < 16; o <<= 1) {   // over the 16 rows j of group g
+          s += __shfl_xor(s, o);
+          sz += __shfl_xor(sz, o);
+          sr += __shfl_xor(sr, o);
+          sc += __shfl_xor(sc, o);
+        }
         bsum[t][q] = s;
+        bz[t][q] = sz;
+        br[t][q] = sr;
+        bc[t][q] = sc;
       }
-    for (int e = lane; e < 2 * H; e += 64) P[H * (3 * H) + e] = 0.f;
     if (j == 0) {
+      float* Pa = P + H * (3 * H);
+      float* Pu = Pa + 3 * H;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) st4(P + H * (3 * H) + 2 * H + 16 * t + 4 * g, bsum[t]);
+      for (int t = 0; t < NT; ++t) {
+        const int u = 16 * t + 4 * g;
+        st4(Pa + u, bz[t]);
+        st4(Pa + H + u, br[t]);
+        st4(Pa + 2 * H + u, bc[t]);
+        st4(Pu + u, bz[t]);
+        st4(Pu + H + u, br[t]);
+        st4(Pu + 2 * H + u, bsum[t]);
+      }
     }
   }
 }
@@ -869,7 +897,7 @@ bool bwd_shape_supported(int din, int h) {
 
 bool seq_bwd_fused_supported(int h) { return h == 16 || h == 32; }
 
-int64_t seq_bwd_partial_floats(int h) { return (int64_t)(kBwdMaxWaves + kTsSegs) * (h + 1) * 3 * h; }
+int64_t seq_bwd_partial_floats(int h) { return (int64_t)(kBwdMaxWaves + kTsSegs) * (h + 2) * 3 * h; }
 
 template <int H>
 static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
@@ -889,13 +917,19 @@ static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_partials_reduce_add(a.part, blocks * 4, H, 3 * H, 1, a.dU, a.db_rec, st);
+  // rows 0..H (dU, da sums) into scratch, row H + 1 (du sums) straight into db_rec
+  e = hipMemsetAsync(a.scratch, 0, (size_t)(H + 1) * 3 * H * sizeof(float), st);
+  if (e != hipSuccess) return e;
+  if ((e = launch_partials_reduce_add(a.part, blocks * 4, H + 1, 3 * H, 1, a.scratch, a.db_rec, st)) != hipSuccess)
+    return e;
+  if ((e = launch_axpy(a.dU, a.scratch, 1.f, (int64_t)H * 3 * H, st)) != hipSuccess) return e;
+  return launch_axpy(a.db_in, a.scratch + (int64_t)H * 3 * H, 1.f, 3 * H, st);
 }
 
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
   if (a.n_dst == 0) return hipSuccess;
   if (a.part) {   // fused dU / b_rec(h) gradients
-    if (!a.dU || !a.db_rec) return hipErrorInvalidValue;
+    if (!a.dU || !a.db_rec || !a.db_in || !a.scratch) return hipErrorInvalidValue;
     if (h == 16) return seq_bwd_fused<16>(a, st);
     if (h == 32) return seq_bwd_fused<32>(a, st);
     return hipErrorInvalidValue;
@@ -1050,8 +1084,15 @@ hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, i
   // one wave per 64x64 tile: a 1- or 2-tile contraction gets 1- or 2-wave blocks, no idle waves
   const int wpb = std::min(4, p.tiles);
   dim3 grid((unsigned)p.chunks, (unsigned)((p.tiles + wpb - 1) / wpb));
-  hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
-  hipError_t e = hipGetLastError();
+  // split-bf16 contraction (kernels_bf.hip) when A is present; IGN_TSGEMM_BF=0 keeps the f32 MFMA form
+  static const int use_bf = [] { const char* v = getenv("IGN_TSGEMM_BF"); return v ? atoi(v) : 1; }();
+  hipError_t e;
+  if (use_bf && A) {
+    e = launch_tsgemm_bf(A, lda, B, ldb, n_rows, M, N, ones, p.chunk, p.chunks, p.tiles, wpb, part, st);
+  } else {
+    hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
+    e = hipGetLastError();
+  }
   if (e != hipSuccess) return e;
   return launch_partials_reduce_add(part, p.chunks, M, N, ones, C, Cb, st);
 }
