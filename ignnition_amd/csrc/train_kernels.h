@@ -29,6 +29,7 @@ struct SeqBwdArgs {
   float* db_rec = nullptr;   // [3H] recurrent-bias gradient (accumulated)
   float* db_in = nullptr;    // [3H] input-bias gradient (accumulated)
   float* scratch = nullptr;  // [(H + 1) * 3H] reduction target
+  const void* Ubf = nullptr; // fused, H = 32: U's split-bf16 pieces (pack_u_bf16) -> gate recompute as seq_gru_bf x6
 };
 
 // Backward of the sum update (AUX:752-765): one GRU step per destination row.

@@ -71,19 +71,29 @@ __global__ void pack_a_kernel(const float* __restrict__ M, int rows, int cols, f
 // k-step ks).  Each wave writes one (H + 2) x 3H partial (row H: the column sums of da = b_in's
 // gradient, row H + 1: those of du = b_rec's; they differ in the h gate only, dc vs dc r), so no
 // separate column-sum pass over ga is needed; launch_seq_gru_bwd reduces the partials in a fixed order.
-template <int H, bool FUSE>
-__global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
-  constexpr int NT = H / 16, KH = H / 4, K3 = 3 * H / 4;
+// BF (H = 32): the gate recompute h.U runs on the forward's split-bf16 path (seq_gru_bf x6: the
+// same pieces, MFMA order and bias seeding), so the recomputed gates are bitwise the forward's.
+template <int H, bool FUSE, bool BF = false>
+__global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
+  constexpr int NT = H / 16, KH = H / 4, K3 = 3 * H / 4, KS = H / 32;
   constexpr bool LDSU = H <= 32;
   static_assert(!FUSE || LDSU, "fused dU: H 16 / 32");
-  constexpr int NUP = LDSU ? 3 * NT * KH * 64 : 1, NUT = LDSU ? NT * K3 * 64 : 1;
+  static_assert(!BF || H == 32, "split-bf16 recompute: H 32");
+  constexpr int NUP = LDSU && !BF ? 3 * NT * KH * 64 : 1, NUT = LDSU ? NT * K3 * 64 : 1;
+  constexpr int NUB = BF ? 9 * NT * KS * 64 : 1;   // bf8 fragments of U's pieces
   constexpr int NTR = FUSE ? 4 * 3 * H * 16 : 1;   // per-wave transpose tiles
   __shared__ float sUp[NUP];
+  __shared__ bf8 sUb[NUB];
   __shared__ float sUt[NUT];
   __shared__ float sT[NTR];
   if constexpr (LDSU) {
-    for (int e = threadIdx.x; e < NUP / 4; e += blockDim.x)
-      reinterpret_cast<f4*>(sUp)[e] = reinterpret_cast<const f4*>(a.Up)[e];
+    if constexpr (BF) {
+      for (int e = threadIdx.x; e < NUB; e += blockDim.x)
+        reinterpret_cast<u4v*>(sUb)[e] = static_cast<const u4v*>(a.Ubf)[e];
+    } else {
+      for (int e = threadIdx.x; e < NUP / 4; e += blockDim.x)
+        reinterpret_cast<f4*>(sUp)[e] = reinterpret_cast<const f4*>(a.Up)[e];
+    }
     for (int e = threadIdx.x; e < NUT / 4; e += blockDim.x)
       reinterpret_cast<f4*>(sUt)[e] = reinterpret_cast<const f4*>(a.Ut)[e];
     __syncthreads();
@@ -149,14 +159,51 @@ __global__ __launch_bounds__(256) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         ar[t] = f4{0, 0, 0, 0};
         ah[t] = bh[t];
       }
+      if constexpr (BF) {
+        bf8 hf[3][KS];
 #pragma unroll
-      for (int s = 0; s < KH; ++s) {
-        const float hb = hp[s >> 2][s & 3];
+        for (int s = 0; s < KS; ++s) {
+          u4v w0, w1, w2;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          az[t] = MFMA(Up[frag_idx(0 * NT + t, s, KH, lofs)], hb, az[t]);
-          ar[t] = MFMA(Up[frag_idx(1 * NT + t, s, KH, lofs)], hb, ar[t]);
-          ah[t] = MFMA(Up[frag_idx(2 * NT + t, s, KH, lofs)], hb, ah[t]);
+          for (int q = 0; q < 4; ++q) {
+            const int e0 = 2 * q, e1 = 2 * q + 1;
+            float a0, a1, a2, b0, b1, b2;
+            split3(hp[2 * s + (e0 >> 2)][e0 & 3], a0, a1, a2);
+            split3(hp[2 * s + (e1 >> 2)][e1 & 3], b0, b1, b2);
+            w0[q] = pack_hi16(a0, b0);
+            w1[q] = pack_hi16(a1, b1);
+            w2[q] = pack_hi16(a2, b2);
+          }
+          hf[0][s] = __builtin_bit_cast(bf8, w0);
+          hf[1][s] = __builtin_bit_cast(bf8, w1);
+          hf[2][s] = __builtin_bit_cast(bf8, w2);
+        }
+#pragma unroll
+        for (int pu = 2; pu >= 0; --pu)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const bf8 wz = sUb[(((pu * 3 + 0) * NT + t) * KS + s) * 64 + lofs];
+              const bf8 wr = sUb[(((pu * 3 + 1) * NT + t) * KS + s) * 64 + lofs];
+              const bf8 wh = sUb[(((pu * 3 + 2) * NT + t) * KS + s) * 64 + lofs];
+#pragma unroll
+              for (int ph = 2 - pu; ph >= 0; --ph) {
+                az[t] = MFMA_BF(wz, hf[ph][s], az[t]);
+                ar[t] = MFMA_BF(wr, hf[ph][s], ar[t]);
+                ah[t] = MFMA_BF(wh, hf[ph][s], ah[t]);
+              }
+            }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KH; ++s) {
+          const float hb = hp[s >> 2][s & 3];
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            az[t] = MFMA(Up[frag_idx(0 * NT + t, s, KH, lofs)], hb, az[t]);
+            ar[t] = MFMA(Up[frag_idx(1 * NT + t, s, KH, lofs)], hb, ar[t]);
+            ah[t] = MFMA(Up[frag_idx(2 * NT + t, s, KH, lofs)], hb, ah[t]);
+          }
         }
       }
       f4 gz[NT], gr[NT], gh[NT], guh[NT], acc[NT];
@@ -899,7 +946,7 @@ bool seq_bwd_fused_supported(int h) { return h == 16 || h == 32; }
 
 int64_t seq_bwd_partial_floats(int h) { return (int64_t)(kBwdMaxWaves + kTsSegs) * (h + 2) * 3 * h; }
 
-template <int H>
+template <int H, bool BF>
 static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
   static int cus = 0;
   if (!cus) {
@@ -909,12 +956,12 @@ static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
     if (cus <= 0) cus = 256;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, seq_gru_bwd_kernel<H, true>, 256, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, seq_gru_bwd_kernel<H, true, BF>, 256, 0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 1;
   const int64_t tiles = (a.n_dst + 15) / 16;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>({(tiles + 3) / 4, (int64_t)per_cu * cus, kBwdMaxWaves / 4}));
-  hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true, BF>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // rows 0..H (dU, da sums) into scratch, row H + 1 (du sums) straight into db_rec
@@ -930,8 +977,8 @@ hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
   if (a.n_dst == 0) return hipSuccess;
   if (a.part) {   // fused dU / b_rec(h) gradients
     if (!a.dU || !a.db_rec || !a.db_in || !a.scratch) return hipErrorInvalidValue;
-    if (h == 16) return seq_bwd_fused<16>(a, st);
-    if (h == 32) return seq_bwd_fused<32>(a, st);
+    if (h == 16) return seq_bwd_fused<16, false>(a, st);
+    if (h == 32) return a.Ubf ? seq_bwd_fused<32, true>(a, st) : seq_bwd_fused<32, false>(a, st);
     return hipErrorInvalidValue;
   }
   if (!a.gu) return hipErrorInvalidValue;
