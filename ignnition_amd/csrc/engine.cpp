@@ -183,7 +183,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(7, std::max(1, atoi(v)));
   if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
-  if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v) != 0;
+  if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
   if (const char* v = getenv("IGN_SUM_SPLIT")) p->sum_split = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
@@ -905,7 +905,11 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
             (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
           return rc;
       }
-      if (!p->sum_split && p->sum_window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
+      // windowed aggregation pays where each destination gathers many messages (one lane per
+      // destination otherwise walks a long dependent chain): auto threshold 64 per destination
+      const bool window = p->sum_window > 0 ||
+                          (p->sum_window < 0 && ND > 0 && (double)mdst.size() >= 64.0 * (double)ND);
+      if (!p->sum_split && window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
         std::vector<int64_t> dstart(ND + 1, 0);

@@ -207,8 +207,10 @@ struct ign_plan {
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
   bool sum_split = false;         // plain sums as a gather-only kernel + the GRU step (IGN_SUM_SPLIT=1)
-  bool sum_window = false;        // windowed sum aggregation where eligible (IGN_SUM_WINDOW=1): measured
-                                  // 0.120 vs 0.112 ms (RouteNet link update), 0.156 vs 0.206 (Q-size)
+  int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
+                                  // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
+                                  // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);
+                                  // Q-size x512 7.33 -> 6.44 ms/step with both sum MPs windowed
   // timing
   bool timing = false;
   uint32_t timing_kinds = ~0u;    // kernel kinds that get event pairs (ign_plan_set_timing_kinds)
