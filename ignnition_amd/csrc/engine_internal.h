@@ -205,6 +205,8 @@ struct ign_plan {
                                   // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
   int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
+  bool tsgemm_bf = true;          // weight-gradient row contractions on tsgemm_bf (IGN_TSGEMM_BF=0: f32 MFMA)
+  bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
   bool sum_split = false;         // plain sums as a gather-only kernel + the GRU step (IGN_SUM_SPLIT=1)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)

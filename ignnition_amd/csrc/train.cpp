@@ -558,6 +558,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
   hipStream_t st = p->stream;
   const int E = (int)p->ents.size();
   const int64_t P = b->n_pred;
+  set_tsgemm_bf(p->tsgemm_bf);
   HIP_TRY(hipMemsetAsync(grads, 0, p->n_params * sizeof(float), st));
   std::vector<int> dcur(E, 0);
   for (int e = 0; e < E; ++e)
@@ -710,8 +711,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
         a.scratch = t->bsum;
         // gate recompute on the forward's split-bf16 path when the forward ran seq_gru_bf x6
         // (bitwise the forward's gates); IGN_BWD_BF=0 keeps the f32 MFMA recompute
-        static const int bwd_bf = [] { const char* v = getenv("IGN_BWD_BF"); return v ? atoi(v) : 1; }();
-        if (bwd_bf && H == 32 && cp.pk_ubf >= 0 && p->seq_variant == 4) a.Ubf = p->d_packed + cp.pk_ubf;
+        if (p->bwd_bf && H == 32 && cp.pk_ubf >= 0 && p->seq_variant == 4) a.Ubf = p->d_packed + cp.pk_ubf;
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
       } else {
         HIP_TRY(launch_seq_gru_bwd(a, H, st));

@@ -92,6 +92,8 @@ hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, f
 // C[M][N] += sum_r A[r][:M]^T B[r][:N] and, if Cb, Cb[N] += sum_r B[r][:N] (a virtual ones column);
 // partial sums per row chunk, reduced in a fixed order (deterministic)
 int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N);
+// weight-gradient contractions on the split-bf16 kernel (default) or f32 MFMA; the plan sets it per backward
+void set_tsgemm_bf(bool on);
 // C[m][n] (row m = M: Cb[n]) += sum of nchunks partial tiles part[c][M + ones][N], in chunk order
 hipError_t launch_partials_reduce_add(float* part, int64_t nchunks, int M, int N, int ones, float* C, float* Cb,
                                       hipStream_t st);

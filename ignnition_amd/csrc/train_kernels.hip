@@ -1118,6 +1118,9 @@ hipError_t launch_act_bwd(const float* da, const float* a, int64_t n, int act, f
   return hipGetLastError();
 }
 
+static int g_tsgemm_bf = 1;   // set per backward from the plan (ign_backward: set_tsgemm_bf)
+void set_tsgemm_bf(bool on) { g_tsgemm_bf = on ? 1 : 0; }
+
 int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N) {
   const TsPlan p = ts_plan(n_rows, M, N, 1);
   return (p.chunks + kTsSegs) * (int64_t)p.Mx * N;
@@ -1131,10 +1134,9 @@ hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, i
   // one wave per 64x64 tile: a 1- or 2-tile contraction gets 1- or 2-wave blocks, no idle waves
   const int wpb = std::min(4, p.tiles);
   dim3 grid((unsigned)p.chunks, (unsigned)((p.tiles + wpb - 1) / wpb));
-  // split-bf16 contraction (kernels_bf.hip) when A is present; IGN_TSGEMM_BF=0 keeps the f32 MFMA form
-  static const int use_bf = [] { const char* v = getenv("IGN_TSGEMM_BF"); return v ? atoi(v) : 1; }();
+  // split-bf16 contraction (kernels_bf.hip) when A is present; the plan's IGN_TSGEMM_BF=0 keeps f32 MFMA
   hipError_t e;
-  if (use_bf && A) {
+  if (g_tsgemm_bf && A) {
     e = launch_tsgemm_bf(A, lda, B, ldb, n_rows, M, N, ones, p.chunk, p.chunks, p.tiles, wpb, part, st);
   } else {
     hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
