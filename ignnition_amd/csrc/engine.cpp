@@ -678,11 +678,22 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       }
       if (mp.sorted) {
         // gather_nd(outputs, [d, final_len-1]) needs final_len <= sum of Lmax (AUX:793-795)
-        for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r)
+        int64_t max_flen = 0;
+        for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r) {
           if (flen[r] > total_slots)
             return fail(IGN_ERR_INVALID, "graph %d: destination row %lld has final_len %lld > %lld padded slots"
                         " (gather_nd out of range, AUX:793-795)", g, (long long)(r - b->row_off[dst][g]),
                         (long long)flen[r], (long long)total_slots);
+          max_flen = std::max(max_flen, flen[r]);
+        }
+        // RNN(mask=tf.sequence_mask(final_len)) (AUX:785-790): the mask is max(final_len) wide, and
+        // K.rnn unstacks it into a TensorList that its while loop reads at every one of the
+        // total_slots time steps -> InvalidArgument at step max(final_len) when that is narrower
+        // ("masked-RNN time length")
+        if (b->row_off[dst][g + 1] > b->row_off[dst][g] && max_flen < total_slots)
+          return fail(IGN_ERR_INVALID, "graph %d: sequence_mask(final_len) is %lld steps wide but the padded "
+                      "sequence has %lld (K.rnn reads the mask TensorList past its end, AUX:785-790)", g,
+                      (long long)max_flen, (long long)total_slots);
       }
     }
     for (int s = 0; s < S; ++s) {   // message networks: per-edge rows and parameters (GM:440-475)

@@ -251,6 +251,13 @@ class DenseOracle:
             if np.any(final_len > src_input.shape[1]):
                 raise OracleError("gather_nd index final_len-1 beyond the padded length")
             L = src_input.shape[1]
+            # mask = tf.sequence_mask(final_len) is max(final_len) steps wide (AUX:790).  Keras
+            # K.rnn (TF 2.1, control flow v2) unstacks it into a TensorList of that length and its
+            # while loop runs time_steps = L iterations, reading mask_ta[t] at each: a narrower mask
+            # fails with InvalidArgument ("Trying to access element t in a list with t elements").
+            if num_dst and final_len.max() < L:
+                raise OracleError("sequence_mask(final_len) is %d steps wide, the padded input %d: "
+                                  "K.rnn reads the mask TensorList past its end" % (final_len.max(), L))
             h = old
             outputs = np.zeros((num_dst, L, old.shape[1]), dt)
             for t in range(L):

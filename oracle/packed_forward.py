@@ -44,6 +44,12 @@ class PackedOracle(DenseOracle):
                 per_dst[int(dst_idx[k])].append((pos, table[int(src_idx[k])].astype(dt)))
                 final_len[int(dst_idx[k])] += 1
             slot_off += lmax
+        if aggr in ("ordered", "interleave", "concat") and num_dst:
+            # the padded sequence has slot_off steps (concat on axis 2: the first source's Lmax);
+            # the masked RNN needs max(final_len) == that length (dense_forward.py, AUX:785-795)
+            L_pad = slot_off if not (aggr == "concat" and int(mp["aggregation"]["concat_axis"]) == 2) else None
+            if L_pad is not None and (final_len.max() < L_pad or final_len.max() > L_pad):
+                raise OracleError("final_len width %d vs padded length %d" % (final_len.max(), L_pad))
         cell = self._cell(dst)
         old = state[dst]
         new = np.empty_like(old)

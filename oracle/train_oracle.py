@@ -182,6 +182,9 @@ class TorchOracle:
         else:
             if bool((final_len == 0).any()):
                 raise OracleError("gather_nd with index -1")
+            if num_dst and int(final_len.max()) != src_input.shape[1]:   # dense_forward.py, AUX:785-795
+                raise OracleError("sequence_mask(final_len) width %d vs padded length %d"
+                                  % (int(final_len.max()), src_input.shape[1]))
             h = old
             outs = []
             for t in range(src_input.shape[1]):

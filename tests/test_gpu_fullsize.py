@@ -1,0 +1,137 @@
+"""BASELINE.json's two headline workloads at their stated sizes (MI355X only).
+
+configs[4] — the synthetic 1M-node / 10M-edge graph, H=64, T=8:
+  * the whole graph on one GPU: finite, and bitwise deterministic run to run;
+  * the 8-way edge-cut the driver's 8-GPU bench runs (contiguous id ranges, halo rows,
+    interior/boundary overlap), all 8 partitions in this process over LoopbackComm: the
+    concatenated predictions equal the whole-graph run bit for bit (each destination keeps its
+    in-edges in order, so every sum associates identically);
+  * the oracle on a 25 000-node instance of the same generator (same degree law and locality),
+    at the full model size (H=64, T=8), within the §8c tolerance.
+
+configs[2] — RouteNet on 512 synth50-size graphs batched into one CSR (the default bench):
+  * deterministic; three graphs of the batch equal the same graph run alone (GM:712-724: the
+    reference runs the model per graph); two graphs against the float64 oracle.
+
+Tolerance: |engine - oracle| <= 1e-4 * max(1, |oracle|).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from ignnition_amd import partition, workloads
+from ignnition_amd.engine import Batch, Engine, MPPlan, device_count
+from ignnition_amd.json_operations import Model_information
+from oracle.dense_forward import DenseOracle
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _scaled_err(got, exp):
+    got = np.asarray(got, np.float64).reshape(-1)
+    exp = np.asarray(exp, np.float64).reshape(-1)
+    assert got.shape == exp.shape
+    return float((np.abs(got - exp) / np.maximum(1.0, np.abs(exp))).max())
+
+
+@pytest.fixture(scope="module")
+def big_graph():
+    if device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=1_000_000)
+    x = graphs[0]
+    assert int(x["num_node"]) == 1_000_000
+    assert 9_500_000 <= len(x["src_adj_nodes_nodes"]) <= 10_500_000
+    plan = MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims))
+    assert plan.hidden[0] == 64 and plan.iterations == 8
+    prm = plan.init_params(3, bias_scale=0.1)
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    whole = Batch(eng, graphs)
+    out = whole.forward().reshape(-1)
+    edges = whole.edges_per_forward
+    out2 = whole.forward().reshape(-1)
+    whole.close()
+    yield x, plan, eng, out, out2, edges
+    eng.close()
+
+
+def test_1m_whole_graph_finite_and_deterministic(big_graph):
+    x, plan, eng, out, out2, edges = big_graph
+    assert out.size == 1_000_000
+    assert np.all(np.isfinite(out))
+    assert edges == 8 * len(x["src_adj_nodes_nodes"])
+    np.testing.assert_array_equal(out, out2)
+
+
+def test_1m_eight_partition_edge_cut_bit_identical(big_graph):
+    """The 8-rank layout of `bench.py --model synthetic --gpus 8`, in one process."""
+    x, plan, eng, out, _, edges = big_graph
+    world = 8
+    parts = [partition.local_part(x, plan, r, world) for r in range(world)]
+    comm = partition.LoopbackComm(world)
+    partition.exchange_requests(parts, comm)
+    halo = [p.halos["node"].n_halo for p in parts]
+    assert all(h > 0 for h in halo)
+    fw = partition.EdgeCutForward(eng, parts, comm, overlap=True)
+    try:
+        assert fw.edges_per_forward == edges
+        splits = [b.mp_split(0) for b in fw.batches]
+        assert all(i > 0 and bd > 0 for i, bd in splits)
+        got = np.concatenate([o.reshape(-1) for o in fw.forward()])
+        np.testing.assert_array_equal(got, out)
+    finally:
+        fw.close()
+        torch.cuda.synchronize()
+
+
+def test_synthetic_full_model_25k_matches_oracle():
+    """H=64, T=8 and the default generator settings, 25k nodes / ~250k edges."""
+    if device_count() == 0:
+        pytest.fail("no GPU visible")
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=25_000)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(4, bias_scale=0.1)
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    b = Batch(eng, graphs)
+    out = b.forward().reshape(-1)
+    b.close()
+    eng.close()
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    err = _scaled_err(out, ref)
+    print("25k synthetic, H=64 T=8: max scaled error %.3g" % err)
+    assert err <= TOL
+
+
+def test_routenet_512_synth50_batch():
+    if device_count() == 0:
+        pytest.fail("no GPU visible")
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "synth50", 512)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(1, bias_scale=0.05)
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    b = Batch(eng, graphs)
+    assert b.edges_per_forward == workloads.edges_per_forward(mi, graphs)
+    o1 = b.forward().reshape(-1)
+    o2 = b.forward().reshape(-1)
+    b.close()
+    np.testing.assert_array_equal(o1, o2)
+    assert np.all(np.isfinite(o1))
+    P = [int(g["num_path"]) for g in graphs]
+    off = np.cumsum([0] + P)
+    assert o1.size == off[-1]
+    for gi in (0, 255, 511):
+        alone = Batch(eng, [graphs[gi]])
+        np.testing.assert_array_equal(o1[off[gi]:off[gi + 1]], alone.forward().reshape(-1))
+        alone.close()
+    ora = DenseOracle(desc, dims, prm)
+    for gi in (7, 400):
+        err = _scaled_err(o1[off[gi]:off[gi + 1]], ora.forward([graphs[gi]]))
+        assert err <= TOL, (gi, err)
+    eng.close()

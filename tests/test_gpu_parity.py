@@ -116,6 +116,31 @@ def test_multi_source_ordered_slots_after_global_lmax():
     _close(out, ref)
 
 
+@pytest.mark.parametrize("aggr", ["interleave", "ordered"])
+def test_narrow_sequence_mask_rejected(aggr):
+    """max(final_len) < padded length in a graph: the reference's masked RNN reads its
+    sequence_mask TensorList past the end and TF raises (AUX:785-790); the engine
+    returns IGN_ERR_INVALID, the oracle raises.  The same graph next to a full-width one (the
+    batch of the reference is per graph) still fails."""
+    from tests.test_oracle import QS_DIMS, holes_input, narrow_mask_input
+    desc = model_examples.qsize(hidden=16, iterations=2)
+    x = narrow_mask_input()
+    ok = holes_input()
+    if aggr == "ordered":
+        desc["message_passing"]["stages"][0]["stage_mp"][0]["aggregation"] = {"type": "ordered"}
+        for g in (x, ok):
+            del g["indices_link_to_path"], g["indices_node_to_path"]
+    mi = Model_information(copy.deepcopy(desc), QS_DIMS)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(0))
+    for graphs in ([x], [ok, x]):
+        with pytest.raises(_lib.EngineError, match="sequence_mask") as ei:
+            Batch(eng, graphs)
+        assert ei.value.code == -1
+    Batch(eng, [ok]).forward()
+
+
 def test_final_len_beyond_padding_rejected():
     """Duplicates that make final_len exceed max(seq)+1: TF's gather_nd fails (AUX:793-795)."""
     desc = model_examples.routenet(hidden=16, iterations=2)
@@ -175,8 +200,9 @@ def test_batch_equals_per_graph():
 
 
 def test_large_batch_properties():
-    """512 x synth50-size batch: finite, deterministic, and graph g of the batch equals the same
-    graph run alone (size-independent property), plus a few graphs vs the oracle."""
+    """64 x synth50-size batch: finite, deterministic, and graph g of the batch equals the same
+    graph run alone (size-independent property), plus a graph vs the oracle.  The full 512-graph
+    batch is tests/test_gpu_fullsize.py::test_routenet_512_synth50_batch."""
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "synth50", 64)
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(1, bias_scale=0.05)

@@ -111,9 +111,30 @@ QS_DIMS = {"link_capacity": 1, "traffic": 1, "queue_sizes": 1, "adj_links_paths"
 
 def holes_input():
     """Interleave with a hole and a dropped position, GEN-consistent indices:
-    p0 has links [l0, l1] and node [n0]; p1 has link [l1] and nodes [n1, n2].  Pattern
-    [node, link] over n_total = 2 + 2 slots -> indices_node = [0, 2], indices_link = [1, 3].
-    p0: final_len 3, link slot 1 lands on position 3 (dropped), position 2 is a hole."""
+    p0 has links [l0, l1] and node [n0]; p1 has link [l1] and nodes [n1, n2]; p2 has links
+    [l0, l1] and nodes [n1, n2].  Pattern [node, link] over n_total = 2 + 2 slots ->
+    indices_node = [0, 2], indices_link = [1, 3].  p0: final_len 3, link slot 1 lands on
+    position 3 (dropped), position 2 is a hole.  p2 fills all 4 positions, so the mask
+    sequence_mask(final_len) is as wide as the padded sequence (narrow_mask_input() is not)."""
+    return {
+        "link_capacity": [0.5, -0.25], "traffic": [0.1, 0.7, -0.3], "queue_sizes": [0.3, -0.6, 0.9],
+        "src_adj_links_paths": [0, 1, 1, 0, 1], "dst_adj_links_paths": [0, 0, 1, 2, 2],
+        "seq_link_path": [0, 1, 0, 0, 1],
+        "src_adj_nodes_paths": [0, 1, 2, 1, 2], "dst_adj_nodes_paths": [0, 1, 1, 2, 2],
+        "seq_node_path": [0, 0, 1, 0, 1],
+        "src_adj_paths_links": [0, 2, 0, 1, 2], "dst_adj_paths_links": [0, 0, 1, 1, 1],
+        "seq_path_link": [0, 1, 0, 1, 2],
+        "src_adj_paths_nodes": [0, 1, 2, 1, 2], "dst_adj_paths_nodes": [0, 1, 1, 2, 2],
+        "seq_path_node": [0, 0, 1, 0, 1],
+        "num_link": 2, "num_path": 3, "num_node": 3,
+        "indices_link_to_path": [1, 3], "indices_node_to_path": [0, 2],
+    }
+
+
+def narrow_mask_input():
+    """holes_input() without p2: every path has final_len 3 while the padded sequence has 4
+    positions.  The reference's RNN reads sequence_mask(final_len) (3 wide) at step 3 and TF
+    raises InvalidArgument (AUX:785-790)."""
     return {
         "link_capacity": [0.5, -0.25], "traffic": [0.1, 0.7], "queue_sizes": [0.3, -0.6, 0.9],
         "src_adj_links_paths": [0, 1, 1], "dst_adj_links_paths": [0, 0, 1], "seq_link_path": [0, 1, 0],
@@ -131,6 +152,20 @@ def test_restatements_agree_on_interleave_holes():
     a = DenseOracle(desc, QS_DIMS, prm).forward([holes_input()])
     b = PackedOracle(desc, QS_DIMS, prm).forward([holes_input()])
     np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("aggr", ["interleave", "ordered"])
+def test_narrow_sequence_mask_raises(aggr):
+    """max(final_len) < padded length: both restatements raise where TF does (AUX:785-790)."""
+    desc = model_examples.qsize(hidden=16, iterations=2)
+    x = narrow_mask_input()
+    if aggr == "ordered":
+        desc["message_passing"]["stages"][0]["stage_mp"][0]["aggregation"] = {"type": "ordered"}
+        del x["indices_link_to_path"], x["indices_node_to_path"]
+    prm = _params(desc, QS_DIMS, seed=5, bias=0.2)
+    for ora in (DenseOracle, PackedOracle):
+        with pytest.raises(OracleError, match="padded"):
+            ora(desc, QS_DIMS, prm).forward([x])
 
 
 def test_ragged_interleave_from_reference_generator_raises(gen_fixtures):
