@@ -34,7 +34,7 @@ def main(d, out=None):
         for k, v in dur.items():
             res[k]["launches"] = len(v)
             res[k]["avg_ms"] = sum(v) / len(v)
-    for p in ("fetch", "write", "sq", "tcc"):
+    for p in ("fetch", "write", "sq", "sq2", "tcc"):
         fs = glob.glob(os.path.join(d, p, "**", "*counter_collection.csv"), recursive=True)
         if not fs:
             continue
