@@ -247,8 +247,8 @@ def main():
                             % (6 if six else 9)) if v else "f32 MFMA"
     contraction = {"ordered_update_hU": split(seq_v >= 4, seq_v == 4),
                    "readout": split(ro_v in (2, 3, 4), ro_v != 3),
-                   # sum variant 7 (default): split-bf16 x.W / h.U when DIN = H = 64 (the synthetic graph)
-                   "sum_update": split(plan.hidden[0] == 64 and sum_v == 7, True),
+                   # sum variant 7 (default): split-bf16 x.W / h.U for plain sums at DIN = H = 32 or 64
+                   "sum_update": split(plan.hidden[0] in (32, 64) and sum_v == 7, True),
                    "projection": "f32 MFMA"}
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,

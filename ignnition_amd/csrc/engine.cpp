@@ -87,18 +87,11 @@ int dev_alloc(ign_batch* b, float** out, int64_t n) {
 
 int act_ok(int a) { return a >= IGN_ACT_LINEAR && a <= IGN_ACT_TANH; }
 
-// Destination processing order.  Default: one global sort by message count, descending (tiles of
-// equal length; the longest sequences start first).  graph_major: per graph by count, so tiles
-// stay inside one graph (with the XCD-aware block mapping one graph's tiles share an L2).
-void sort_order(std::vector<int32_t>& order, const std::vector<int64_t>& cnt, const std::vector<int64_t>& goff,
-                bool graph_major) {
-  auto by_cnt = [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; };
-  if (!graph_major) {
-    std::stable_sort(order.begin(), order.end(), by_cnt);
-    return;
-  }
-  for (size_t g = 0; g + 1 < goff.size(); ++g)
-    std::stable_sort(order.begin() + goff[g], order.begin() + goff[g + 1], by_cnt);
+// Destination processing order: one global stable sort by message count, descending (tiles of
+// equal length; the longest sequences start first).  Measured faster than per-graph orders with
+// XCD-aware tiles for both the ordered and the sum updates (profiles/r02/seq_experiments).
+void sort_order(std::vector<int32_t>& order, const std::vector<int64_t>& cnt) {
+  std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
 }
 
 // Per-launch algorithmic cost: one GRU application = 2*3H*(DIN+H) + 14H flops.
@@ -176,20 +169,15 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(7, std::max(1, atoi(v)));
-  if (const char* v = getenv("IGN_GRAPH_MAJOR")) p->graph_major = atoi(v) != 0;
-  if (const char* v = getenv("IGN_XCD_REMAP")) p->xcd_remap = atoi(v) != 0;
-  if (const char* v = getenv("IGN_SUM_ORDER")) p->sum_order = atoi(v);
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(5, std::max(2, atoi(v)));
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
-  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = std::min(7, std::max(1, atoi(v)));
-  if (const char* v = getenv("IGN_SEQ_ABLATE")) p->ablate = atoi(v);
+  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 ? 7 : 3;
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
-  if (const char* v = getenv("IGN_SUM_SPLIT")) p->sum_split = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TSGEMM_BF")) p->tsgemm_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
-  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(7, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(3, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -370,7 +358,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.pk_u = pk; pk = align(pk + 3LL * cp.H * cp.H);
     cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
     if (pack_u_bf16_floats(cp.H)) { cp.pk_ubf = pk; pk = align(pk + pack_u_bf16_floats(cp.H)); }
-    if (cp.din == 64 && cp.H == 64) { cp.pk_wbf = pk; pk = align(pk + pack_w_bf16_floats(cp.din, cp.H)); }
+    if ((cp.din == 64 && cp.H == 64) || (cp.din == 32 && cp.H == 32)) { cp.pk_wbf = pk; pk = align(pk + pack_w_bf16_floats(cp.din, cp.H)); }
   }
   for (size_t l = 0; l < p->dense.size(); ++l) {
     DenseP& dp = p->dense[l];
@@ -736,7 +724,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if (flen[r] == 0)   // AUX:793-795: gather_nd(outputs, [d, final_len-1]) with -1
           return fail(IGN_ERR_INVALID, "destination row %lld receives no message: the reference's sorted update"
                       " gathers position -1 (AUX:793-795)", (long long)r);
-      sort_order(order, flen, b->row_off[dst], p->graph_major);
+      sort_order(order, flen);
       // bucket messages by destination (stable), keep those with pos < final_len, sort by pos
       std::vector<int64_t> dcnt(ND + 1, 0);
       for (size_t k = 0; k < mdst.size(); ++k) dcnt[mdst[k] + 1]++;
@@ -820,13 +808,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.bytes = (double)steps * (4.0 * H + 4) + (double)ND * 8.0 * H + 4.0 * (ND + 1);
       b->gru_steps += steps * p->T;
     } else {
-      if (p->sum_order == 0 || p->sum_order >= 3) {   // 3 / 4: graph-major for sum MPs (3: + XCD-aware tiles)
-        sort_order(order, flen, b->row_off[dst], p->graph_major || p->sum_order >= 3);
-      } else if (p->sum_order == 1) {
-        auto by_cnt = [&](int32_t x, int32_t y) { return flen[x] > flen[y]; };
-        for (int64_t c = 0; c < ND; c += 256)
-          std::stable_sort(order.begin() + c, order.begin() + std::min<int64_t>(ND, c + 256), by_cnt);
-      }
+      sort_order(order, flen);
       // edge-cut partitions: destinations reading a halo row go last (they wait for the exchange)
       std::vector<char> bnd(ND, 0);
       for (size_t k = 0; k < mdst.size(); ++k) {
@@ -908,21 +890,11 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         for (int g = 0; g < G; ++g)
           max_src_rows = std::max(max_src_rows, b->row_off[mp.src[0].entity][g + 1] - b->row_off[mp.src[0].entity][g]);
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
-      // split sum update (IGN_SUM_SPLIT=1): gather-only kernel, then the GRU step through an identity CSR
-      if (p->sum_split && mp.aggr == IGN_AGGR_SUM && (DIN == 16 || DIN == 32 || DIN == 64)) {
-        std::vector<int32_t> id_ptr(ND + 1);
-        std::vector<uint32_t> id_src(ND);
-        for (int64_t i = 0; i <= ND; ++i) id_ptr[i] = (int32_t)i;
-        for (int64_t i = 0; i < ND; ++i) id_src[i] = (uint32_t)order[i];
-        if ((rc = dev_upload(b.get(), &mb.d_id_ptr, id_ptr)) || (rc = dev_upload(b.get(), &mb.d_id_src, id_src)) ||
-            (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
-          return rc;
-      }
       // windowed aggregation pays where each destination gathers many messages (one lane per
       // destination otherwise walks a long dependent chain): auto threshold 64 per destination
       const bool window = p->sum_window > 0 ||
                           (p->sum_window < 0 && ND > 0 && (double)mdst.size() >= 64.0 * (double)ND);
-      if (!p->sum_split && window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
+      if (window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
         std::vector<int64_t> dstart(ND + 1, 0);
@@ -1165,11 +1137,8 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                                mb.d_table + mb.zero_row * W3, st));
       tm.end();
     }
-    if (cp.H == 64 && p->seq_variant < 2)
-      return fail(IGN_ERR_UNSUPPORTED, "64-unit ordered updates need the LDS variants (IGN_SEQ_VARIANT=2 or 3)");
     SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
-                 p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, p->ablate,
-                 mb.n_steps};
+                 p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
     if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
     tm.begin(K_SEQ, mb.flops, mb.bytes);
     HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
@@ -1198,20 +1167,10 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       HIP_TRY(launch_sum_win(wa, mp.din, st));
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
       tm.end();
-    } else if (count > 0 && mb.d_id_ptr && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
-      SumGruArgs g{hin, hout, sbases, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, nullptr, nullptr, nullptr, mb.n_dst, 0};
-      SrcBases xb{};
-      xb.base[0] = mb.d_xsum;
-      SumGruArgs a{hin, hout, xb, mb.d_order, mb.d_id_ptr, mb.d_id_src, p->d_packed + cp.pk_w,
-                   p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
-      tm.begin(K_SUM, mb.flops, mb.bytes);
-      HIP_TRY(launch_sum_only(g, mp.din, mb.d_xsum, st));
-      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
-      tm.end();
     } else if (count > 0) {
       SumGruArgs a{hin, hout, sbases, mb.d_order + first, mb.d_msg_ptr + first, mb.d_msg_src,
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count,
-                   p->xcd_remap || p->sum_order == 3};
+                   p->xcd_remap};
       if (mp.aggr == IGN_AGGR_ATTENTION) a.msg_w = mb.d_msg_w;
       if (mp.aggr == IGN_AGGR_SUM && cp.pk_wbf >= 0 && cp.pk_ubf >= 0 && mp.din == cp.din && !mp.feature_concat) {
         a.Wbf = p->d_packed + cp.pk_wbf;
@@ -1284,9 +1243,7 @@ int readout(ign_plan* p, ign_batch* b) {
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0));
     if (p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0)
       HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
-                                p->readout_variant == 3 ? 9 : p->readout_variant == 4 ? -6 :
-                                p->readout_variant == 5 ? -7 : p->readout_variant == 6 ? -8 :
-                                p->readout_variant == 7 ? -9 : 6, st));
+                                p->readout_variant == 3 ? 9 : 6, st));
     else
       HIP_TRY(launch_readout3(a, l1.in, l1.out, l2.out, st));
     tm.end();

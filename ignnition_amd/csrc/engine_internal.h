@@ -185,30 +185,18 @@ struct ign_plan {
   bool params_set = false;
   bool fused_readout = false;
   int readout_variant = 2;        // fused readout: 1 = f32 MFMA (readout3), 2 / 3 = split-bf16 with 6 / 9
-                                  // piece products (readout_bf); 4-7 = readout_bf layout diagnostics
-                                  // (32-unit chunks, 4-wave blocks, one tile per wave, two blocks per
-                                  // CU); IGN_READOUT_VARIANT
+                                  // piece products (readout_bf); IGN_READOUT_VARIANT
   int ro_width = 0;
-  int seq_variant = 4;            // ordered-update kernel: 1 = U in VGPRs, 2 = U in LDS (more waves),
-                                  // 3 = 2 software-pipelined, 4/5 = split-bf16 h.U (6 / 9 piece products)
-  // Measured on 512 x synth50 (profiles/r01): one global length sort without XCD remap is the
-  // fastest order (seq 0.311 ms vs 0.320 graph-major); the alternatives stay selectable.
-  bool graph_major = false;       // destination order (see sort_order); IGN_GRAPH_MAJOR=1
-  int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels; IGN_XCD_REMAP=1
-  int sum_variant = 7;            // 64-wide sum update: 1 = weights streamed from L2, 2 = LDS,
-                                  // 7 = LDS + split-bf16 x.W / h.U (kernels_bf.hip),
-                                  // 3 = LDS + 4 messages in flight per lane, 4 = warp-specialised
-                                  // (producer waves gather, consumer waves MFMA), 5 = LDS + header /
-                                  // index prefetch one tile ahead; IGN_SUM_VARIANT
-  int sum_order = 0;              // sum MPs: 0 global in-degree sort, 1 sort within 256-row chunks
-                                  // (keeps id locality), 2 id order, 3 per-graph sort + XCD-aware
-                                  // tiles (one graph's source rows shared in one L2); IGN_SUM_ORDER
-  int ablate = 0;                 // diagnostics only (IGN_SEQ_ABLATE): results are wrong when set
+  int seq_variant = 4;            // ordered update: 4 / 5 = split-bf16 h.U with 6 / 9 piece products
+                                  // (H = 32, 64), 2 = f32 MFMA; IGN_SEQ_VARIANT
+  int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels (placement only; off:
+                                  // measured slower, profiles/r02/seq_experiments)
+  int sum_variant = 7;            // sum update: 7 = split-bf16 GRU step where available (DIN = H = 32
+                                  // or 64), 3 = f32 MFMA; IGN_SUM_VARIANT
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
   bool tsgemm_bf = true;          // weight-gradient row contractions on tsgemm_bf (IGN_TSGEMM_BF=0: f32 MFMA)
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
-  bool sum_split = false;         // plain sums as a gather-only kernel + the GRU step (IGN_SUM_SPLIT=1)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
                                   // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
                                   // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);

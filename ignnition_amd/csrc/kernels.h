@@ -26,8 +26,6 @@ struct SeqGruArgs {
   const float* bias;         // [4][H] combined biases
   int64_t n_dst;
   int xcd_remap;             // XCD-aware tile order (speed only)
-  int ablate;                // diagnostics: 1 = every step reads the zero row (see kernel)
-  int64_t zero_slot;         // index in step_code of a padding entry (= zero row)
   float* hs_save = nullptr;  // training: [n_steps + n_dst][H], order position p writes rows
                              // step_ptr[p] + p (state before) .. + len[p] (after each step)
   const void* Ubf = nullptr;  // variants 4/5: recurrent kernel as exact 3-piece bf16 A fragments
@@ -92,7 +90,7 @@ hipError_t launch_multi_sum(float* table, int64_t multi_base, int64_t n_multi, c
                             const uint32_t* rows, int W, const float* bias_row, hipStream_t st);
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st);
 // split-bf16 ordered update (kernels_bf.hip), passes 6 or 9
-hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int prefetch, hipStream_t st);
+hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStream_t st);
 // recurrent kernel -> split-bf16 A fragments for seq variants 4/5 (H = 32 or 64); floats used: 9 H^2 / 2
 hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H * H / 2 : 0; }
@@ -101,6 +99,8 @@ hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream
 inline int64_t pack_w_bf16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 9LL * K * H / 2 : 0; }
 // split-bf16 sum update (DIN = H = 64, no message weights / convolution); hipErrorInvalidValue otherwise
 hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t st);
+// sum update at DIN = H = 32: code-prefetched gather (gu rows in flight per lane), split-bf16 GRU step
+hipError_t launch_sum_gru_g32(const SumGruArgs& args, int gu, hipStream_t st);
 // split-bf16 form of the training row contraction (train_kernels.hip tsgemm; same grid and partials)
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
                             int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st);
@@ -120,8 +120,6 @@ struct SumWinArgs {
   int64_t n_wg;
 };
 hipError_t launch_sum_win(const SumWinArgs& args, int din, hipStream_t st);
-// the message gather of a plain sum update alone: xsum[dst row] = sum of its source rows
-hipError_t launch_sum_only(const SumGruArgs& args, int din, float* xsum, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

@@ -258,99 +258,10 @@ __global__ void multi_sum_kernel(float* __restrict__ table, int64_t multi_base, 
 // where several messages share the position.  Steps t >= final_len[d] leave the state
 // unchanged (sequence_mask); their (padded, always valid) codes are still read so the loop
 // has no data-dependent branch or select.
-template <int H>
-__global__ __launch_bounds__(256) void seq_gru_kernel(SeqGruArgs a) {
-  constexpr int NT = H / 16, KH = H / 4;
-  __shared__ float sbias[4 * H];
-  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t pos = (xcd_block(a.xcd_remap) * 4 + wave) * 16 + j;
-  const bool valid = pos < a.n_dst;
-
-  float u[3][NT][KH];   // recurrent kernel fragments, resident for the whole sequence
-#pragma unroll
-  for (int G = 0; G < 3; ++G)
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int s = 0; s < KH; ++s) u[G][t][s] = a.Up[frag_idx(G * NT + t, s, KH, lane)];
-
-  const int row = valid ? a.order[pos] : 0;
-  const int L = valid ? a.len[pos] : 0;
-  const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
-  const float* tab = a.table + 16 * 0 + 4 * g;
-
-  f4 h[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-
-  int Lmax = L;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
-  __syncthreads();
-
-  // Per step: issue the projected row of this step and the code of the next one, run the
-  // h.U MFMAs (independent of x: the accumulators start from the biases), then consume x in the
-  // gate math.  The sched_barriers keep the compiler from sinking the loads below the MFMAs or
-  // hoisting their consumers above them, so the gather latency hides under the MFMA block.
-  uint32_t code = codes[0];
-  for (int t = 0; t < Lmax; ++t) {
-    f4 x[3][NT];
-    {
-      const float* p = tab + (int64_t)code * (3 * H);
-#pragma unroll
-      for (int G = 0; G < 3; ++G)
-#pragma unroll
-        for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
-    }
-    const uint32_t next = codes[t + 1];
-    __builtin_amdgcn_sched_barrier(0);
-    f4 az[NT], ar[NT], ah[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      az[i] = f4{0, 0, 0, 0};
-      ar[i] = f4{0, 0, 0, 0};
-      ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
-    }
-#pragma unroll
-    for (int s = 0; s < KH; ++s) {
-      const float hb = h[s >> 2][s & 3];
-#pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        az[i] = MFMA(u[0][i][s], hb, az[i]);
-        ar[i] = MFMA(u[1][i][s], hb, ar[i]);
-        ah[i] = MFMA(u[2][i][s], hb, ah[i]);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const bool act = t < L;
-#pragma unroll
-    for (int i = 0; i < NT; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
-        const float z = sig2_(az[i][r] + x[0][i][r]);
-        const float rr = sig2_(ar[i][r] + x[1][i][r]);
-        const float c = tanh2_(x[2][i][r] + rr * ah[i][r]);
-        const float hn = c + z * (h[i][r] - c);
-        h[i][r] = act ? hn : h[i][r];
-      }
-    }
-    code = next;
-  }
-  if (valid) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Variant 2 of the ordered update: identical math to seq_gru_kernel, but the recurrent-kernel
-// fragments live in LDS (12 KB per block at H=32, shared by its 4 waves) instead of 48 VGPRs per
-// lane, so more waves fit per SIMD to hide the gather latency.  LDS image: float4 per lane
-// holding 4 consecutive k-steps, [gate][unit tile][k-step/4][lane] -> one ds_read_b128 feeds 4 MFMAs.
+// f32-MFMA form (v_mfma_f32_16x16x4_f32; the split-bf16 default is seq_gru_bf in kernels_bf.hip):
+// the recurrent-kernel fragments live in LDS (12 KB per block at H=32, shared by its 4 waves).
+// LDS image: float4 per lane holding 4 consecutive k-steps, [gate][unit tile][k-step/4][lane] ->
+// one ds_read_b128 feeds 4 MFMAs.  Also the training forward's SAVE form at H = 16.
 template <int H>
 __device__ __forceinline__ void stage_frag_lds(f4* dst, const float* __restrict__ src, int KS) {
   // src is already float4-grouped ([3][NT][KS/4][64] x f4): a straight vector copy
@@ -380,10 +291,7 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
   const bool valid = pos < a.n_dst;
   const int row = valid ? a.order[pos] : 0;
   const int L = valid ? a.len[pos] : 0;
-  // ablation (diagnostics only, IGN_SEQ_ABLATE=1): every step reads the zero row's code slot,
-  // so the gather hits one cached row while the instruction stream stays the same
-  const uint32_t* codes = a.ablate ? a.step_code + a.zero_slot
-                                   : a.step_code + (valid ? a.step_ptr[pos] : 0);
+  const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
   f4 h[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
@@ -463,185 +371,16 @@ __global__ __launch_bounds__(256) void seq_gru2_kernel(SeqGruArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Variant 3 of the ordered update: seq_gru2's math, software-pipelined across output tiles so
-// that a wave's gate VALU runs in the shadow of its own MFMAs.  In seq_gru2 a step is
-// [48 MFMAs] -> [gate VALU], strictly serial within the wave, so the matrix pipe idles while a
-// wave computes gates unless another wave happens to be in its MFMA block (measured 52 % busy).
-// Here the hidden state's unit tiles h[0..NT-1] are finished one at a time:
-//   acc_t[o] = sum_j U[j][o] h_{t-1}[j]   (j = input tile, o = output tile, per gate)
-// and h_t[o] needs only acc_t[o].  So step t issues, in order,
-//   V0   gates of tile NT-1 of step t-1           ||  M1  acc_t[*] += U[j][*] h_{t-1}[j], j < NT-1
-//   M2   acc_t[0] += U[NT-1][0] h_{t-1}[NT-1]
-//   M3_o acc_t[o+1] += U[NT-1][o+1] h_{t-1}[NT-1] ||  V_o gates of tile o of step t (o < NT-1)
-// and tile NT-1 of step t is carried into the next iteration (accP, xP, actP).  Same fma order
-// per accumulator as seq_gru2 (bias, then k ascending), so results are bitwise identical.
-template <int H>
-__device__ __forceinline__ f4 gru_gate_tile(const f4& az, const f4& ar, const f4& ah, const f4& xz, const f4& xr,
-                                            const f4& xh, const f4& h, bool act) {
-  f4 out;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float z = sig2_(az[r] + xz[r]);
-    const float rr = sig2_(ar[r] + xr[r]);
-    const float c = tanh2_(xh[r] + rr * ah[r]);
-    const float hn = c + z * (h[r] - c);
-    out[r] = act ? hn : h[r];
-  }
-  return out;
-}
-
-template <int H, bool SAVE>
-__global__ __launch_bounds__(256) void seq_gru3_kernel(SeqGruArgs a) {
-  constexpr int NT = H / 16, KH = H / 4, K4 = KH / 4;
-  static_assert(NT >= 2 && K4 == NT, "pipelining needs at least two unit tiles");
-  __shared__ float sbias[4 * H];
-  __shared__ f4 su[3 * NT * K4 * 64];
-  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
-  stage_frag_lds<H>(su, a.Up, KH);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  const float* tab = a.table + 4 * g;
-  __syncthreads();
-  const int64_t n_tiles = (a.n_dst + 15) / 16;
-  for (int64_t tile = xcd_block(a.xcd_remap) * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t pos = tile * 16 + j;
-    const bool valid = pos < a.n_dst;
-    const int row = valid ? a.order[pos] : 0;
-    const int L = valid ? a.len[pos] : 0;
-    const uint32_t* codes = a.ablate ? a.step_code + a.zero_slot
-                                     : a.step_code + (valid ? a.step_ptr[pos] : 0);
-    f4 h[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-    int Lmax = L;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
-    float* hsv = nullptr;
-    if constexpr (SAVE) {
-      hsv = a.hs_save + (valid ? (int64_t)a.step_ptr[pos] + pos : 0) * H + 4 * g;
-      if (valid) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
-      }
-    }
-
-    // pending tile NT-1 of the previous step (none before step 0: actP = false keeps h)
-    f4 accP[3] = {f4{0, 0, 0, 0}, f4{0, 0, 0, 0}, f4{0, 0, 0, 0}};
-    f4 xP[3] = {f4{0, 0, 0, 0}, f4{0, 0, 0, 0}, f4{0, 0, 0, 0}};
-    bool actP = false;
-    uint32_t code = codes[0];
-    for (int t = 0; t < Lmax; ++t) {
-      // V0: finish tile NT-1 of step t-1 (independent of M1 below; same basic block, so the
-      // scheduler can interleave the two)
-      h[NT - 1] = gru_gate_tile<H>(accP[0], accP[1], accP[2], xP[0], xP[1], xP[2], h[NT - 1], actP);
-      if constexpr (SAVE) {
-        if (actP && valid) st4(hsv + (int64_t)t * H + 16 * (NT - 1), h[NT - 1]);
-      }
-      f4 x[3][NT];
-      {
-        const float* p = tab + (int64_t)code * (3 * H);
-#pragma unroll
-        for (int G = 0; G < 3; ++G)
-#pragma unroll
-          for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
-      }
-      const uint32_t next = codes[t + 1];
-      f4 az[NT], ar[NT], ah[NT];
-#pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        az[i] = f4{0, 0, 0, 0};
-        ar[i] = f4{0, 0, 0, 0};
-        ah[i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
-      }
-      // M1: input tiles 0..NT-2 (ready since the previous iteration) into every output tile
-#pragma unroll
-      for (int s4 = 0; s4 < NT - 1; ++s4) {
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-          const f4 wz = su[((0 * NT + i) * K4 + s4) * 64 + lane];
-          const f4 wr = su[((1 * NT + i) * K4 + s4) * 64 + lane];
-          const f4 wh = su[((2 * NT + i) * K4 + s4) * 64 + lane];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float hb = h[s4][q];
-            az[i] = MFMA(wz[q], hb, az[i]);
-            ar[i] = MFMA(wr[q], hb, ar[i]);
-            ah[i] = MFMA(wh[q], hb, ah[i]);
-          }
-        }
-      }
-      // interleave V0's VALU with M1's MFMAs: the loads first, then {1 MFMA, 3 VALU} groups
-      __builtin_amdgcn_sched_group_barrier(0x0020, 3 * NT + 1, 0);   // VMEM reads (x row, code)
-      __builtin_amdgcn_sched_group_barrier(0x0100, 3 * NT, 0);       // DS reads (U fragments)
-#pragma unroll
-      for (int k = 0; k < 12 * NT * (NT - 1); ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x0002, 3, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const bool act = t < L;
-      // M2 / M3_o: input tile NT-1, output tile by output tile; gates of tile o follow its M
-#pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        {
-          constexpr int s4 = NT - 1;
-          const f4 wz = su[((0 * NT + i) * K4 + s4) * 64 + lane];
-          const f4 wr = su[((1 * NT + i) * K4 + s4) * 64 + lane];
-          const f4 wh = su[((2 * NT + i) * K4 + s4) * 64 + lane];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float hb = h[s4][q];
-            az[i] = MFMA(wz[q], hb, az[i]);
-            ar[i] = MFMA(wr[q], hb, ar[i]);
-            ah[i] = MFMA(wh[q], hb, ah[i]);
-          }
-        }
-        if (i >= 1) {   // V_{i-1}: tile i-1 of step t (h[NT-1] is still h_{t-1}: read above)
-          const int o = i - 1;
-          h[o] = gru_gate_tile<H>(az[o], ar[o], ah[o], x[0][o], x[1][o], x[2][o], h[o], act);
-          if constexpr (SAVE) {
-            if (act && valid) st4(hsv + (int64_t)(t + 1) * H + 16 * o, h[o]);
-          }
-        }
-      }
-      accP[0] = az[NT - 1];
-      accP[1] = ar[NT - 1];
-      accP[2] = ah[NT - 1];
-      xP[0] = x[0][NT - 1];
-      xP[1] = x[1][NT - 1];
-      xP[2] = x[2][NT - 1];
-      actP = act;
-      code = next;
-    }
-    h[NT - 1] = gru_gate_tile<H>(accP[0], accP[1], accP[2], xP[0], xP[1], xP[2], h[NT - 1], actP);
-    if constexpr (SAVE) {
-      if (actP && valid) st4(hsv + (int64_t)Lmax * H + 16 * (NT - 1), h[NT - 1]);
-    }
-    if (valid) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t]);
-    }
-  }  // tile loop
-}
-
-// ---------------------------------------------------------------------------------------------
 // Sum aggregation + single GRU step (AUX:254-262 then AUX:752-765).  Every destination is
 // updated, with x = 0 when it receives no message.  One wave = 16 destinations of similar
 // in-degree (sorted descending); each lane accumulates its quarter of the row in f32.
-// MODE 0 sum (AUX:261); 3 the same sum with the tile's message indices staged in LDS (IGN_SUM_VARIANT=6,
-// measured slower: 0.157 vs 0.112 ms on 512 x synth50); 1 attention: messages weighted by their
-// softmax coefficient (AUX:339-342);
+// MODE 0 sum (AUX:261); 1 attention: messages weighted by their softmax coefficient (AUX:339-342);
 // 2 convolution: x = act((sum_m h_src . K + h) / deg) (AUX:384-401; K.sum = sum.K, exact
 // reassociation).  Then one GRU step (AUX:764).
-constexpr int kIdxCap = 1024;   // MODE 3: staged message indices per wave
-
 template <int DIN, int H, int MODE>
 __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
   constexpr int NC = DIN / 16, NT = H / 16;
   __shared__ float sbias[4 * H];
-  __shared__ uint32_t sidx[MODE == 3 ? 4 : 1][MODE == 3 ? kIdxCap : 1];
   for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
 
   const int lane = threadIdx.x & 63;
@@ -663,46 +402,7 @@ __global__ __launch_bounds__(256) void sum_gru_kernel(SumGruArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
     int64_t m = m0;
-    if constexpr (MODE == 3) {
-      // plain sum with the tile's message indices staged in LDS: the 16 rows' CSR ranges are one
-      // contiguous range, read with coalesced loads in one memory round trip, so the row gathers
-      // no longer wait behind dependent index loads (18 -> 10 round trips at ~36 messages)
-      const int64_t p0 = tile * 16, p1 = p0 + 16 < a.n_dst ? p0 + 16 : a.n_dst;
-      const int64_t t0 = a.msg_ptr[p0], t1 = a.msg_ptr[p1];
-      uint32_t* sx = sidx[wave];
-      for (int64_t base = t0; base < t1; base += kIdxCap) {
-        const int cnt = (int)(t1 - base < kIdxCap ? t1 - base : kIdxCap);
-        for (int i = lane; i < cnt; i += 64) sx[i] = a.msg_src[base + i];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int64_t lo = m0 > base ? m0 : base, hi = m1 < base + cnt ? m1 : base + cnt;
-        int64_t q = lo;
-        for (; q + 4 <= hi; q += 4) {
-          const uint32_t* c = sx + (q - base);
-          const float* r0 = src_ptr(a.src, c[0], DIN);
-          const float* r1 = src_ptr(a.src, c[1], DIN);
-          const float* r2 = src_ptr(a.src, c[2], DIN);
-          const float* r3 = src_ptr(a.src, c[3], DIN);
-          f4 v0[NC], v1[NC], v2[NC], v3[NC];
-#pragma unroll
-          for (int cc = 0; cc < NC; ++cc) {
-            v0[cc] = ld4(r0 + 16 * cc + 4 * g);
-            v1[cc] = ld4(r1 + 16 * cc + 4 * g);
-            v2[cc] = ld4(r2 + 16 * cc + 4 * g);
-            v3[cc] = ld4(r3 + 16 * cc + 4 * g);
-          }
-#pragma unroll
-          for (int cc = 0; cc < NC; ++cc) x[cc] = (((x[cc] + v0[cc]) + v1[cc]) + v2[cc]) + v3[cc];
-        }
-        for (; q < hi; ++q) {
-          const float* r = src_ptr(a.src, sx[q - base], DIN);
-#pragma unroll
-          for (int cc = 0; cc < NC; ++cc) x[cc] += ld4(r + 16 * cc + 4 * g);
-        }
-        __builtin_amdgcn_wave_barrier();   // every lane is done with sx before the next chunk
-      }
-    } else if constexpr (MODE == 1) {
+    if constexpr (MODE == 1) {
       for (; m < m1; ++m) {
         const float w = a.msg_w[m];
         const float* p = src_ptr(a.src, a.msg_src[m], DIN);
@@ -820,47 +520,6 @@ __global__ __launch_bounds__(1024) void sum_win_kernel(SumWinArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Split sum update, part 1 (IGN_SUM_SPLIT=1): the message gather of sum_gru without the GRU
-// weights, so the kernel is small (≈40 VGPRs, 8 waves/SIMD) and keeps 8 source rows in flight per
-// lane; x[dst row] is written and the GRU step runs on it through an identity CSR.
-template <int DIN>
-__global__ __launch_bounds__(256) void sum_only_kernel(SumGruArgs a, float* __restrict__ xsum) {
-  constexpr int NC = DIN / 16, GU = 8;
-  const int lane = threadIdx.x & 63;
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t pos = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + j;
-  const bool valid = pos < a.n_dst;
-  const int row = valid ? a.order[pos] : 0;
-  const int64_t m0 = valid ? a.msg_ptr[pos] : 0, m1 = valid ? a.msg_ptr[pos + 1] : 0;
-  f4 x[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
-  int64_t m = m0;
-  for (; m + GU <= m1; m += GU) {
-    f4 v[GU][NC];
-#pragma unroll
-    for (int u = 0; u < GU; ++u) {
-      const float* p = src_ptr(a.src, a.msg_src[m + u], DIN);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
-    }
-#pragma unroll
-    for (int u = 0; u < GU; ++u)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] += v[u][c];
-  }
-  for (; m < m1; ++m) {
-    const float* p = src_ptr(a.src, a.msg_src[m], DIN);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
-  }
-  if (valid) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) st4(xsum + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
-  }
-}
-
 // Attention softmax weights: one wave per (graph, position) group.
 __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63;
@@ -907,103 +566,6 @@ __global__ void attn_vectors_kernel(const float* __restrict__ K1, const float* _
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sum update for wide cells (H or DIN = 64, e.g. the 1M-node synthetic graph): the 2 x 3H x K
-// weight fragments (96 KB at 64/64) fit neither in registers nor comfortably in LDS, so they
-// stream from L2 as float4 (4 k-steps) per lane, reused across the 16 rows of the tile.
-template <int DIN, int H>
-__global__ __launch_bounds__(256) void sum_gru_wide_kernel(SumGruArgs a) {
-  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16;
-  __shared__ float sbias[4 * H];
-  for (int i = threadIdx.x; i < 4 * H; i += blockDim.x) sbias[i] = a.bias[i];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t pos = (xcd_block(a.xcd_remap) * 4 + wave) * 16 + j;
-  const bool valid = pos < a.n_dst;
-  const int row = valid ? a.order[pos] : 0;
-  const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
-  const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
-
-  f4 x[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
-  int64_t m = m0;
-  for (; m + 2 <= m1; m += 2) {
-    const float* p0 = src_ptr(a.src, a.msg_src[m], DIN);
-    const float* p1 = src_ptr(a.src, a.msg_src[m + 1], DIN);
-    f4 v0[NC], v1[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      v0[c] = ld4(p0 + 16 * c + 4 * g);
-      v1[c] = ld4(p1 + 16 * c + 4 * g);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
-  }
-  for (; m < m1; ++m) {
-    const float* p = src_ptr(a.src, a.msg_src[m], DIN);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
-  }
-  f4 h[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-  if (a.x_save && valid) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
-  }
-  __syncthreads();
-
-  const f4* W4 = reinterpret_cast<const f4*>(a.Wp);
-  const f4* U4 = reinterpret_cast<const f4*>(a.Up);
-  f4 hn[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int u0 = 16 * t + 4 * g;
-    f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
-    f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
-    f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
-    f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
-#pragma unroll
-    for (int s4 = 0; s4 < X4; ++s4) {
-      const f4 wz = W4[((0 * NT + t) * X4 + s4) * 64 + lane];
-      const f4 wr = W4[((1 * NT + t) * X4 + s4) * 64 + lane];
-      const f4 wh = W4[((2 * NT + t) * X4 + s4) * 64 + lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float xb = x[s4][q];
-        az = MFMA(wz[q], xb, az);
-        ar = MFMA(wr[q], xb, ar);
-        ax = MFMA(wh[q], xb, ax);
-      }
-    }
-#pragma unroll
-    for (int s4 = 0; s4 < H4; ++s4) {
-      const f4 wz = U4[((0 * NT + t) * H4 + s4) * 64 + lane];
-      const f4 wr = U4[((1 * NT + t) * H4 + s4) * 64 + lane];
-      const f4 wh = U4[((2 * NT + t) * H4 + s4) * 64 + lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float hb = h[s4][q];
-        az = MFMA(wz[q], hb, az);
-        ar = MFMA(wr[q], hb, ar);
-        ah = MFMA(wh[q], hb, ah);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float z = sig2_(az[r]);
-      const float rr = sig2_(ar[r]);
-      const float c = tanh2_(ax[r] + rr * ah[r]);
-      hn[t][r] = c + z * (h[t][r] - c);
-    }
-  }
-  if (valid) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
-  }
-}
-
 // Sum update for wide cells with the weights in LDS: W and U fragments (96 KB at 64/64) are
 // staged once per block, so the per-tile weight stream (96 KB per 16 rows) comes from LDS
 // instead of L2.  One 12-wave block per CU (3 waves per SIMD), persistent over the
@@ -1124,287 +686,6 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_lds_kernel(SumGruArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
     }
-  }
-}
-
-// Sum update for wide cells, W/U in LDS, with the gather's dependent loads taken off the
-// critical path: the next tile's header (order, msg_ptr) is loaded while this tile gathers,
-// and its first NI message indices while this tile runs its MFMAs, so a tile's gather starts
-// with all row addresses known and issues GU rows per lane back to back.
-template <int DIN, int H, int WAVES, int GU, int NI>
-__global__ __launch_bounds__(64 * WAVES) void sum_gru_pf_kernel(SumGruArgs a) {
-  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16;
-  constexpr int WF = 3 * NT * X4 * 64, UF = 3 * NT * H4 * 64;
-  __shared__ f4 sW[WF];
-  __shared__ f4 sU[UF];
-  __shared__ float sbias[4 * H];
-  {
-    const f4* gW = reinterpret_cast<const f4*>(a.Wp);
-    const f4* gU = reinterpret_cast<const f4*>(a.Up);
-    for (int i = threadIdx.x; i < WF; i += 64 * WAVES) sW[i] = gW[i];
-    for (int i = threadIdx.x; i < UF; i += 64 * WAVES) sU[i] = gU[i];
-    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) sbias[i] = a.bias[i];
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t n_tiles = (a.n_dst + 15) / 16;
-  const int64_t step = (int64_t)gridDim.x * WAVES;
-  int64_t tile = xcd_block(a.xcd_remap) * WAVES + wave;
-
-  int row_n;
-  int64_t m0_n, m1_n;
-  uint32_t idx_n[NI];
-  auto load_hdr = [&](int64_t t) {
-    const int64_t pos = t * 16 + j;
-    const bool ok = t < n_tiles && pos < a.n_dst;
-    row_n = ok ? a.order[pos] : -1;
-    m0_n = ok ? a.msg_ptr[pos] : 0;
-    m1_n = ok ? a.msg_ptr[pos + 1] : 0;
-  };
-  auto load_idx = [&]() {
-#pragma unroll
-    for (int k = 0; k < NI; ++k) idx_n[k] = m0_n + k < m1_n ? a.msg_src[m0_n + k] : 0u;
-  };
-  load_hdr(tile);
-  load_idx();
-  for (; tile < n_tiles; tile += step) {
-    const int row = row_n;
-    const int64_t m0 = m0_n, m1 = m1_n;
-    uint32_t idx[NI];
-#pragma unroll
-    for (int k = 0; k < NI; ++k) idx[k] = idx_n[k];
-    load_hdr(tile + step);                   // consumed after the gather
-    const bool valid = row >= 0;
-    f4 h[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-    const int deg = (int)(m1 - m0);
-    int dmax = deg;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o));
-    f4 x[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
-#pragma unroll
-    for (int c0 = 0; c0 < NI; c0 += GU) {
-      if (c0 < dmax) {
-        f4 v[GU][NC];
-#pragma unroll
-        for (int u = 0; u < GU; ++u) {
-          const float* p = src_ptr(a.src, idx[c0 + u], DIN);
-#pragma unroll
-          for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
-        }
-#pragma unroll
-        for (int u = 0; u < GU; ++u) {
-          const bool ok = c0 + u < deg;
-#pragma unroll
-          for (int c = 0; c < NC; ++c) x[c] = ok ? x[c] + v[u][c] : x[c];
-        }
-      }
-    }
-    for (int64_t m = m0 + NI; m < m1; ++m) {   // rows with more than NI messages
-      const float* p = src_ptr(a.src, a.msg_src[m], DIN);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
-    }
-    load_idx();                              // next tile's indices land during the MFMAs
-    int wofs = lane;
-    asm volatile("" : "+v"(wofs));
-    f4 hn[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int u0 = 16 * t + 4 * g;
-      f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
-      f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
-      f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
-      f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
-#pragma unroll
-      for (int s4 = 0; s4 < X4; ++s4) {
-        const f4 wz = sW[((0 * NT + t) * X4 + s4) * 64 + wofs];
-        const f4 wr = sW[((1 * NT + t) * X4 + s4) * 64 + wofs];
-        const f4 wh = sW[((2 * NT + t) * X4 + s4) * 64 + wofs];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float xb = x[s4][q];
-          az = MFMA(wz[q], xb, az);
-          ar = MFMA(wr[q], xb, ar);
-          ax = MFMA(wh[q], xb, ax);
-        }
-      }
-#pragma unroll
-      for (int s4 = 0; s4 < H4; ++s4) {
-        const f4 wz = sU[((0 * NT + t) * H4 + s4) * 64 + wofs];
-        const f4 wr = sU[((1 * NT + t) * H4 + s4) * 64 + wofs];
-        const f4 wh = sU[((2 * NT + t) * H4 + s4) * 64 + wofs];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float hb = h[s4][q];
-          az = MFMA(wz[q], hb, az);
-          ar = MFMA(wr[q], hb, ar);
-          ah = MFMA(wh[q], hb, ah);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = sig2_(az[r]);
-        const float rr = sig2_(ar[r]);
-        const float c = tanh2_(ax[r] + rr * ah[r]);
-        hn[t][r] = c + z * (h[t][r] - c);
-      }
-    }
-    if (valid) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
-    }
-  }
-}
-
-// Warp-specialised sum update for wide cells.  A 16-wave block per CU: 8 producer waves gather
-// and sum the messages of the next 8 tiles (16 destinations each) into an LDS x buffer while 8
-// consumer waves run the GRU MFMAs of the current 8 tiles with W/U fragments from LDS.  The
-// gather latency is then hidden behind the MFMA pipe instead of stalling it.  Per phase:
-//   consumers copy their x tile from LDS to registers and issue their h loads | barrier |
-//   producers gather phase p+1 into LDS; consumers compute phase p           | barrier
-template <int DIN, int H, int GU>
-__global__ __launch_bounds__(1024) void sum_gru_ws_kernel(SumGruArgs a) {
-  constexpr int NC = DIN / 16, NT = H / 16, X4 = DIN / 16, H4 = H / 16, CW = 8;
-  constexpr int WF = 3 * NT * X4 * 64, UF = 3 * NT * H4 * 64;
-  __shared__ f4 sW[WF];
-  __shared__ f4 sU[UF];
-  __shared__ f4 sx[CW * NC * 64];
-  __shared__ float sbias[4 * H];
-  {
-    const f4* gW = reinterpret_cast<const f4*>(a.Wp);
-    const f4* gU = reinterpret_cast<const f4*>(a.Up);
-    for (int i = threadIdx.x; i < WF; i += 1024) sW[i] = gW[i];
-    for (int i = threadIdx.x; i < UF; i += 1024) sU[i] = gU[i];
-    for (int i = threadIdx.x; i < 4 * H; i += 1024) sbias[i] = a.bias[i];
-  }
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const bool producer = wave >= CW;
-  const int slot = wave & (CW - 1);          // tile of the phase this wave produces / consumes
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t n_tiles = (a.n_dst + 15) / 16;
-  const int64_t n_groups = (n_tiles + CW - 1) / CW;
-  const int64_t stride = gridDim.x;
-  int64_t q = xcd_block(a.xcd_remap);
-
-  auto gather = [&](int64_t grp) {           // producers: x of tile (grp, slot) -> sx
-    const int64_t pos = (grp * CW + slot) * 16 + j;
-    const bool valid = grp < n_groups && pos < a.n_dst;
-    const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
-    const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
-    f4 x[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
-    int64_t m = m0;
-    for (; m + GU <= m1; m += GU) {
-      f4 v[GU][NC];
-#pragma unroll
-      for (int u = 0; u < GU; ++u) {
-        const float* p = src_ptr(a.src, a.msg_src[m + u], DIN);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
-      }
-#pragma unroll
-      for (int u = 0; u < GU; ++u)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) x[c] += v[u][c];
-    }
-    for (; m + 2 <= m1; m += 2) {
-      const float* p0 = src_ptr(a.src, a.msg_src[m], DIN);
-      const float* p1 = src_ptr(a.src, a.msg_src[m + 1], DIN);
-      f4 v0[NC], v1[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        v0[c] = ld4(p0 + 16 * c + 4 * g);
-        v1[c] = ld4(p1 + 16 * c + 4 * g);
-      }
-#pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
-    }
-    for (; m < m1; ++m) {
-      const float* p = src_ptr(a.src, a.msg_src[m], DIN);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) sx[(slot * NC + c) * 64 + lane] = x[c];
-  };
-
-  if (producer && q < n_groups) gather(q);
-  __syncthreads();
-  for (; q < n_groups; q += stride) {
-    f4 x[NC], h[NT];
-    int row = 0;
-    bool valid = false;
-    if (!producer) {
-      const int64_t pos = (q * CW + slot) * 16 + j;
-      valid = pos < a.n_dst;
-      row = valid ? a.order[pos] : 0;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) x[c] = sx[(slot * NC + c) * 64 + lane];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-    }
-    __syncthreads();
-    if (producer) {
-      if (q + stride < n_groups) gather(q + stride);
-    } else {
-      int wofs = lane;                       // opaque: keeps the weight reads inside the loop
-      asm volatile("" : "+v"(wofs));
-      f4 hn[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int u0 = 16 * t + 4 * g;
-        f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0);
-        f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0);
-        f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0);
-        f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0);
-#pragma unroll
-        for (int s4 = 0; s4 < X4; ++s4) {
-          const f4 wz = sW[((0 * NT + t) * X4 + s4) * 64 + wofs];
-          const f4 wr = sW[((1 * NT + t) * X4 + s4) * 64 + wofs];
-          const f4 wh = sW[((2 * NT + t) * X4 + s4) * 64 + wofs];
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float xb = x[s4][qq];
-            az = MFMA(wz[qq], xb, az);
-            ar = MFMA(wr[qq], xb, ar);
-            ax = MFMA(wh[qq], xb, ax);
-          }
-        }
-#pragma unroll
-        for (int s4 = 0; s4 < H4; ++s4) {
-          const f4 wz = sU[((0 * NT + t) * H4 + s4) * 64 + wofs];
-          const f4 wr = sU[((1 * NT + t) * H4 + s4) * 64 + wofs];
-          const f4 wh = sU[((2 * NT + t) * H4 + s4) * 64 + wofs];
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float hb = h[s4][qq];
-            az = MFMA(wz[qq], hb, az);
-            ar = MFMA(wr[qq], hb, ar);
-            ah = MFMA(wh[qq], hb, ah);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float z = sig2_(az[r]);
-          const float rr = sig2_(ar[r]);
-          const float c = tanh2_(ax[r] + rr * ah[r]);
-          hn[t][r] = c + z * (h[t][r] - c);
-        }
-      }
-      if (valid) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
-      }
-    }
-    __syncthreads();
   }
 }
 
@@ -1638,47 +919,20 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) 
 
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (variant >= 4 && (h == 32 || h == 64))   // split-bf16 h.U (kernels_bf.hip); 6: + row prefetch
-    return launch_seq_gru_bf(args, h, variant == 5 ? 9 : 6, variant == 6, st);
-  if (variant == 3 && h >= 32) {   // pipelined (needs >= 2 unit tiles)
-    const int64_t work = grid_for(args.n_dst, 64);
-    if (h == 32) {
-      auto k = args.hs_save ? seq_gru3_kernel<32, true> : seq_gru3_kernel<32, false>;
-      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
-    } else if (h == 64) {
-      auto k = args.hs_save ? seq_gru3_kernel<64, true> : seq_gru3_kernel<64, false>;
-      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
-    } else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
-  if (variant >= 2) {
-    const int64_t work = grid_for(args.n_dst, 64);
-    if (h == 32) {
-      auto k = args.hs_save ? seq_gru2_kernel<32, true> : seq_gru2_kernel<32, false>;
-      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
-    } else if (h == 16) {
-      auto k = args.hs_save ? seq_gru2_kernel<16, true> : seq_gru2_kernel<16, false>;
-      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
-    } else if (h == 64) {
-      auto k = args.hs_save ? seq_gru2_kernel<64, true> : seq_gru2_kernel<64, false>;
-      hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
-    } else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
-  dim3 grid(grid_for(args.n_dst, 64)), block(256);
-  if (h == 32) hipLaunchKernelGGL((seq_gru_kernel<32>), grid, block, 0, st, args);
-  else if (h == 16) hipLaunchKernelGGL((seq_gru_kernel<16>), grid, block, 0, st, args);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-hipError_t launch_sum_only(const SumGruArgs& args, int din, float* xsum, hipStream_t st) {
-  if (args.n_dst == 0) return hipSuccess;
-  const dim3 grid((unsigned)((args.n_dst + 63) / 64)), block(256);
-  if (din == 32) hipLaunchKernelGGL((sum_only_kernel<32>), grid, block, 0, st, args, xsum);
-  else if (din == 16) hipLaunchKernelGGL((sum_only_kernel<16>), grid, block, 0, st, args, xsum);
-  else if (din == 64) hipLaunchKernelGGL((sum_only_kernel<64>), grid, block, 0, st, args, xsum);
-  else return hipErrorInvalidValue;
+  // 4 / 5: split-bf16 h.U with 6 / 9 piece products (kernels_bf.hip; H = 32, 64); 2: f32 MFMA
+  if ((variant == 4 || variant == 5) && (h == 32 || h == 64))
+    return launch_seq_gru_bf(args, h, variant == 5 ? 9 : 6, st);
+  const int64_t work = grid_for(args.n_dst, 64);
+  if (h == 32) {
+    auto k = args.hs_save ? seq_gru2_kernel<32, true> : seq_gru2_kernel<32, false>;
+    hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
+  } else if (h == 16) {
+    auto k = args.hs_save ? seq_gru2_kernel<16, true> : seq_gru2_kernel<16, false>;
+    hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
+  } else if (h == 64) {
+    auto k = args.hs_save ? seq_gru2_kernel<64, true> : seq_gru2_kernel<64, false>;
+    hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);
+  } else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -1698,23 +952,17 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
   // (0.109 vs 0.141 ms on 512 x synth50): more independent waves queue behind the resident ones
   dim3 grid(grid_for(args.n_dst, 64));
   const int mode = args.conv_kp ? 2 : args.msg_w ? 1 : 0;
+  // variant 7 (default): split-bf16 GRU step where its kernels exist (plain sums at DIN = H = 32
+  // or 64); otherwise the f32-MFMA kernels
+  if (din == 32 && h == 32 && mode == 0 && variant == 7 && args.Wbf && args.Ubf)
+    return launch_sum_gru_g32(args, 6, st);   // 6 rows in flight: 0.100 ms vs 0.105 (8), 0.108 (4)
 #define SUM_CASE(D, HH)                                                                    \
   if (din == D && h == HH) {                                                               \
     if (mode == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 1>), grid, dim3(256), 0, st, args); \
     else if (mode == 2 && D == HH) hipLaunchKernelGGL((sum_gru_kernel<D, (D == HH ? HH : D), (D == HH ? 2 : 0)>), grid, dim3(256), 0, st, args); \
     else if (mode == 2) return hipErrorInvalidValue;                                       \
-    else if (variant == 6) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 3>), grid, dim3(256), 0, st, args); \
     else hipLaunchKernelGGL((sum_gru_kernel<D, HH, 0>), grid, dim3(256), 0, st, args);    \
     return hipGetLastError();                                                              \
-  }
-  if (din == 32 && h == 32 && mode == 0 && (variant == 4 || variant == 5)) {   // measured slower: diagnostics
-    // W/U fragments in LDS (24 KB per block) instead of 96 VGPRs: 4-5 waves per SIMD instead of 2
-    // (0.124-0.137 ms vs 0.114 on 512 x synth50: more waves did not help)
-    constexpr int WV = 4;
-    auto kern = variant == 5 ? sum_gru_lds_kernel<32, 32, WV, 8> : sum_gru_lds_kernel<32, 32, WV, 4>;
-    const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
-    hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
-    return hipGetLastError();
   }
   SUM_CASE(32, 32)
   SUM_CASE(16, 16)
@@ -1724,24 +972,10 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
   if (din == 64 && h == 64) {
     if (mode != 0) return hipErrorInvalidValue;
     if (variant == 7 && args.Wbf && args.Ubf) return launch_sum_gru_bf(args, din, h, st);
-    if (variant == 7) variant = 3;
-    if (variant == 5) {
-      constexpr int WV = 12;
-      auto kern = sum_gru_pf_kernel<64, 64, WV, 4, 16>;
-      const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
-      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
-    } else if (variant == 4) {
-      auto kern = sum_gru_ws_kernel<64, 64, 4>;
-      const int64_t work = (args.n_dst + 127) / 128;
-      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 1024)), dim3(1024), 0, st, args);
-    } else if (variant >= 2) {
-      constexpr int WV = 12;
-      auto kern = variant == 3 ? sum_gru_lds_kernel<64, 64, WV, 4> : sum_gru_lds_kernel<64, 64, WV, 2>;
-      const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
-      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
-    } else {
-      hipLaunchKernelGGL((sum_gru_wide_kernel<64, 64>), grid, dim3(256), 0, st, args);
-    }
+    constexpr int WV = 12;   // f32 MFMA, W / U in LDS, 4 rows in flight per lane
+    auto kern = sum_gru_lds_kernel<64, 64, WV, 4>;
+    const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
+    hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
     return hipGetLastError();
   }
   return hipErrorInvalidValue;

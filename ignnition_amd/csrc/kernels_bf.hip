@@ -63,7 +63,7 @@ __global__ void pack_u_bf16_kernel(const float* __restrict__ U, uint16_t* __rest
   }
 }
 
-template <int H, bool SAVE, int PASSES, bool PF>
+template <int H, bool SAVE, int PASSES>
 __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
   constexpr int NT = H / 16, KS = H / 32;
   constexpr int NF = 9 * NT * KS;            // fragments: 3 pieces x 3 gates x NT tiles x KS k-steps
@@ -102,38 +102,20 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
         for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
       }
     }
+    // the projected row of step t is loaded at the start of step t and consumed by the gates after
+    // the h.U MFMAs (measured faster than a one-step-ahead prefetch at 3 waves per SIMD or seeded
+    // into the first MFMA's C operand: profiles/r02/seq_experiments)
     uint32_t code = codes[0];
-    // PF: the projected row of step t+1 is loaded during step t, and its z / r parts seed the
-    // accumulators (x + h.U instead of h.U, then + x: 16 fewer adds per step)
-    f4 xn[3][NT];
-    if constexpr (PF) {
-      const float* p = tab + (int64_t)code * (3 * H);
-#pragma unroll
-      for (int G = 0; G < 3; ++G)
-#pragma unroll
-        for (int i = 0; i < NT; ++i) xn[G][i] = ld4(p + G * H + 16 * i);
-      code = codes[1];
-    }
     for (int t = 0; t < Lmax; ++t) {
       f4 x[3][NT];
-      if constexpr (PF) {
-#pragma unroll
-        for (int G = 0; G < 3; ++G)
-#pragma unroll
-          for (int i = 0; i < NT; ++i) x[G][i] = xn[G][i];
-        const float* p = tab + (int64_t)code * (3 * H);
-#pragma unroll
-        for (int G = 0; G < 3; ++G)
-#pragma unroll
-          for (int i = 0; i < NT; ++i) xn[G][i] = ld4(p + G * H + 16 * i);
-      } else {
+      {
         const float* p = tab + (int64_t)code * (3 * H);
 #pragma unroll
         for (int G = 0; G < 3; ++G)
 #pragma unroll
           for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
       }
-      const uint32_t next = codes[t + (PF ? 2 : 1)];
+      const uint32_t next = codes[t + 1];
       // B fragments: the three exact bf16 pieces of the state, k-step s = accumulator tiles 2s, 2s+1
       bf8 hf[3][KS];
 #pragma unroll
@@ -156,8 +138,8 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
       f4 acc[3][NT];
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        acc[0][i] = PF ? x[0][i] : f4{0, 0, 0, 0};
-        acc[1][i] = PF ? x[1][i] : f4{0, 0, 0, 0};
+        acc[0][i] = f4{0, 0, 0, 0};
+        acc[1][i] = f4{0, 0, 0, 0};
         acc[2][i] = *reinterpret_cast<const f4*>(sbias + 3 * H + 16 * i + 4 * g);
       }
       // the fragment reads are loop-invariant: an opaque lane offset keeps the compiler from
@@ -190,8 +172,8 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
-          const float z = sig2_(PF ? acc[0][i][r] : acc[0][i][r] + x[0][i][r]);
-          const float rr = sig2_(PF ? acc[1][i][r] : acc[1][i][r] + x[1][i][r]);
+          const float z = sig2_(acc[0][i][r] + x[0][i][r]);
+          const float rr = sig2_(acc[1][i][r] + x[1][i][r]);
           const float c = tanh2_(x[2][i][r] + rr * acc[2][i][r]);
           const float hn = c + z * (h[i][r] - c);
           h[i][r] = act ? hn : h[i][r];
@@ -372,6 +354,138 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_bf_kernel(SumGruArgs a) {
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sum update at DIN = H = 32 (RouteNet's path -> link MP): a latency-bound gather of ~36 scattered
+// 128-B rows per destination, then one GRU step.  One 16-destination tile per wave, no persistent
+// loop (waves that finish free their slot for a new tile at once).  Against sum_gru_kernel<32,32>:
+//  * the message codes of group k+1 load while the rows of group k are in flight (one memory
+//    round trip per group instead of two); GU rows per lane in flight, codes clamped to the
+//    destination's range (no branches around loads) and the adds predicated, in message order;
+//  * the GRU step on the split-bf16 path (x6) with W / U pieces in LDS, staged by LDS-DMA while
+//    the gather runs, instead of 96 f32 MFMAs with the weights in 96 VGPRs: about half the
+//    registers, so twice the waves (and rows in flight) per SIMD.
+// The message sum associates exactly as in sum_gru_kernel (one message at a time, in CSR order).
+template <int GU>
+__global__ __launch_bounds__(256) void sum_gru_g32_kernel(SumGruArgs a) {
+  constexpr int DIN = 32, H = 32, NC = 2, NT = 2, NF = 18;   // fragments per matrix
+  __shared__ bf8 sw[2 * NF * 64];                              // W pieces | U pieces
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  {   // 36 KB: 9 LDS-DMA pieces of 1 KB per wave, in flight during the gather
+    const u4v* gw = static_cast<const u4v*>(a.Wbf);
+    const u4v* gu = static_cast<const u4v*>(a.Ubf);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int piece = k * 4 + wave;                          // 0 .. 35
+      const u4v* src = piece < NF ? gw + piece * 64 + lane : gu + (piece - NF) * 64 + lane;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(sw + piece * 64), 16, 0, 0);
+    }
+  }
+  const int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t pos = tile * 16 + j;
+  const bool valid = pos < a.n_dst;
+  const int row = valid ? a.order[pos] : 0;
+  const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+  const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+  const int64_t last = m1 > 0 ? m1 - 1 : 0;
+  f4 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+  uint32_t cc[GU];
+#pragma unroll
+  for (int u = 0; u < GU; ++u) cc[u] = a.msg_src[m0 + u < last ? m0 + u : last];
+  for (int64_t m = m0; m < m1; m += GU) {
+    f4 v[GU][NC];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const float* p = src_row_bf(a.src, cc[u], DIN) + 4 * g;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) cc[u] = a.msg_src[m + GU + u < last ? m + GU + u : last];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const bool on = m + u < m1;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const f4 s = x[c] + v[u][c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[c][q] = on ? s[q] : x[c][q];
+      }
+    }
+  }
+  if (a.x_save && valid) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+  }
+  f4 h[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+  f4 bz[NT], br[NT], bx[NT], bh[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int u0 = 16 * t + 4 * g;
+    bz[t] = ld4(a.bias + 0 * H + u0);
+    br[t] = ld4(a.bias + 1 * H + u0);
+    bx[t] = ld4(a.bias + 2 * H + u0);
+    bh[t] = ld4(a.bias + 3 * H + u0);
+  }
+  bf8 xf[3][1], hf[3][1];
+  split_frags<1>(x, xf);
+  split_frags<1>(h, hf);
+  __syncthreads();   // the block's LDS-DMA pieces have landed
+  const bf8* sW = sw;
+  const bf8* sU = sw + NF * 64;
+  f4 hn[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f4 az = bz[t], ar = br[t], ax = bx[t], ah = bh[t];
+#pragma unroll
+    for (int pu = 2; pu >= 0; --pu) {   // as sum_gru_bf: weight piece major, small products first
+      const bf8 wz = sW[((pu * 3 + 0) * NT + t) * 64 + lane];
+      const bf8 wr = sW[((pu * 3 + 1) * NT + t) * 64 + lane];
+      const bf8 wh = sW[((pu * 3 + 2) * NT + t) * 64 + lane];
+#pragma unroll
+      for (int ph = 2 - pu; ph >= 0; --ph) {
+        az = MFMA_BF(wz, xf[ph][0], az);
+        ar = MFMA_BF(wr, xf[ph][0], ar);
+        ax = MFMA_BF(wh, xf[ph][0], ax);
+      }
+      const bf8 uz = sU[((pu * 3 + 0) * NT + t) * 64 + lane];
+      const bf8 ur = sU[((pu * 3 + 1) * NT + t) * 64 + lane];
+      const bf8 uh = sU[((pu * 3 + 2) * NT + t) * 64 + lane];
+#pragma unroll
+      for (int ph = 2 - pu; ph >= 0; --ph) {
+        az = MFMA_BF(uz, hf[ph][0], az);
+        ar = MFMA_BF(ur, hf[ph][0], ar);
+        ah = MFMA_BF(uh, hf[ph][0], ah);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = sig2_(az[r]);
+      const float rr = sig2_(ar[r]);
+      const float c = tanh2_(ax[r] + rr * ah[r]);
+      hn[t][r] = c + z * (h[t][r] - c);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
+  }
+}
+
+hipError_t launch_sum_gru_g32(const SumGruArgs& args, int gu, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  if (!args.Wbf || !args.Ubf || args.msg_w || args.conv_kp) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((args.n_dst + 63) / 64));
+  if (gu != 6) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sum_gru_g32_kernel<6>, grid, dim3(256), 0, st, args);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -795,29 +909,19 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
   }
 }
 
-hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, int prefetch, hipStream_t st) {
+hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (!args.Ubf || (h != 32 && h != 64)) return hipErrorInvalidValue;
+  if (!args.Ubf || (h != 32 && h != 64) || (passes != 6 && passes != 9)) return hipErrorInvalidValue;
   const int64_t work = grid_for(args.n_dst, 64);
 #define SEQ_BF(HH, P)                                                                              \
   {                                                                                                \
-    auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P, PFX> : seq_gru_bf_kernel<HH, false, P, PFX>; \
+    auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P> : seq_gru_bf_kernel<HH, false, P>;      \
     hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);                \
   }
-  if (h == 32 && passes == 6) {
-    if (prefetch) {
-      constexpr bool PFX = true;
-      SEQ_BF(32, 6)
-    } else {
-      constexpr bool PFX = false;
-      SEQ_BF(32, 6)
-    }
-  } else {
-    constexpr bool PFX = false;
-    if (h == 32) SEQ_BF(32, 9)
-    else if (passes == 6) SEQ_BF(64, 6)
-    else SEQ_BF(64, 9)
-  }
+  if (h == 32 && passes == 6) SEQ_BF(32, 6)
+  else if (h == 32) SEQ_BF(32, 9)
+  else if (passes == 6) SEQ_BF(64, 6)
+  else SEQ_BF(64, 9)
 #undef SEQ_BF
   return hipGetLastError();
 }
@@ -847,17 +951,9 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f) return hipErrorInvalidValue;
   // default (passes 6): two 16-row tiles per wave sharing every W2 fragment read, 8-wave blocks
   // (246 VGPRs, 2 waves/SIMD): 1.03-1.05 ms against 1.13-1.16 ms for one tile per wave in 12-wave
-  // blocks (-8), 512 x synth50. Diagnostics: -6 = 32-unit W2 chunks (1.18 ms), -7 = 4-wave blocks
-  // with W1 from L2, -9 = two tiles per wave in 4-wave blocks, two blocks per CU (1.39-1.41 ms).
-  if (din == 32) {
-    if (passes == -6) return readout_bf_din<32, 12, 6, 2>(args, W1f, W2f, st);
-    if (passes == -7) return readout_bf_din<32, 4, 6, 1, false>(args, W1f, W2f, st);
-    if (passes == -8) return readout_bf_din<32, 12, 6, 1>(args, W1f, W2f, st);
-    if (passes == -9) return readout_bf_din<32, 4, 6, 1, false, 2>(args, W1f, W2f, st);
+  // blocks, 1.18 ms with 32-unit W2 chunks, 1.39-1.41 ms with 4-wave blocks (512 x synth50, round 1)
+  if (din == 32)
     return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2>(args, W1f, W2f, st);
-  }
-  if (passes == -8) return readout_bf_din<64, 12, 6, 1>(args, W1f, W2f, st);
-  if (passes == -9) return readout_bf_din<64, 4, 6, 1, false, 2>(args, W1f, W2f, st);
   return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 8, 6, 1, false, 2>(args, W1f, W2f, st);
 }
 

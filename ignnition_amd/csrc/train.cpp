@@ -483,7 +483,7 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
       if (mp.sorted) {
         if ((rc = build_table(p, mp, mb, cp, srcs))) return rc;
         SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
-                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap, 0, mb.n_steps};
+                     p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         a.hs_save = mt.hs[it];
         if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
         HIP_TRY(launch_seq_gru(a, cp.H, std::max(2, p->seq_variant), st));

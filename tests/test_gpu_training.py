@@ -233,7 +233,7 @@ def test_fused_backward_is_deterministic_and_matches_unfused(monkeypatch):
     assert np.linalg.norm(g1.astype(np.float64) - g3) <= 1e-5 * np.linalg.norm(g3)
 
 
-@pytest.mark.parametrize("switch", ["IGN_TSGEMM_BF", "IGN_BWD_BF"])
+@pytest.mark.parametrize("switch", ["IGN_TSGEMM_BF", "IGN_BWD_BF", "IGN_TRAIN_DENSE_BF"])
 def test_split_bf16_backward_matches_f32(monkeypatch, switch):
     """The split-bf16 weight-gradient contractions (tsgemm_bf) and the split-bf16 gate recompute of
     the ordered backward (the forward's x6 path) against their f32-MFMA forms: bitwise
