@@ -16,7 +16,8 @@ Extra objects on the JSON line:
                 launch from the committed rocprofv3 PMC summary (profiles/), or null.
                 warmup_kernels: every kernel kind, timed during the warm-up.
   cpu_baseline  the dense-padded oracle (oracle/dense_forward.py, float32 numpy, the TF op
-                sequence incl. padded work) on a bounded sample of the same workload, rank 0, N=1.
+                sequence incl. padded work) on a bounded sample of the same workload, rank 0, N=1,
+                one process per CPU this process may use (CPU model and count on the line).
 """
 
 import argparse
@@ -46,6 +47,12 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="time the training step (forward keeping activations, MSE, backward, gradient "
                          "all-reduce over ranks, Adam) instead of the forward")
+    ap.add_argument("--fresh-batches", action="store_true",
+                    help="with --train: time the real train_and_evaluate loop (tar.gz reader -> normalisation -> "
+                         "batch build -> step, every step a new shuffled batch of the rank's dataset), with the "
+                         "next batches built on a worker thread")
+    ap.add_argument("--no-prefetch", action="store_true", help="with --fresh-batches: build each batch inline")
+    ap.add_argument("--input-workers", type=int, default=6, help="with --fresh-batches: batch-building threads")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -64,31 +71,71 @@ def load_traffic(kernel_kind, workload):
         return None
 
 
-def cpu_baseline(desc, dims, prm, graphs, budget_s, what="synth50 graphs"):
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_share():
+    """CPUs this process may use: its affinity set, capped by OMP_NUM_THREADS when the launcher
+    sets it (the GPU box grants 16 CPUs per GPU and sets it to 16; os.cpu_count() shows the whole
+    host there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else max(1, n)
+
+
+def _cpu_worker(job):
+    """One process of the CPU baseline: the dense oracle, one BLAS thread, graph after graph of
+    its share until the shared deadline."""
+    desc, dims, prm, graphs, t_end = job
     import numpy as np
     from threadpoolctl import threadpool_limits
 
     from ignnition_amd import workloads
     from ignnition_amd.json_operations import Model_information
     from oracle.dense_forward import DenseOracle
-
-    threads = max(1, min(16, os.cpu_count() or 1))
     ora = DenseOracle(desc, dims, prm, dtype=np.float32)
     mi = Model_information(desc, dims)
-    done, edges = 0, 0
-    with threadpool_limits(limits=threads):
-        ora.forward(graphs[:1])  # warm-up
-        t0 = time.perf_counter()
-        while done < len(graphs):
-            ora.forward([graphs[done]])
-            edges += workloads.edges_per_forward(mi, [graphs[done]])
+    done = edges = 0
+    per_graph = [workloads.edges_per_forward(mi, [g]) for g in graphs]
+    with threadpool_limits(limits=1):
+        while time.time() < t_end:     # cycles over its share until the deadline
+            k = done % len(graphs)
+            ora.forward([graphs[k]])
+            edges += per_graph[k]
             done += 1
-            if time.perf_counter() - t0 >= budget_s:
-                break
-        dt = time.perf_counter() - t0
-    return {"value": edges / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": "%d of the %d %s, full T=8 forward each, dense-padded numpy float32 oracle "
-                      "(TF op sequence incl. padded rows), %.1f s" % (done, len(graphs), what, dt)}
+    return done, edges
+
+
+def cpu_baseline(desc, dims, prm, graphs, budget_s, what="synth50 graphs"):
+    """The dense-padded numpy oracle (the TF op sequence incl. padded rows) on every CPU this
+    process may use, one process per CPU with one BLAS thread each, graphs dealt round-robin,
+    for ``budget_s`` seconds of wall time.  Forked before the process touches the GPU."""
+    import multiprocessing as mproc
+    n = _cpu_share()
+    graphs = list(graphs)
+    while len(graphs) < n:
+        graphs = graphs + graphs
+    _cpu_worker((desc, dims, prm, graphs[:1], time.time()))   # imports, before the clock starts
+    t0 = time.time()
+    jobs = [(desc, dims, prm, graphs[k::n], t0 + budget_s) for k in range(n)]
+    with mproc.get_context("fork").Pool(n) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    dt = time.time() - t0
+    done = sum(r[0] for r in res)
+    edges = sum(r[1] for r in res)
+    return {"value": edges / dt, "unit": "edges/s", "cores": n, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": "%d forwards of %s (full T=8 each; %d distinct) in %.1f s on %d processes x 1 BLAS "
+                      "thread, dense-padded numpy float32 oracle (TF op sequence incl. padded rows)"
+                      % (done, what, len(set(map(id, graphs))), dt, n)}
 
 
 def main():
@@ -121,6 +168,7 @@ def main():
             eng.synchronize()
 
     synthetic = args.model == "synthetic"
+    cleanup = []
     if synthetic:
         # one graph edge-cut across the ranks (strong scaling): every rank generates the same seeded
         # graph, keeps its node range and in-edges, and exchanges halo rows over RCCL (partition.py)
@@ -133,6 +181,15 @@ def main():
                                                                      first_id=ids[0])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(seed=0, bias_scale=0.05)
+    cpu = None
+    if world == 1 and not args.no_cpu and not args.train:
+        # before anything touches the GPU: the baseline's worker processes are forked
+        if synthetic:
+            # bounded sample: 25k-node graphs from the same generator (same degree law and locality)
+            sd, sdims, _, sg, _ = workloads.make_synthetic_inputs(n_nodes=25_000)
+            cpu = cpu_baseline(sd, sdims, prm, sg, args.cpu_seconds, "a 25k-node / 250k-edge synthetic graph")
+        else:
+            cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
     eng = Engine(plan, device if world > 1 else 0)
     eng.set_params(prm)
     t_build = time.perf_counter()
@@ -152,6 +209,36 @@ def main():
         edges = fw.edges_per_forward
         gru_steps = fw.batches[0].gru_steps_per_forward
         halo_rows = part.halos[plan.entities[0]].n_halo
+    elif args.train and args.fresh_batches:
+        # the real input pipeline: write the rank's graphs as a tar.gz dataset in the reference
+        # layout, then every step reads a new shuffled batch through the native reader
+        import tempfile
+
+        import torch
+        from ignnition_amd import generate_model as gm
+        from ignnition_amd import synthetic
+        from ignnition_amd.training import Trainer
+        torch.cuda.set_device(device if world > 1 else 0)
+        tmp = tempfile.mkdtemp(prefix="ign_bench_")
+        synthetic.write_tar_dataset(synthetic.dataset(args.topology, len(ids), first_id=ids[0]), os.path.join(tmp, "train"))
+        gm.register_user_functions(workloads.USER_FUNCTIONS)
+        gm.set_model_info(mi)
+        trainer = Trainer(mi, params=prm, device=device if world > 1 else 0, dist=dist)
+        eng = trainer.engine
+        probe = Batch(eng, graphs)
+        edges, gru_steps = probe.edges_per_forward, probe.gru_steps_per_forward
+        probe.close()
+        source = gm.NativeInput(os.path.join(tmp, "train"), shuffle=True, batch_size=len(ids), seed=1)
+        if args.no_prefetch:
+            batches = (trainer.prepare(*source.load(i)) for i in source.ids())
+        else:
+            batches = trainer.prefetch(source.ids(), depth=args.input_workers + 1, workers=args.input_workers,
+                                       load=source.load)
+
+        def step():   # train_and_evaluate's loop (FO:108-166): next batch from the pipeline, one step
+            trainer.train_prepared(*next(batches))
+        if not args.no_prefetch:
+            cleanup.append(batches.close)
     else:
         batch = Batch(eng, graphs)
         step = lambda: batch.forward(to_host=False)
@@ -194,6 +281,8 @@ def main():
     barrier_sync(eng)
     dt = time.perf_counter() - t0
     stats = eng.stats()
+    for fn in cleanup:
+        fn()
     dev = None
     if dist is not None and backend == "nccl":
         import torch
@@ -206,7 +295,9 @@ def main():
         dist.destroy_process_group()
         return
 
-    workload = "%s_%s_x%d%s" % (args.model, args.topology, args.graphs, "_train" if args.train else "")
+    workload = "%s_%s_x%d%s" % (args.model, args.topology, args.graphs,
+                                ("_train_fresh" + ("" if args.no_prefetch else "_prefetch")) if args.fresh_batches
+                                else "_train" if args.train else "")
     roof = None
     if not args.no_timing and not args.train and stats[dom]["ms"] > 0:
         s = stats[dom]
@@ -232,14 +323,6 @@ def main():
                                        "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2),
                                        "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
                                    for k, v in warm.items() if v["launches"]}}
-    cpu = None
-    if world == 1 and not args.no_cpu and not args.train:
-        if synthetic:
-            # bounded sample: a 25k-node graph from the same generator (same degree law and locality)
-            sd, sdims, _, sg, _ = workloads.make_synthetic_inputs(n_nodes=25_000)
-            cpu = cpu_baseline(sd, sdims, prm, sg * 16, args.cpu_seconds, "25k-node / 250k-edge synthetic graphs")
-        else:
-            cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
     seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "4"))
     ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "2"))
     sum_v = int(os.environ.get("IGN_SUM_VARIANT", "7"))
@@ -268,7 +351,8 @@ def main():
                    "parallelism": ("edge-cut over %d ranks, RCCL halo all-to-all per iteration (rank 0 halo rows: %d)"
                                    % (world, halo_rows)) if synthetic else
                                   "graph-sharded (%d ranks), no collective in the forward" % world,
-                   "batch_build_s": round(t_build, 3), "contraction": contraction},
+                   "batch_build_s": round(t_build, 3), "contraction": contraction,
+                   "samples_per_s": round(args.graphs * world * args.steps / dt, 1)},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

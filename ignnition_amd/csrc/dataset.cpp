@@ -398,19 +398,93 @@ Sample to_data(const JVal& s, const Spec& sp) {
 
 }  // namespace
 
-struct ign_dataset {
-  Spec spec;
-  std::vector<std::string> files;
-  std::vector<std::vector<Sample>> per_file;
-  std::vector<Sample*> samples;
-  std::vector<std::string> errors;
-  // the last gathered batch
+// One gathered batch with its own buffers: any number of them may exist and be filled at once
+// (one per input-pipeline worker thread); they only read the dataset's parsed samples.
+struct ign_dataset_batch {
+  const ign_dataset* ds = nullptr;
   std::vector<int64_t> ids;
   std::map<std::string, Arr> cat;
   std::map<std::string, std::vector<int64_t>> lens;
   Arr labels;
   std::vector<int64_t> label_lens;
 };
+
+struct ign_dataset {
+  Spec spec;
+  std::vector<std::string> files;
+  std::vector<std::vector<Sample>> per_file;
+  std::vector<Sample*> samples;
+  std::vector<std::string> errors;
+  ign_dataset_batch last;   // the batch of ign_dataset_gather / ign_dataset_get
+};
+
+namespace {
+
+int batch_gather(const ign_dataset* ds, ign_dataset_batch* b, const int64_t* ids, int32_t count) {
+  if (!ds || !b || (!ids && count)) return fail(IGN_ERR_INVALID, "null argument");
+  for (int32_t k = 0; k < count; ++k)
+    if (ids[k] < 0 || ids[k] >= (int64_t)ds->samples.size()) return fail(IGN_ERR_INVALID, "sample id %lld out of range", (long long)ids[k]);
+  b->ds = ds;
+  b->ids.assign(ids, ids + count);
+  b->cat.clear();
+  b->lens.clear();
+  b->labels = Arr();
+  b->label_lens.clear();
+  size_t n = 0;
+  for (int64_t id : b->ids) n += ds->samples[id]->label.size();
+  b->labels.f.reserve(n);
+  for (int64_t id : b->ids) {
+    const Sample& s = *ds->samples[id];
+    b->labels.f.insert(b->labels.f.end(), s.label.begin(), s.label.end());
+    b->label_lens.push_back((int64_t)s.label.size());
+  }
+  return IGN_OK;
+}
+
+int batch_get(ign_dataset_batch* b, const char* key, int32_t* dtype, const void** ptr, int64_t* total,
+              const int64_t** per_graph) {
+  if (!b || !b->ds || !key || !dtype || !ptr || !total || !per_graph) return fail(IGN_ERR_INVALID, "null argument");
+  std::string k(key);
+  if (k == "__label__") {
+    *dtype = 0;
+    *ptr = b->labels.f.data();
+    *total = (int64_t)b->labels.f.size();
+    *per_graph = b->label_lens.data();
+    return IGN_OK;
+  }
+  auto it = b->cat.find(k);
+  if (it == b->cat.end()) {
+    Arr c;
+    std::vector<int64_t> lens;
+    lens.reserve(b->ids.size());
+    size_t n = 0;
+    for (size_t q = 0; q < b->ids.size(); ++q) {
+      const int64_t id = b->ids[q];
+      const Arr* a = b->ds->samples[id]->get(k);
+      if (!a) return fail(IGN_ERR_INVALID, "sample %lld has no key '%s'", (long long)id, key);
+      if (q == 0) c.dtype = a->dtype;
+      if (a->dtype != c.dtype) return fail(IGN_ERR_INVALID, "key '%s' has mixed types", key);
+      n += a->dtype == 0 ? a->f.size() : a->i.size();
+    }
+    if (c.dtype == 0) c.f.reserve(n);
+    else c.i.reserve(n);
+    for (int64_t id : b->ids) {
+      const Arr* a = b->ds->samples[id]->get(k);
+      if (a->dtype == 0) c.f.insert(c.f.end(), a->f.begin(), a->f.end());
+      else c.i.insert(c.i.end(), a->i.begin(), a->i.end());
+      lens.push_back(a->dtype == 0 ? (int64_t)a->f.size() : (int64_t)a->i.size());
+    }
+    it = b->cat.emplace(k, std::move(c)).first;
+    b->lens[k] = std::move(lens);
+  }
+  *dtype = it->second.dtype;
+  *ptr = it->second.dtype == 0 ? (const void*)it->second.f.data() : (const void*)it->second.i.data();
+  *total = it->second.dtype == 0 ? (int64_t)it->second.f.size() : (int64_t)it->second.i.size();
+  *per_graph = b->lens[k].data();
+  return IGN_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -492,56 +566,31 @@ const char* ign_dataset_error(const ign_dataset* ds, int32_t i) {
 }
 
 int ign_dataset_gather(ign_dataset* ds, const int64_t* ids, int32_t count) {
-  if (!ds || (!ids && count)) return fail(IGN_ERR_INVALID, "null argument");
-  for (int32_t k = 0; k < count; ++k)
-    if (ids[k] < 0 || ids[k] >= (int64_t)ds->samples.size()) return fail(IGN_ERR_INVALID, "sample id %lld out of range", (long long)ids[k]);
-  ds->ids.assign(ids, ids + count);
-  ds->cat.clear();
-  ds->lens.clear();
-  ds->labels = Arr();
-  ds->label_lens.clear();
-  for (int64_t id : ds->ids) {
-    const Sample& s = *ds->samples[id];
-    ds->labels.f.insert(ds->labels.f.end(), s.label.begin(), s.label.end());
-    ds->label_lens.push_back((int64_t)s.label.size());
-  }
-  return IGN_OK;
+  if (!ds) return fail(IGN_ERR_INVALID, "null argument");
+  return batch_gather(ds, &ds->last, ids, count);
 }
 
 int ign_dataset_get(ign_dataset* ds, const char* key, int32_t* dtype, const void** ptr, int64_t* total,
                     const int64_t** per_graph) {
-  if (!ds || !key || !dtype || !ptr || !total || !per_graph) return fail(IGN_ERR_INVALID, "null argument");
-  std::string k(key);
-  if (k == "__label__") {
-    *dtype = 0;
-    *ptr = ds->labels.f.data();
-    *total = (int64_t)ds->labels.f.size();
-    *per_graph = ds->label_lens.data();
-    return IGN_OK;
-  }
-  auto it = ds->cat.find(k);
-  if (it == ds->cat.end()) {
-    Arr c;
-    std::vector<int64_t> lens;
-    bool first = true;
-    for (int64_t id : ds->ids) {
-      const Arr* a = ds->samples[id]->get(k);
-      if (!a) return fail(IGN_ERR_INVALID, "sample %lld has no key '%s'", (long long)id, key);
-      if (first) c.dtype = a->dtype;
-      first = false;
-      if (a->dtype != c.dtype) return fail(IGN_ERR_INVALID, "key '%s' has mixed types", key);
-      if (a->dtype == 0) c.f.insert(c.f.end(), a->f.begin(), a->f.end());
-      else c.i.insert(c.i.end(), a->i.begin(), a->i.end());
-      lens.push_back(a->dtype == 0 ? (int64_t)a->f.size() : (int64_t)a->i.size());
-    }
-    it = ds->cat.emplace(k, std::move(c)).first;
-    ds->lens[k] = std::move(lens);
-  }
-  *dtype = it->second.dtype;
-  *ptr = it->second.dtype == 0 ? (const void*)it->second.f.data() : (const void*)it->second.i.data();
-  *total = it->second.dtype == 0 ? (int64_t)it->second.f.size() : (int64_t)it->second.i.size();
-  *per_graph = ds->lens[k].data();
+  if (!ds) return fail(IGN_ERR_INVALID, "null argument");
+  return batch_get(&ds->last, key, dtype, ptr, total, per_graph);
+}
+
+int ign_dataset_batch_create(const ign_dataset* ds, const int64_t* ids, int32_t count, ign_dataset_batch** out) {
+  if (!out) return fail(IGN_ERR_INVALID, "null argument");
+  *out = nullptr;
+  std::unique_ptr<ign_dataset_batch> b(new ign_dataset_batch());
+  int rc = batch_gather(ds, b.get(), ids, count);
+  if (rc) return rc;
+  *out = b.release();
   return IGN_OK;
 }
+
+int ign_dataset_batch_get(ign_dataset_batch* b, const char* key, int32_t* dtype, const void** ptr, int64_t* total,
+                          const int64_t** per_graph) {
+  return batch_get(b, key, dtype, ptr, total, per_graph);
+}
+
+void ign_dataset_batch_destroy(ign_dataset_batch* b) { delete b; }
 
 }  // extern "C"

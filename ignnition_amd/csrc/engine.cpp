@@ -75,6 +75,12 @@ int ensure_device(ign_plan* p) {
   return IGN_OK;
 }
 
+hipStream_t upload_stream() {
+  thread_local hipStream_t s = nullptr;
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
+
 int dev_alloc(ign_batch* b, float** out, int64_t n) {
   void* p = nullptr;
   // +256 floats of slack: kernels may read a whole (masked-off) row at index 0 of an empty table
@@ -558,7 +564,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     const int64_t sr = (b->rows[e] + b->halo[e]) * H;
     for (int k = 0; k < 2; ++k) {
       if ((rc = dev_alloc(b.get(), &b->d_state[k][e], sr))) return rc;
-      if (b->halo[e]) HIP_TRY(hipMemset(b->d_state[k][e], 0, sr * sizeof(float)));   // halo defined before use
+      if (b->halo[e]) HIP_TRY(hipMemsetAsync(b->d_state[k][e], 0, sr * sizeof(float), upload_stream()));   // halo defined before use
     }
   }
 
@@ -705,7 +711,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if ((rc = dev_upload(b.get(), &mb.d_edge_params[s], prm))) return rc;
       }
       if ((rc = dev_alloc(b.get(), &mb.d_msg_in[s], ne * nn.din_pad))) return rc;
-      HIP_TRY(hipMemset(mb.d_msg_in[s], 0, ne * nn.din_pad * sizeof(float)));   // zero padding columns
+      HIP_TRY(hipMemsetAsync(mb.d_msg_in[s], 0, ne * nn.din_pad * sizeof(float), upload_stream()));   // zero padding columns
       for (auto& dp : nn.layers) {
         float* f = nullptr;
         if ((rc = dev_alloc(b.get(), &f, ne * dp.out))) return rc;
@@ -799,7 +805,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.h_multi_rows = std::move(multi_rows);
       const int64_t tfloats = (mb.zero_row + 1 + mb.n_multi) * 3LL * H;
       if ((rc = dev_alloc(b.get(), &mb.d_table, tfloats))) return rc;
-      HIP_TRY(hipMemset(mb.d_table, 0, (tfloats + 256) * sizeof(float)));   // zero row stays zero
+      HIP_TRY(hipMemsetAsync(mb.d_table, 0, (tfloats + 256) * sizeof(float), upload_stream()));   // zero row stays zero
       // per launch of the recurrence: h.U + gates per step; one projected row (3H floats) per step
       // FLOPs executed (fp32-equivalent): h.U + gates per step (x.W is hoisted into project);
       // bytes per SURVEY §8d, B_stage = E (4 + 4H) + 2 N_d 4H + 4 (N_d + 1): one message row and
@@ -967,6 +973,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     }
   }
   if ((rc = dev_alloc(b.get(), &b->d_pred, P * b->out_units))) return rc;
+  HIP_TRY(hipStreamSynchronize(upload_stream()));   // every clear has landed before the batch is used
   *out = b.release();
   return IGN_OK;
 }

@@ -263,6 +263,11 @@ int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d);
 int readout_ops_run(ign_plan* p, ign_batch* b, hipStream_t st, const float* const* ent = nullptr);
 const float* readout_tensor(const ign_plan* p, const ign_batch* b, int id);
 int64_t space_rows(const ign_plan* p, const ign_batch* b, const RoTensor& t);
+// Batch construction (ign_batch_create, ign_batch_enable_training) copies and clears on a
+// non-blocking stream of the calling host thread, never the legacy null stream: a batch built on a
+// worker thread does not wait for, or serialise with, the GPU step running on the engine's stream
+// (the training input pipeline overlaps them, ignnition_amd/training.py BatchPrefetcher).
+hipStream_t upload_stream();
 template <typename T>
 int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
   size_t n = std::max<size_t>(host.size(), 1);
@@ -270,8 +275,10 @@ int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
   hipError_t e = hipMalloc(&p, n * sizeof(T));
   if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
   b->allocs.push_back(p);
-  if (!host.empty()) HIP_TRY(hipMemcpy(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
-  else HIP_TRY(hipMemset(p, 0, sizeof(T)));
+  hipStream_t us = upload_stream();
+  if (!host.empty()) HIP_TRY(hipMemcpyAsync(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, us));
+  else HIP_TRY(hipMemsetAsync(p, 0, sizeof(T), us));
+  HIP_TRY(hipStreamSynchronize(us));   // the host vector may die after the call
   *out = static_cast<T*>(p);
   return IGN_OK;
 }

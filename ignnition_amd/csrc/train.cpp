@@ -109,7 +109,10 @@ int tupload(TrainState* t, T** out, const std::vector<T>& h) {
   hipError_t e = hipMalloc(&p, n * sizeof(T));
   if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: hipMalloc: %s", hipGetErrorString(e));
   t->allocs.push_back(p);
-  if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  if (!h.empty()) {
+    HIP_TRY(hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, upload_stream()));
+    HIP_TRY(hipStreamSynchronize(upload_stream()));
+  }
   *out = static_cast<T*>(p);
   return IGN_OK;
 }
@@ -358,8 +361,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       mz_n = std::max(mz_n, ne * widest);
       mdin_n = std::max(mdin_n, ne * nn.din);
       std::vector<int32_t> es(ne), ed(ne);
-      HIP_TRY(hipMemcpy(es.data(), mb.d_edge_src[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(ed.data(), mb.d_edge_dst[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpyAsync(es.data(), mb.d_edge_src[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost, upload_stream()));
+      HIP_TRY(hipMemcpyAsync(ed.data(), mb.d_edge_dst[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost, upload_stream()));
+      HIP_TRY(hipStreamSynchronize(upload_stream()));
       std::vector<std::pair<int64_t, int32_t>> ks(ne), kd(ne);
       for (int64_t e = 0; e < ne; ++e) {
         ks[e] = {es[e], (int32_t)e};

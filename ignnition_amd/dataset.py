@@ -82,11 +82,30 @@ class NativeDataset:
         return vals.astype(np_t, copy=False), glen
 
     def batch(self, ids, keys):
-        """BatchedGraphs holding ``keys`` for samples ``ids``, and the labels (or None)."""
-        self.gather(ids)
-        arrays = {k: self.get(k) for k in keys}
-        labels = self.get("__label__") if self.training else None
-        return BatchedGraphs(arrays, len(ids)), labels
+        """BatchedGraphs holding ``keys`` for samples ``ids``, and the labels (or None).  Thread
+        safe: the gather has buffers of its own (``ign_dataset_batch``), which the returned
+        arrays view without a copy and keep alive."""
+        ids = np.ascontiguousarray(np.asarray(ids, np.int64))
+        h = C.c_void_p()
+        check(lib.ign_dataset_batch_create(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), len(ids),
+                                           C.byref(h)))
+        owner = _GatherOwner(h)
+        G = len(ids)
+
+        def get(key):
+            dt, ptr, total, lens = C.c_int32(), C.c_void_p(), C.c_int64(), C.POINTER(C.c_int64)()
+            check(lib.ign_dataset_batch_get(owner.handle, key.encode(), C.byref(dt), C.byref(ptr), C.byref(total),
+                                            C.byref(lens)))
+            ctype = C.c_float if dt.value == 0 else C.c_int64
+            vals = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(max(total.value, 1),))[:total.value]
+            glen = np.ctypeslib.as_array(lens, shape=(max(G, 1),))[:G].copy()
+            return vals, glen
+
+        arrays = {k: get(k) for k in keys}
+        labels = get("__label__") if self.training else None
+        bg = BatchedGraphs(arrays, G)
+        bg._owner = owner          # the arrays view the gather's buffers
+        return bg, (None if labels is None else (labels[0].copy(), labels[1]))
 
     def close(self):
         h = getattr(self, "handle", None)
@@ -96,6 +115,18 @@ class NativeDataset:
 
     def __del__(self):
         self.close()
+
+
+class _GatherOwner:
+    """Frees an ``ign_dataset_batch`` when the last array viewing it is gone."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def __del__(self):
+        if self.handle:
+            lib.ign_dataset_batch_destroy(self.handle)
+            self.handle = None
 
 
 def plan_keys(plan) -> list:

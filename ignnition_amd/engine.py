@@ -389,9 +389,17 @@ class Engine:
             self.layout.append((name, shape, off.value))
 
     def set_params(self, params: dict):
+        """Every tensor of the layout, by its Keras-like name and with its exact shape (the
+        reference's Saver.restore also refuses a missing variable or a shape mismatch)."""
         flat = np.zeros(self.n_params, np.float32)
+        missing = [name for name, _, _ in self.layout if name not in params]
+        if missing:
+            raise ValueError("set_params: missing parameter tensor(s) %s" % ", ".join(missing))
         for name, shape, off in self.layout:
-            v = np.ascontiguousarray(params[name], dtype=np.float32).reshape(-1)
+            v = np.asarray(params[name], dtype=np.float32)
+            if v.size != int(np.prod(shape)) or (v.ndim > 1 and tuple(v.shape) != tuple(shape)):
+                raise ValueError("set_params: %s has shape %s, the model needs %s" % (name, tuple(v.shape), tuple(shape)))
+            v = np.ascontiguousarray(v).reshape(-1)
             flat[off:off + v.size] = v
         check(lib.ign_plan_set_params(self.handle, flat.ctypes.data_as(C.c_void_p), 0))
 
@@ -540,7 +548,7 @@ class Batch:
             v, lens = bg.get(key)
             il_len[:, i] = lens
             ils.append(_i64(v))
-        self._arrays = (num, feats, cnt, srcs, dsts, seqs, il_len, ils)
+        self._arrays = (num, feats, cnt, srcs, dsts, seqs, il_len, ils)   # (may view bg's buffers)
         fp = C.POINTER(C.c_float)
         lp = C.POINTER(C.c_int64)
         feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
@@ -579,6 +587,7 @@ class Batch:
         else:
             self.graph_predictions = cnt[:, space[1]].copy()
         self._arrays = None  # the engine copied what it needs
+        self._prm_arrays = None
         self._bound = {}
 
     # ---- stepped forward (edge-cut partitions) -----------------------------------

@@ -144,11 +144,27 @@ def debug(model_description, out_dir: str = "../debug_model/"):
     return dump
 
 
-def _shard(stream, rank: int, world: int):
-    """Data parallel: rank r keeps batches r, r + world, ... of the shared stream."""
-    for k, item in enumerate(stream):
-        if k % world == rank:
-            yield item
+WARM_START_VARS = ["kernel.*", "recurrent_kernel.*", "bias.*"]   # FO:127-129
+
+
+def warm_start(defaults: dict, checkpoint: dict, patterns=WARM_START_VARS) -> dict:
+    """tf.estimator.WarmStartSettings(vars_to_warm_start=["kernel.*", "recurrent_kernel.*",
+    "bias.*"]) (FO:126-131) over the model's freshly initialised ``defaults``: a tensor is taken
+    from the checkpoint when its variable name (the last component of the Keras-like name, e.g.
+    ``kernel1`` of ``attention/kernel1``) matches one of the regexes; every other tensor keeps
+    its initial value.  A checkpoint tensor of another shape raises, as TF's warm start does; a
+    checkpoint that lacks a matching tensor leaves it initialised."""
+    import re
+    out = dict(defaults)
+    for name, init in defaults.items():
+        if name not in checkpoint or not any(re.match(p, name.split("/")[-1]) for p in patterns):
+            continue
+        v = np.asarray(checkpoint[name], np.float32)
+        if v.shape != np.shape(init):
+            raise ValueError("warm start: %s has shape %s in the checkpoint, the model needs %s"
+                             % (name, v.shape, np.shape(init)))
+        out[name] = v
+    return out
 
 
 def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
@@ -169,8 +185,9 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
     - metrics appended to ``<model_dir>/metrics.jsonl``.
 
     ``execute_gpu`` is ignored: in the reference, ``True`` *hides* the GPU (FO:134-145); here
-    every step runs on the HIP engine. With ``dist`` (torch.distributed, initialised),
-    each rank takes every world-th batch and gradients are averaged by all-reduce."""
+    every step runs on the HIP engine. With ``dist`` (torch.distributed, initialised), each rank
+    trains on its slice of every global batch (disjoint samples, one shuffle seed broadcast from
+    rank 0) and gradients are averaged by all-reduce."""
     import time
 
     from .checkpoint import load_params, save_params
@@ -191,22 +208,30 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
     model_dir = os.path.join(paths["model_dir"], "experiment_" + str(datetime.datetime.now()).replace(" ", "_"))
     if rank == 0:
         os.makedirs(model_dir, exist_ok=True)
-    params = None
+    trainer = Trainer(model, device=device, dist=dist)
     if paths.get("warm_start_path", None):
-        warm = load_params(paths["warm_start_path"])
-        params = {k: v for k, v in warm.items()
-                  if k.endswith("kernel") or k.endswith("recurrent_kernel") or k.endswith("bias")}
-    trainer = Trainer(model, params=params, device=device, dist=dist)
-    if params is not None and set(params) != set(trainer.params()):
-        full = trainer.params()
-        full.update(params)
-        trainer.set_params(full)
+        trainer.set_params(warm_start(trainer.params(), load_params(paths["warm_start_path"])))
     native = str_to_bool(opts.get("native_reader", "True"))   # C++ reader
     make_input = gm.input_fn_native if native else gm.input_fn
-    train_stream = make_input(paths["train_dataset"], shuffle=str_to_bool(opts.get("shuffle_train_samples", "False")),
-                              batch_size=batch_size)
+    # data parallel: one shuffle seed for every rank (rank 0's), each rank reads its slice of
+    # every global batch of world * batch_size samples
+    seed = int(np.random.SeedSequence().entropy % (2 ** 31))
     if world > 1:
-        train_stream = _shard(train_stream, rank, world)
+        box = [seed]
+        dist.broadcast_object_list(box, src=0)
+        seed = int(box[0])
+    shuffle_train = str_to_bool(opts.get("shuffle_train_samples", "False"))
+    depth = int(opts.get("prefetch_batches", "4"))
+    workers = int(opts.get("input_workers", "4"))
+    if native:   # the gathers, normalisation and host CSR builds of `workers` batches run in parallel
+        source = gm.NativeInput(paths["train_dataset"], shuffle=shuffle_train, batch_size=batch_size, seed=seed,
+                                rank=rank, world=world)
+        prepared = trainer.prefetch(source.ids(), depth=depth, workers=workers, load=source.load)
+    else:
+        import random
+        random.seed(seed)   # the generator's random.shuffle (GEN) draws the same order on every rank
+        prepared = trainer.prefetch(gm.input_fn(paths["train_dataset"], shuffle=shuffle_train, batch_size=batch_size,
+                                                rank=rank, world=world), depth=depth)
 
     def eval_batches():
         it = make_input(paths["eval_dataset"], shuffle=str_to_bool(opts.get("shuffle_eval_samples", "False")),
@@ -236,14 +261,17 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
             log.warning("IGNNITION: eval at step %d: %s", step, metrics)
             last_eval = time.time()
 
-    for step in range(1, train_steps + 1):
-        features, labels = next(train_stream)
-        out = trainer.train_step(features, labels)
-        if rank == 0 and (step % log_every == 0 or step == 1):
-            log.warning("IGNNITION: step %d  Loss %.6g  Regularization loss %.6g  Total loss %.6g", step,
-                        out["loss"], out["regularization_loss"], out["total_loss"])
-        if time.time() - last_save >= save_secs:
-            checkpoint_and_eval(step)
+    # the next batches are read and built on worker threads while the GPU runs the current step
+    try:
+        for step in range(1, train_steps + 1):
+            out = trainer.train_prepared(*next(prepared))
+            if rank == 0 and (step % log_every == 0 or step == 1):
+                log.warning("IGNNITION: step %d  Loss %.6g  Regularization loss %.6g  Total loss %.6g", step,
+                            out["loss"], out["regularization_loss"], out["total_loss"])
+            if time.time() - last_save >= save_secs:
+                checkpoint_and_eval(step)
+    finally:
+        prepared.close()
     checkpoint_and_eval(train_steps, force=True)
     return {"model_dir": model_dir, "final_metrics": metrics, "history": history, "checkpoints": list(ckpts),
             "trainer": trainer}

@@ -68,8 +68,25 @@ def normalization(x, feature_list, output_name, output_normalization, y=None):
     return x
 
 
-def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True):
-    """GM:102-198: generator -> normalization -> repeat -> batches of ``batch_size`` graphs."""
+def _global_batches(stream, batch_size: int, rank: int, world: int):
+    """Batches of a sample stream for rank ``rank`` of ``world`` data-parallel ranks: the stream is
+    cut into global batches of ``world * batch_size`` consecutive samples and rank r keeps the r-th
+    ``batch_size`` of each, so the ranks of a step train on disjoint samples and every sample of an
+    epoch is used once.  Batches run across epoch boundaries, as the reference's
+    ``ds.repeat()`` followed by ``batching_func`` (GM:185-194) makes them."""
+    import itertools
+    while True:
+        chunk = list(itertools.islice(stream, world * batch_size))
+        mine = chunk[rank * batch_size:(rank + 1) * batch_size]
+        if not mine:
+            return
+        yield mine
+
+
+def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, rank=0, world=1):
+    """GM:102-198: generator -> normalization -> repeat -> batches of ``batch_size`` graphs.
+    ``rank`` / ``world``: data-parallel slice of every global batch (``_global_batches``); the
+    ranks must draw the same stream (seed ``random`` identically when ``shuffle``)."""
     mi = model_info
     feature_list = mi.get_all_features()
     adjacency_info = mi.get_adjecency_info()
@@ -93,62 +110,81 @@ def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True):
             if not repeat or n == 0:
                 return
 
-    it = stream()
-    while True:
-        batch = []
-        for _ in range(batch_size):
-            try:
-                batch.append(next(it))
-            except StopIteration:
-                break
-        if not batch:
-            return
+    for batch in _global_batches(stream(), batch_size, rank, world):
         if training:
             yield [b[0] for b in batch], [b[1] for b in batch]
         else:
             yield batch
 
 
-def input_fn_native(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, threads=16, seed=None):
-    """input_fn on the native reader (ignnition_amd.dataset): yields ``BatchedGraphs`` (and the
-    batch's label array when training).  Normalisation functions are applied by name to each
-    feature's graph-concatenated array and to the labels: the same values as the per-sample
-    call for elementwise functions (those of the examples)."""
-    from .dataset import NativeDataset, plan_keys
-    mi = model_info
-    ds = NativeDataset.for_model(data_dir, mi, training=training, threads=threads)
-    plan = MPPlan.from_model_info(mi)
-    keys = plan_keys(plan)
-    feature_list = mi.get_all_features()
-    output_name, output_normalization, _ = mi.get_output_info()
-    rng = np.random.default_rng(seed)
-    n = len(ds)
-    if n == 0:
-        return
-    while True:
-        order = rng.permutation(n) if shuffle else np.arange(n)
-        for b0 in range(0, n, batch_size):
-            ids = order[b0:b0 + batch_size]
-            bg, labels = ds.batch(ids, keys)
-            for f in feature_list:
-                if str(f.normalization) != "None" and f.name in bg:
-                    v, lens = bg.get(f.name)
-                    try:
-                        fn = _resolve(f.normalization)
-                    except KeyError:
-                        log.error("IGNNITION: The normalization function " + str(f.normalization) +
-                                  " is not defined in the main file.")
-                        sys.exit(1)
-                    bg.arrays[f.name] = (np.asarray(fn(v, f.name), np.float32), lens)
-            if training:
-                y = labels[0]
-                if str(output_normalization) != "None":
-                    y = np.asarray(_resolve(output_normalization)(y, output_name), np.float32)
-                yield bg, [y]
-            else:
-                yield bg
-        if not repeat:
+class NativeInput:
+    """input_fn on the native reader (ignnition_amd.dataset), in two halves so that an input
+    pipeline can run the second on worker threads:
+
+    * ``ids()``: the sample-id stream (one repeated stream, reshuffled every epoch with ``seed``,
+      the same on every data-parallel rank) cut into this rank's batches (``_global_batches``);
+    * ``load(ids)``: the native reader's gather (thread safe) and the normalisation functions,
+      applied by name to each feature's graph-concatenated array and to the labels (the same
+      values as the per-sample call for elementwise functions, those of the examples).  Returns
+      a ``BatchedGraphs`` with ``sample_ids``, and the batch's label array when training.
+
+    Iterating yields ``load(ids)`` for every batch of ``ids()``."""
+
+    def __init__(self, data_dir, shuffle=False, training=True, batch_size=1, repeat=True, threads=16, seed=None,
+                 rank=0, world=1):
+        from .dataset import NativeDataset, plan_keys
+        mi = model_info
+        self.ds = NativeDataset.for_model(data_dir, mi, training=training, threads=threads)
+        self.keys = plan_keys(MPPlan.from_model_info(mi))
+        self.feature_list = mi.get_all_features()
+        self.output_name, self.output_normalization, _ = mi.get_output_info()
+        self.shuffle, self.training, self.batch_size, self.repeat = shuffle, training, batch_size, repeat
+        self.rng = np.random.default_rng(seed)
+        self.rank, self.world = rank, world
+
+    def ids(self):
+        n = len(self.ds)
+        if n == 0:
             return
+
+        def id_stream():
+            while True:
+                yield from (self.rng.permutation(n) if self.shuffle else np.arange(n)).tolist()
+                if not self.repeat:
+                    return
+
+        yield from _global_batches(id_stream(), self.batch_size, self.rank, self.world)
+
+    def load(self, ids):
+        bg, labels = self.ds.batch(ids, self.keys)
+        bg.sample_ids = list(ids)
+        for f in self.feature_list:
+            if str(f.normalization) != "None" and f.name in bg:
+                v, lens = bg.get(f.name)
+                try:
+                    fn = _resolve(f.normalization)
+                except KeyError:
+                    log.error("IGNNITION: The normalization function " + str(f.normalization) +
+                              " is not defined in the main file.")
+                    sys.exit(1)
+                bg.arrays[f.name] = (np.asarray(fn(v, f.name), np.float32), lens)
+        if not self.training:
+            return bg
+        y = labels[0]
+        if str(self.output_normalization) != "None":
+            y = np.asarray(_resolve(self.output_normalization)(y, self.output_name), np.float32)
+        return bg, [y]
+
+    def __iter__(self):
+        for ids in self.ids():
+            yield self.load(ids)
+
+
+def input_fn_native(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, threads=16, seed=None,
+                    rank=0, world=1):
+    """input_fn on the native reader: an iterator over ``NativeInput(...)`` (BatchedGraphs, and
+    the label arrays when training)."""
+    return iter(NativeInput(data_dir, shuffle, training, batch_size, repeat, threads, seed, rank, world))
 
 
 def r_squared(labels, predictions):

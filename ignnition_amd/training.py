@@ -92,20 +92,46 @@ class Trainer:
         y = np.concatenate([np.asarray(l, np.float32).reshape(-1) for l in labels])
         return self.torch.from_numpy(y).to(self.device)
 
-    def train_step(self, features: list, labels: list) -> dict:
-        """One optimizer step on a batch of graphs (model_fn TRAIN, GM:712-830)."""
+    def prepare(self, features, labels):
+        """The host half of a step: the batch (CSR tables, H2D copies, the training tables) and the
+        device label vector.  Safe on a worker thread while the GPU runs another step (the engine
+        builds batches on a non-blocking stream of the calling thread; the labels use a torch
+        stream of their own)."""
         b = self.model.batch(features)
         try:
             b.enable_training()
+            y = np.concatenate([np.asarray(l, np.float32).reshape(-1) for l in labels])
+            if y.size != b.predictions * b.output_units:
+                raise ValueError("labels hold %d values for %d predictions" % (y.size, b.predictions * b.output_units))
+            torch = self.torch
+            with torch.cuda.device(self.device):
+                s = torch.cuda.Stream(self.device)
+                with torch.cuda.stream(s):
+                    yd = torch.from_numpy(y).pin_memory().to(self.device, non_blocking=True)
+                s.synchronize()
+        except BaseException:
+            b.close()
+            raise
+        return b, yd
+
+    def train_step(self, features: list, labels: list) -> dict:
+        """One optimizer step on a batch of graphs (model_fn TRAIN, GM:712-830)."""
+        return self.train_prepared(*self.prepare(features, labels))
+
+    def train_prepared(self, b, y) -> dict:
+        """One optimizer step on a batch made by ``prepare`` (closed here)."""
+        try:
             b.forward_train(to_host=False)
-            y = self._labels(labels)
-            if y.numel() != b.predictions * b.output_units:
-                raise ValueError("labels hold %d values for %d predictions" % (y.numel(), b.predictions * b.output_units))
             dpred = self.torch.empty_like(y)
             loss = self.engine.mse_loss(b.predictions_ptr(), y, dpred)
             b.backward(dpred, self.grads)
             if self.dist is not None and self.dist.is_initialized() and self.dist.get_world_size() > 1:
-                self.dist.all_reduce(self.grads)
+                if self.dist.get_backend() == "gloo":   # CPU collectives (tests, rehearsals): host-staged
+                    g = self.grads.cpu()
+                    self.dist.all_reduce(g)
+                    self.grads.copy_(g)
+                else:                                   # RCCL over xGMI
+                    self.dist.all_reduce(self.grads)
                 self.grads /= self.dist.get_world_size()
             lr = self.lr(self.iterations)
             self.engine.adam_step(self.grads, self.m, self.v, self.iterations, lr, self.beta1, self.beta2, self.epsilon)
@@ -152,5 +178,99 @@ class Trainer:
     def params(self) -> dict:
         return self.engine.get_params()
 
+    def prefetch(self, jobs, depth: int = 2, workers: int = 1, load=None) -> "BatchPrefetcher":
+        return BatchPrefetcher(self, jobs, depth, workers, load)
+
     def set_params(self, params: dict):
         self.model.set_params(params)
+
+
+class BatchPrefetcher:
+    """The training input pipeline overlapped with the GPU (the role of tf.data's
+    ``map(num_parallel_calls)`` + ``prefetch``, GM:181-192).  ``workers`` threads take the next
+    jobs of ``jobs`` (in order), turn each into (features, labels) with ``load`` (default: the job
+    is that pair; with the native reader, ``NativeInput.load`` of a batch of sample ids) and run
+    ``Trainer.prepare`` on it (the engine's host CSR build and copies, the training tables), while
+    the main thread's step runs on the GPU.  At most ``depth`` batches are built ahead.  Iterating
+    yields prepared (batch, labels) pairs in job order, for ``Trainer.train_prepared``; an
+    exception in a worker is raised in the consumer at its position."""
+
+    _END = object()
+
+    def __init__(self, trainer: Trainer, jobs, depth: int = 2, workers: int = 1, load=None):
+        import threading
+        self.trainer = trainer
+        self.jobs = iter(jobs)
+        self.load = load
+        self.lock = threading.Lock()          # the job iterator
+        self.cv = threading.Condition()       # results by sequence number
+        self.slots = threading.Semaphore(max(1, depth))
+        self.results = {}
+        self.issued = 0
+        self.end = None                       # sequence number of the end of the jobs
+        self.next_out = 0
+        self.stop = threading.Event()
+        self.threads = [threading.Thread(target=self._run, daemon=True) for _ in range(max(1, workers))]
+        for t in self.threads:
+            t.start()
+
+    def _run(self):
+        while True:
+            while not self.slots.acquire(timeout=0.1):
+                if self.stop.is_set():
+                    return
+            if self.stop.is_set():
+                return
+            with self.lock:
+                if self.end is not None:
+                    self.slots.release()
+                    return
+                k = self.issued
+                try:
+                    job = next(self.jobs)
+                except StopIteration:
+                    self.end = k
+                    with self.cv:
+                        self.cv.notify_all()
+                    self.slots.release()
+                    return
+                except BaseException as e:
+                    self.end = k + 1
+                    job = e
+                self.issued += 1
+            try:
+                if isinstance(job, BaseException):
+                    raise job
+                features, labels = self.load(job) if self.load is not None else job
+                res = self.trainer.prepare(features, labels)
+            except BaseException as e:   # handed to the consumer
+                res = e
+            with self.cv:
+                self.results[k] = res
+                self.cv.notify_all()
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        with self.cv:
+            while self.next_out not in self.results:
+                if self.end is not None and self.next_out >= self.end:
+                    raise StopIteration
+                self.cv.wait(0.1)
+            res = self.results.pop(self.next_out)
+            self.next_out += 1
+        self.slots.release()
+        if isinstance(res, BaseException):
+            raise res
+        return res
+
+    def close(self):
+        self.stop.set()
+        for t in self.threads:
+            t.join()
+        with self.cv:
+            for res in self.results.values():
+                if isinstance(res, tuple):
+                    res[0].close()
+            self.results.clear()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 6
+#define IGN_ABI_VERSION 7
 
 enum ign_status {
   IGN_OK = 0,
@@ -319,6 +319,14 @@ int  ign_dataset_gather(ign_dataset* ds, const int64_t* ids, int32_t count);
 /* dtype: 0 float32, 1 int64 */
 int  ign_dataset_get(ign_dataset* ds, const char* key, int32_t* dtype, const void** ptr, int64_t* total,
                      const int64_t** per_graph);
+/* The same gather as a batch object with its own buffers (pointers valid until it is destroyed):
+ * any number may exist, and threads may create and read them concurrently on one dataset (the
+ * training input pipeline builds several batches in parallel; tf.data's map/prefetch, GM:181-192). */
+typedef struct ign_dataset_batch ign_dataset_batch;
+int  ign_dataset_batch_create(const ign_dataset* ds, const int64_t* ids, int32_t count, ign_dataset_batch** out);
+int  ign_dataset_batch_get(ign_dataset_batch* batch, const char* key, int32_t* dtype, const void** ptr,
+                           int64_t* total, const int64_t** per_graph);
+void ign_dataset_batch_destroy(ign_dataset_batch* batch);
 
 #ifdef __cplusplus
 }

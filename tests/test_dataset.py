@@ -112,3 +112,64 @@ def test_native_reader_is_faster(tmp_path):
     t_native = time.perf_counter() - t0
     assert len(ds) == len(py)
     assert t_native < t_py
+
+
+def test_concurrent_batches_equal_serial(tmp_path):
+    """ign_dataset_batch objects are independent: batches gathered on 4 threads at once hold
+    exactly what one thread gathers (the training input pipeline's workers share one dataset)."""
+    from concurrent.futures import ThreadPoolExecutor
+    desc, dims, mi = workloads.model("qsize")
+    synthetic.write_tar_dataset(synthetic.dataset("nsfnet", 12, qsize=True), str(tmp_path), per_file=5)
+    ds = NativeDataset.for_model(str(tmp_path), mi)
+    keys = plan_keys(MPPlan.from_model_info(mi))
+    rng = np.random.default_rng(0)
+    id_sets = [rng.choice(12, size=5, replace=False) for _ in range(16)]
+
+    def one(ids):
+        bg, y = ds.batch(ids, keys)
+        return {k: (np.array(v), np.array(l)) for k, (v, l) in bg.arrays.items()}, y[0].copy()
+
+    serial = [one(ids) for ids in id_sets]
+    with ThreadPoolExecutor(4) as ex:
+        par = list(ex.map(one, id_sets))
+    for (a, ya), (b, yb) in zip(serial, par):
+        np.testing.assert_array_equal(ya, yb)
+        assert a.keys() == b.keys()
+        for k in a:
+            np.testing.assert_array_equal(a[k][0], b[k][0])
+            np.testing.assert_array_equal(a[k][1], b[k][1])
+    ds.close()
+
+
+class _FakeBatch:
+    def __init__(self, v):
+        self.v, self.closed = v, False
+
+    def close(self):
+        self.closed = True
+
+
+class _FakeTrainer:
+    """Trainer.prepare's contract for the prefetcher: (batch with close(), labels)."""
+
+    def prepare(self, features, labels):
+        import random
+        time.sleep(random.uniform(0, 0.01))
+        if features == "bad":
+            raise ValueError("bad batch")
+        return _FakeBatch(features), labels
+
+
+def test_prefetcher_keeps_job_order_and_raises_in_place():
+    from ignnition_amd.training import BatchPrefetcher
+    jobs = [(k, -k) for k in range(40)]
+    pf = BatchPrefetcher(_FakeTrainer(), jobs, depth=6, workers=4)
+    got = [(b.v, y) for b, y in pf]
+    assert got == jobs
+    pf.close()
+    pf = BatchPrefetcher(_FakeTrainer(), [(0, 0), ("bad", 1), (2, 2)], depth=3, workers=3,
+                         load=lambda job: job)
+    assert next(pf)[0].v == 0
+    with pytest.raises(ValueError, match="bad batch"):
+        next(pf)
+    pf.close()
