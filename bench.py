@@ -32,6 +32,7 @@ sys.path.insert(0, REPO)
 METRIC = "message-passing edges/sec, RouteNet synth50 batched, 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md), the split-bf16 kernels' pipe
 
 
 def parse():
@@ -295,6 +296,15 @@ def main():
         dist.destroy_process_group()
         return
 
+    def pipe(v):
+        if v["ms"] <= 0 or (v["mfma_bf16"] <= 0 and v["mfma_f32"] <= 0):
+            return None
+        bf = v["mfma_bf16"] >= v["mfma_f32"]
+        tf = (v["mfma_bf16"] if bf else v["mfma_f32"]) / (v["ms"] / 1e3) / 1e12
+        peak = PEAK_BF16_MFMA_TFLOPS if bf else PEAK_FP32_MFMA_TFLOPS
+        return {"dtype": "bf16" if bf else "f32", "achieved_tflops": round(tf, 2), "peak_tflops": peak,
+                "frac": round(tf / peak, 4)}
+
     workload = "%s_%s_x%d%s" % (args.model, args.topology, args.graphs,
                                 ("_train_fresh" + ("" if args.no_prefetch else "_prefetch")) if args.fresh_batches
                                 else "_train" if args.train else "")
@@ -319,9 +329,13 @@ def main():
                 "hbm_frac_alg": round(bytes_launch / avg_s / 1e9 / PEAK_HBM_GBS, 4),
                 "mfma_frac_alg": round(flops_launch / avg_s / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
                 "timed_launches": s["launches"],
+                # the matrix pipe the kernel actually runs on: FLOPs its MFMAs execute (bf16 piece
+                # products on the split-bf16 kernels) per launch time, against that pipe's dense peak
+                "mfma_pipe": pipe(s),
                 "warmup_kernels": {k: {"launches": v["launches"], "ms_total": round(v["ms"], 3),
                                        "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2),
-                                       "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                                       "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1),
+                                       "mfma_pipe": pipe(v)}
                                    for k, v in warm.items() if v["launches"]}}
     seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "4"))
     ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "2"))

@@ -77,7 +77,7 @@ class BatchInfo(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("kinds", i32), ("launches", i64 * 8), ("ms", C.c_double * 8), ("flops", C.c_double * 8),
-                ("bytes", C.c_double * 8)]
+                ("bytes", C.c_double * 8), ("mfma_bf16", C.c_double * 8), ("mfma_f32", C.c_double * 8)]
 
 
 KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "project", "other"]

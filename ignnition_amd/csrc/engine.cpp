@@ -63,14 +63,17 @@ int set_device(int dev) {
 int ensure_device(ign_plan* p) {
   int rc = set_device(p->device);
   if (rc) return rc;
-  if (!p->d_params) {
-    HIP_TRY(hipMalloc(&p->d_params, std::max<int64_t>(p->n_params, 1) * sizeof(float)));
-    HIP_TRY(hipMemset(p->d_params, 0, std::max<int64_t>(p->n_params, 1) * sizeof(float)));
-    HIP_TRY(hipMalloc(&p->d_packed, std::max<int64_t>(p->n_packed, 1) * sizeof(float)));
-  }
   if (!p->stream && !p->external_stream) {
     HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->own_stream = true;
+  }
+  if (!p->d_params) {
+    HIP_TRY(hipMalloc(&p->d_params, std::max<int64_t>(p->n_params, 1) * sizeof(float)));
+    HIP_TRY(hipMalloc(&p->d_packed, std::max<int64_t>(p->n_packed, 1) * sizeof(float)));
+    // on the plan stream and waited for: a null-stream memset is not ordered with the
+    // non-blocking plan stream and could land after ign_plan_set_params' copy
+    HIP_TRY(hipMemsetAsync(p->d_params, 0, std::max<int64_t>(p->n_params, 1) * sizeof(float), p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
   }
   return IGN_OK;
 }
@@ -95,9 +98,22 @@ int act_ok(int a) { return a >= IGN_ACT_LINEAR && a <= IGN_ACT_TANH; }
 
 // Destination processing order: one global stable sort by message count, descending (tiles of
 // equal length; the longest sequences start first).  Measured faster than per-graph orders with
-// XCD-aware tiles for both the ordered and the sum updates (profiles/r02/seq_experiments).
+// XCD-aware tiles for both the ordered and the sum updates (profiles/r02/seq_experiments).  A
+// counting sort (counts are small): O(n), the same order as std::stable_sort.
 void sort_order(std::vector<int32_t>& order, const std::vector<int64_t>& cnt) {
-  std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
+  const int64_t n = (int64_t)order.size();
+  int64_t mx = 0;
+  for (int32_t r : order) mx = std::max(mx, cnt[r]);
+  if (mx > (int64_t)16 * n + 4096) {
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
+    return;
+  }
+  std::vector<int64_t> start(mx + 2, 0);   // bucket c holds count mx - c (descending)
+  for (int32_t r : order) start[mx - cnt[r] + 1]++;
+  for (int64_t c = 0; c <= mx; ++c) start[c + 1] += start[c];
+  std::vector<int32_t> out(n);
+  for (int32_t r : order) out[start[mx - cnt[r]]++] = r;
+  order.swap(out);
 }
 
 // Per-launch algorithmic cost: one GRU application = 2*3H*(DIN+H) + 14H flops.
@@ -731,15 +747,6 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
           return fail(IGN_ERR_INVALID, "destination row %lld receives no message: the reference's sorted update"
                       " gathers position -1 (AUX:793-795)", (long long)r);
       sort_order(order, flen);
-      // bucket messages by destination (stable), keep those with pos < final_len, sort by pos
-      std::vector<int64_t> dcnt(ND + 1, 0);
-      for (size_t k = 0; k < mdst.size(); ++k) dcnt[mdst[k] + 1]++;
-      for (int64_t r = 0; r < ND; ++r) dcnt[r + 1] += dcnt[r];
-      std::vector<int64_t> byd(mdst.size());
-      {
-        std::vector<int64_t> fill(dcnt.begin(), dcnt.end() - 1);
-        for (size_t k = 0; k < mdst.size(); ++k) byd[fill[mdst[k]]++] = (int64_t)k;
-      }
       // combined projected table: source s occupies rows [src_off[s], src_off[s] + rows_s)
       int64_t trow = 0;
       for (int s = 0; s < S; ++s) {
@@ -753,42 +760,53 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       auto table_row = [&](uint32_t code) -> int64_t {
         return mb.src_off[code >> IGN_SLOT_SHIFT] + (code & IGN_ROW_MASK);
       };
+      // Step t of the destination at sorted position i is slot step_ptr[i] + t.  A slot holds its
+      // message's table row, the zero row (a hole), or a pre-summed "multi" row when several
+      // messages share the position (scatter_nd adds them); messages at positions >= final_len
+      // are dropped (the masked RNN never reads them).  Multi rows are numbered in slot order and
+      // list their messages in message order.  maxL + 8 trailing zero-row slots: the kernels read
+      // codes past a row's end unconditionally.
       std::vector<int32_t> len(ND), step_ptr(ND), multi_ptr(1, 0);
-      std::vector<uint32_t> scode, multi_rows;
-      scode.reserve(mdst.size() + 64);
-      int64_t steps = 0, maxL = 0, n_msgs = 0;
-      std::vector<int64_t> tmp;
+      std::vector<int32_t> where(ND);
+      int64_t steps = 0, maxL = 0;
       for (int64_t i = 0; i < ND; ++i) {
         const int64_t r = order[i];
-        const int64_t L = flen[r];
-        maxL = std::max(maxL, L);
-        len[i] = (int32_t)L;
+        where[r] = (int32_t)i;
+        len[i] = (int32_t)flen[r];
         step_ptr[i] = (int32_t)steps;
-        tmp.assign(byd.begin() + dcnt[r], byd.begin() + dcnt[r + 1]);
-        std::stable_sort(tmp.begin(), tmp.end(), [&](int64_t x, int64_t y) { return mpos[x] < mpos[y]; });
-        size_t q = 0;
-        for (int64_t t = 0; t < L; ++t) {
-          while (q < tmp.size() && mpos[tmp[q]] < t) ++q;
-          size_t q0 = q;
-          while (q < tmp.size() && mpos[tmp[q]] == t) ++q;
-          const size_t cnt = q - q0;
-          n_msgs += (int64_t)cnt;
-          if (cnt == 1) {
-            scode.push_back((uint32_t)table_row(mcode[tmp[q0]]));
-          } else if (cnt == 0) {
-            scode.push_back((uint32_t)mb.zero_row);        // hole: zero input
-          } else {                                            // several messages: pre-summed row
-            scode.push_back((uint32_t)(mb.zero_row + 1 + mb.n_multi));
-            for (size_t k = q0; k < q; ++k) multi_rows.push_back((uint32_t)table_row(mcode[tmp[k]]));
-            multi_ptr.push_back((int32_t)multi_rows.size());
-            mb.n_multi++;
-          }
-        }
-        steps += L;
+        maxL = std::max(maxL, flen[r]);
+        steps += flen[r];
       }
-      for (int64_t k = 0; k < maxL + 8; ++k) scode.push_back((uint32_t)mb.zero_row);  // unconditional reads
-      if (steps >= INT32_MAX || mb.zero_row + 1 + mb.n_multi >= (int64_t)UINT32_MAX)
-        return fail(IGN_ERR_UNSUPPORTED, "MP too large");
+      if (steps >= INT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
+      std::vector<uint32_t> scode((size_t)(steps + maxL + 8), (uint32_t)mb.zero_row);
+      std::vector<int32_t> slot_of(mdst.size(), -1), scount(steps, 0);
+      int64_t n_msgs = 0;
+      for (size_t k = 0; k < mdst.size(); ++k) {
+        const int64_t r = mdst[k];
+        if (mpos[k] >= flen[r]) continue;
+        const int64_t slot = step_ptr[where[r]] + mpos[k];
+        slot_of[k] = (int32_t)slot;
+        if (++scount[slot] == 1) scode[slot] = (uint32_t)table_row(mcode[k]);
+        ++n_msgs;
+      }
+      std::vector<uint32_t> multi_rows;
+      std::vector<int32_t> multi_of(steps, -1);
+      for (int64_t slot = 0; slot < steps; ++slot)
+        if (scount[slot] > 1) {
+          multi_of[slot] = (int32_t)mb.n_multi;
+          scode[slot] = (uint32_t)(mb.zero_row + 1 + mb.n_multi);
+          multi_ptr.push_back(multi_ptr.back() + scount[slot]);
+          mb.n_multi++;
+        }
+      if (mb.n_multi) {
+        multi_rows.resize(multi_ptr.back());
+        std::vector<int32_t> fill(multi_ptr.begin(), multi_ptr.end() - 1);
+        for (size_t k = 0; k < mdst.size(); ++k)
+          if (slot_of[k] >= 0 && multi_of[slot_of[k]] >= 0)
+            multi_rows[fill[multi_of[slot_of[k]]]++] = (uint32_t)table_row(mcode[k]);
+      }
+      for (int64_t i = 0; i < ND; i += 16) mb.wave_steps += len[i];   // sorted: a tile's first row is its longest
+      if (mb.zero_row + 1 + mb.n_multi >= (int64_t)UINT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
       mb.n_steps = steps;
       mb.n_msgs = n_msgs;
       if ((rc = dev_upload(b.get(), &mb.d_order, order))) return rc;
@@ -1014,7 +1032,7 @@ namespace {
 struct Timer {
   ign_plan* p;
   bool on = false;
-  void begin(int kind, double flops, double bytes) {
+  void begin(int kind, double flops, double bytes, double mfma_bf16 = 0, double mfma_f32 = 0) {
     on = p->timing && ((p->timing_kinds >> kind) & 1u);
     if (!on) return;
     const int slot = p->ev_slot;
@@ -1026,12 +1044,10 @@ struct Timer {
     }
     if ((int)p->ev_kind.size() <= slot) {
       p->ev_kind.resize(slot + 1);
-      p->ev_flops.resize(slot + 1);
-      p->ev_bytes.resize(slot + 1);
+      p->ev_cost.resize(slot + 1);
     }
     p->ev_kind[slot] = kind;
-    p->ev_flops[slot] = flops;
-    p->ev_bytes[slot] = bytes;
+    p->ev_cost[slot] = EvCost{flops, bytes, mfma_bf16, mfma_f32};
     hipEventRecord(p->ev[2 * slot], p->stream);
   }
   void end() {
@@ -1099,6 +1115,12 @@ int ign_forward_begin(ign_plan* p, ign_batch* b) {
   return IGN_OK;
 }
 
+// f32 MFMA FLOPs of a sum update's GRU step (sum_gru_kernel / sum_gru_lds: 3 gates x H/16 unit tiles x
+// (DIN + H)/4 k-steps per 16-row tile)
+static double sum_mfma_f32(int64_t n, int din, int H) {
+  return (double)((n + 15) / 16) * 3 * (H / 16) * ((din + H) / 4) * kMfmaF32Flops;
+}
+
 int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   int rc = check_pb(p, b);
   if (rc) return rc;
@@ -1131,7 +1153,9 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     const int W3 = 3 * cp.H;
     for (size_t s = 0; s < mp.src.size(); ++s) {
       const int64_t rs = mb.src_rows[s];
-      tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3));
+      const int sdin_t = mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : mp.din;
+      tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3), 0,
+               (double)((rs + 15) / 16) * 3 * (cp.H / 16) * (sdin_t / 4) * kMfmaF32Flops);
       const int sdin = mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : mp.din;
       const float* wp = mp.feature_concat ? p->d_packed + mp.pk_slice[s] : p->d_packed + cp.pk_w;
       HIP_TRY(launch_project(sbases.base[s], rs, wp, p->d_packed + cp.pk_b, mb.d_table + mb.src_off[s] * W3,
@@ -1147,7 +1171,14 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                  p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
     if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
-    tm.begin(K_SEQ, mb.flops, mb.bytes);
+    {   // MFMAs per wave step: split-bf16 (variants 4 / 5, H = 32 / 64) passes x 3 gates x H/16 x H/32;
+        // f32 (seq_gru2) 3 gates x H/16 x H/4
+      const bool bf = (p->seq_variant == 4 || p->seq_variant == 5) && (cp.H == 32 || cp.H == 64) && a.Ubf;
+      const double ws = (double)mb.wave_steps;
+      tm.begin(K_SEQ, mb.flops, mb.bytes,
+               bf ? ws * (p->seq_variant == 5 ? 9 : 6) * 3 * (cp.H / 16) * (cp.H / 32) * kMfmaBf16Flops : 0,
+               bf ? 0 : ws * 3 * (cp.H / 16) * (cp.H / 4) * kMfmaF32Flops);
+    }
     HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
     tm.end();
   } else {
@@ -1170,7 +1201,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       xb.base[0] = mb.d_xsum;
       SumGruArgs a{hin, hout, xb, mb.d_order, mb.d_id_ptr, mb.d_id_src, p->d_packed + cp.pk_w,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
-      tm.begin(K_SUM, mb.flops, mb.bytes);
+      tm.begin(K_SUM, mb.flops, mb.bytes, 0, sum_mfma_f32(mb.n_dst, mp.din, cp.H));
       HIP_TRY(launch_sum_win(wa, mp.din, st));
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
       tm.end();
@@ -1188,7 +1219,12 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
         a.conv_act = mp.act;
       }
       const double frac = mb.n_dst ? (double)count / mb.n_dst : 0.0;
-      tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac);
+      // split-bf16 GRU step (sum_gru_g32 / sum_gru_bf: x6 of x.W and h.U per 16-row tile) or f32
+      const bool bf = p->sum_variant == 7 && a.Wbf && a.Ubf && mp.din == cp.H && (cp.H == 32 || cp.H == 64);
+      const double tiles = (double)((count + 15) / 16);
+      tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac,
+               bf ? tiles * 6 * 3 * (cp.H / 16) * (mp.din / 32 + cp.H / 32) * kMfmaBf16Flops : 0,
+               bf ? 0 : sum_mfma_f32(count, mp.din, cp.H));
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
       tm.end();
     }
@@ -1199,7 +1235,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
 
 namespace {
 
-int accumulate_stats(ign_plan* p, int n, const int* kind, const double* flops, const double* bytes) {
+int accumulate_stats(ign_plan* p, int n, const int* kind, const EvCost* cost) {
   HIP_TRY(hipStreamSynchronize(p->stream));
   ign_stats_t& s = p->stats;
   s.kinds = K_KINDS;
@@ -1208,8 +1244,10 @@ int accumulate_stats(ign_plan* p, int n, const int* kind, const double* flops, c
     hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]);
     s.launches[kind[i]] += 1;
     s.ms[kind[i]] += ms;
-    s.flops[kind[i]] += flops[i];
-    s.bytes[kind[i]] += bytes[i];
+    s.flops[kind[i]] += cost[i].flops;
+    s.bytes[kind[i]] += cost[i].bytes;
+    s.mfma_bf16[kind[i]] += cost[i].mfma_bf16;
+    s.mfma_f32[kind[i]] += cost[i].mfma_f32;
   }
   return IGN_OK;
 }
@@ -1247,8 +1285,16 @@ int readout(ign_plan* p, ign_batch* b) {
                    l1.act, l2.act, l3.act, b->d_pred};
     if (!a.b1 || !a.b2) return fail(IGN_ERR_UNSUPPORTED, "fused readout requires use_bias on hidden layers");
     double flops = 2.0 * P * ((double)l1.in * l1.out + (double)l2.in * l2.out + l3.in);
-    tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0));
-    if (p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0)
+    const bool bf = p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0;
+    const double tiles = (double)((P + 15) / 16);
+    // per 16-row tile: layer 1 out/16 x in/32 and layer 2 out/16 x in/32 MFMAs of 16x16x32, x6 or x9
+    // products (readout_bf); f32 (readout3): out/16 x in/4 each of 16x16x4
+    const double k1 = (double)(l1.out / 16) * (l1.in / 32) + (double)(l2.out / 16) * (l2.in / 32);
+    const double k1f = (double)(l1.out / 16) * (l1.in / 4) + (double)(l2.out / 16) * (l2.in / 4);
+    tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0),
+             bf ? tiles * k1 * (p->readout_variant == 3 ? 9 : 6) * kMfmaBf16Flops : 0,
+             bf ? 0 : tiles * k1f * kMfmaF32Flops);
+    if (bf)
       HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
                                 p->readout_variant == 3 ? 9 : 6, st));
     else
@@ -1315,8 +1361,7 @@ int capture(ign_plan* p, ign_batch* b) {
   b->graph_timing = p->timing;
   const int n = p->timing ? p->ev_slot : 0;
   b->graph_kind.assign(p->ev_kind.begin(), p->ev_kind.begin() + n);
-  b->graph_flops.assign(p->ev_flops.begin(), p->ev_flops.begin() + n);
-  b->graph_bytes.assign(p->ev_bytes.begin(), p->ev_bytes.begin() + n);
+  b->graph_cost.assign(p->ev_cost.begin(), p->ev_cost.begin() + n);
   p->ev_slot = 0;
   return IGN_OK;
 }
@@ -1328,7 +1373,7 @@ int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
   if (rc) return rc;
   if ((rc = readout(p, b))) return rc;
   if ((rc = copy_out(p, b, pred_out))) return rc;
-  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_flops.data(), p->ev_bytes.data())))
+  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_cost.data())))
     return rc;
   p->ev_slot = 0;
   return IGN_OK;
@@ -1350,13 +1395,12 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
     HIP_TRY(hipGraphLaunch(b->graph, p->stream));
     if ((rc = copy_out(p, b, pred_out))) return rc;
     if (p->timing)
-      return accumulate_stats(p, (int)b->graph_kind.size(), b->graph_kind.data(), b->graph_flops.data(),
-                              b->graph_bytes.data());
+      return accumulate_stats(p, (int)b->graph_kind.size(), b->graph_kind.data(), b->graph_cost.data());
     return IGN_OK;
   }
   if ((rc = forward_body(p, b))) return rc;
   if ((rc = copy_out(p, b, pred_out))) return rc;
-  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_flops.data(), p->ev_bytes.data())))
+  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_cost.data())))
     return rc;
   p->ev_slot = 0;
   return IGN_OK;

@@ -26,6 +26,13 @@ int fail(int code, const char* fmt, ...);
 
 enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_PROJECT = 4, K_OTHER = 5, K_KINDS = 6 };
 
+// per timed launch: algorithmic FLOPs / bytes and the FLOPs its MFMAs execute (bf16 / f32 pipe)
+struct EvCost {
+  double flops = 0, bytes = 0, mfma_bf16 = 0, mfma_f32 = 0;
+};
+constexpr double kMfmaBf16Flops = 2.0 * 16 * 16 * 32;   // v_mfma_f32_16x16x32_bf16
+constexpr double kMfmaF32Flops = 2.0 * 16 * 16 * 4;     // v_mfma_f32_16x16x4_f32
+
 struct Tensor {
   int kind, owner;
   int64_t offset;
@@ -77,6 +84,7 @@ struct MPP {
 struct MPB {
   bool sorted = false;
   int64_t n_dst = 0, n_steps = 0, n_msgs = 0, edges = 0;
+  int64_t wave_steps = 0;          // sorted MPs: sum over 16-row tiles of the tile's longest sequence
   int32_t* d_order = nullptr;
   int32_t* d_len = nullptr;
   int32_t* d_step_ptr = nullptr;
@@ -206,7 +214,7 @@ struct ign_plan {
   uint32_t timing_kinds = ~0u;    // kernel kinds that get event pairs (ign_plan_set_timing_kinds)
   std::vector<hipEvent_t> ev;     // pairs
   std::vector<int> ev_kind;
-  std::vector<double> ev_flops, ev_bytes;
+  std::vector<EvCost> ev_cost;
   int ev_slot = 0;                // events recorded since ign_forward_begin
   double* d_red = nullptr;        // loss reductions (training)
   bool use_graph = true;          // replay ign_forward as one captured hipGraph; IGN_HIP_GRAPH=0 disables
@@ -238,7 +246,7 @@ struct ign_batch {
   hipGraphExec_t graph = nullptr;
   bool graph_timing = false;
   std::vector<int> graph_kind;
-  std::vector<double> graph_flops, graph_bytes;
+  std::vector<EvCost> graph_cost;
 };
 
 namespace ign {

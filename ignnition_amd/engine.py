@@ -413,7 +413,8 @@ class Engine:
     def stats(self) -> dict:
         s = _lib.Stats()
         check(lib.ign_stats(self.handle, C.byref(s)))
-        return {k: {"launches": s.launches[i], "ms": s.ms[i], "flops": s.flops[i], "bytes": s.bytes[i]}
+        return {k: {"launches": s.launches[i], "ms": s.ms[i], "flops": s.flops[i], "bytes": s.bytes[i],
+                    "mfma_bf16": s.mfma_bf16[i], "mfma_f32": s.mfma_f32[i]}
                 for i, k in enumerate(_lib.KERNEL_KINDS)}
 
     def synchronize(self):

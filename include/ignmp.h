@@ -201,6 +201,9 @@ typedef struct {
   double  ms[8];
   double  flops[8];                /* algorithmic FLOPs of those launches */
   double  bytes[8];                /* algorithmic HBM bytes of those launches */
+  double  mfma_bf16[8];            /* FLOPs the matrix pipe executed as bf16 MFMAs (the split-bf16
+                                      kernels' piece products; dense peak 2.5 PFLOP/s) */
+  double  mfma_f32[8];             /* FLOPs executed as f32 MFMAs (v_mfma_f32_16x16x4_f32) */
 } ign_stats_t;
 
 int  ign_abi_version(void);
