@@ -53,7 +53,7 @@ def parse():
                          "batch build -> step, every step a new shuffled batch of the rank's dataset), with the "
                          "next batches built on a worker thread")
     ap.add_argument("--no-prefetch", action="store_true", help="with --fresh-batches: build each batch inline")
-    ap.add_argument("--input-workers", type=int, default=6, help="with --fresh-batches: batch-building threads")
+    ap.add_argument("--input-workers", type=int, default=8, help="with --fresh-batches: batch-building threads")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")

@@ -1,0 +1,261 @@
+// Device-memory cache of one plan: the buffers of its batches and their training state.
+//
+// The training input pipeline (ignnition_amd/training.py BatchPrefetcher) builds the next batches
+// on worker threads while the GPU runs the current step.  Straight hipMalloc / hipFree there cost
+// more than the step itself: hipMalloc serialises across threads and hipFree waits for the device.
+// Batches of one workload have near-identical shapes, so their blocks are cached by size class and
+// handed to the next batch.  A returned block carries an event recorded on the plan stream when
+// its batch was destroyed; it is reused only once that event has completed, so no kernel still in
+// flight can see its memory change.  Size classes keep 3 significant bits (<= 12.5% slack).
+//
+// IGN_POOL=0 bypasses the cache (hipMalloc / hipFree per block).  IGN_POOL_POISON=1 fills every
+// scratch block it hands out with NaN (0xFF bytes): the parity tests under it show that no kernel
+// reads batch scratch it has not written (tests/test_gpu_parity.py).  IGN_POOL_CACHE_GB caps the
+// idle bytes kept (default 64).
+//
+// The host side has the same problem: the batch builders' index tables are ~10^8 bytes of host
+// memory per batch.  hvec (engine_internal.h) draws blocks >= 1 MiB from a process-wide cache
+// (IGN_HOST_CACHE_GB idle bytes kept, default 16) whose blocks keep their pages and are pinned,
+// so the uploads from them are direct DMA.
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "engine_internal.h"
+
+namespace ign {
+
+namespace {
+
+struct Fence {
+  hipEvent_t ev = nullptr;
+  bool done = false;
+  ~Fence() {
+    if (ev) hipEventDestroy(ev);
+  }
+  bool ready() {
+    if (!done && (!ev || hipEventQuery(ev) == hipSuccess)) done = true;
+    return done;
+  }
+};
+
+size_t size_class(size_t bytes) {
+  if (bytes <= 4096) return 4096;
+  int top = 63 - __builtin_clzll(bytes);        // 2^top <= bytes
+  size_t step = (size_t)1 << (top - 2);         // 4 classes per octave
+  return (bytes + step - 1) / step * step;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+}  // namespace
+
+struct DevPool {
+  struct Idle {
+    void* ptr;
+    std::shared_ptr<Fence> fence;
+  };
+  std::mutex mu;
+  std::map<size_t, std::vector<Idle>> idle;    // by size class, oldest first
+  std::unordered_map<void*, size_t> live;      // block -> size class
+  size_t idle_bytes = 0;
+  size_t cap = (size_t)64 << 30;
+  bool enabled = true, poison = false;
+  int device = 0;
+
+  // free idle blocks whose fence has completed, oldest classes' first, until idle_bytes <= target;
+  // with wait, also those still in flight (their fences are waited for)
+  void trim(size_t target, bool wait) {
+    for (auto it = idle.begin(); it != idle.end() && idle_bytes > target;) {
+      auto& v = it->second;
+      for (size_t i = 0; i < v.size() && idle_bytes > target;) {
+        if (wait && v[i].fence->ev) hipEventSynchronize(v[i].fence->ev);
+        if (v[i].fence->ready()) {
+          hipFree(v[i].ptr);
+          idle_bytes -= it->first;
+          v.erase(v.begin() + i);
+        } else {
+          ++i;
+        }
+      }
+      it = v.empty() ? idle.erase(it) : std::next(it);
+    }
+  }
+
+  ~DevPool() {
+    hipSetDevice(device);
+    trim(0, true);
+  }
+};
+
+std::shared_ptr<DevPool> pool_create(int device) {
+  auto pool = std::make_shared<DevPool>();
+  pool->device = device;
+  pool->enabled = env_int("IGN_POOL", 1) != 0;
+  pool->poison = env_int("IGN_POOL_POISON", 0) != 0;
+  pool->cap = (size_t)std::max(0, env_int("IGN_POOL_CACHE_GB", 64)) << 30;
+  return pool;
+}
+
+hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch) {
+  *out = nullptr;
+  if (!pool->enabled) {
+    hipError_t e = hipMalloc(out, bytes);
+    if (e == hipSuccess && scratch && pool->poison) e = hipMemsetAsync(*out, 0xFF, bytes, upload_stream());
+    return e;
+  }
+  const size_t cls = size_class(bytes);
+  {
+    std::lock_guard<std::mutex> g(pool->mu);
+    auto it = pool->idle.find(cls);
+    if (it != pool->idle.end()) {
+      auto& v = it->second;
+      for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].fence->ready()) {
+          *out = v[i].ptr;
+          v.erase(v.begin() + i);
+          if (v.empty()) pool->idle.erase(it);
+          pool->idle_bytes -= cls;
+          pool->live[*out] = cls;
+          break;
+        }
+    }
+  }
+  if (!*out) {
+    hipError_t e = hipMalloc(out, cls);
+    if (e == hipErrorOutOfMemory) {   // give back every idle block (waiting for in-flight ones), retry
+      (void)hipGetLastError();
+      {
+        std::lock_guard<std::mutex> g(pool->mu);
+        pool->trim(0, true);
+      }
+      e = hipMalloc(out, cls);
+    }
+    if (e != hipSuccess) {
+      *out = nullptr;
+      return e;
+    }
+    std::lock_guard<std::mutex> g(pool->mu);
+    pool->live[*out] = cls;
+  }
+  if (scratch && pool->poison) return hipMemsetAsync(*out, 0xFF, bytes, upload_stream());
+  return hipSuccess;
+}
+
+void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t after) {
+  if (blocks.empty()) return;
+  if (!pool->enabled) {
+    if (after) hipStreamSynchronize(after);
+    for (void* b : blocks) hipFree(b);
+    return;
+  }
+  auto fence = std::make_shared<Fence>();
+  if (hipEventCreateWithFlags(&fence->ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(fence->ev, after) != hipSuccess) {
+    if (fence->ev) hipEventDestroy(fence->ev);
+    fence->ev = nullptr;
+    if (after) hipStreamSynchronize(after);
+  }
+  std::lock_guard<std::mutex> g(pool->mu);
+  for (void* b : blocks) {
+    auto it = pool->live.find(b);
+    if (it == pool->live.end()) continue;   // not ours (cannot happen): leave it alone
+    const size_t cls = it->second;
+    pool->live.erase(it);
+    pool->idle[cls].push_back({b, fence});
+    pool->idle_bytes += cls;
+  }
+  if (pool->idle_bytes > pool->cap) pool->trim(pool->cap, false);
+}
+
+// ---- host blocks ----------------------------------------------------------------------------
+namespace {
+
+struct HostCache {
+  std::mutex mu;
+  std::map<size_t, std::vector<void*>> idle;   // by size class
+  std::unordered_map<void*, bool> pinned;      // every live or idle block -> registered for DMA
+  size_t idle_bytes = 0;
+  size_t cap = 0;
+  HostCache() { cap = (size_t)std::max(0, env_int("IGN_HOST_CACHE_GB", 16)) << 30; }
+  void unmap(void* p, size_t cls) {
+    auto it = pinned.find(p);
+    if (it != pinned.end()) {
+      if (it->second) hipHostUnregister(p);
+      pinned.erase(it);
+    }
+    munmap(p, cls);
+  }
+};
+
+HostCache& host_cache() {
+  static HostCache* c = new HostCache();   // never destroyed: blocks may be freed during exit
+  return *c;
+}
+
+size_t host_class(size_t bytes) {
+  const size_t two_mb = (size_t)2 << 20;
+  return std::max(size_class(bytes), (bytes + two_mb - 1) / two_mb * two_mb);
+}
+
+}  // namespace
+
+void* host_block_alloc(size_t bytes) {
+  HostCache& c = host_cache();
+  const size_t cls = host_class(bytes);
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.idle.find(cls);
+    if (it != c.idle.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      c.idle_bytes -= cls;
+      return p;
+    }
+  }
+  void* p = mmap(nullptr, cls, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  madvise(p, cls, MADV_HUGEPAGE);
+  // pinned: hipMemcpyAsync from it is a direct DMA instead of a staged copy (best effort: the
+  // block works as pageable memory when registration is refused)
+  const bool reg = hipHostRegister(p, cls, hipHostRegisterPortable) == hipSuccess;
+  if (!reg) (void)hipGetLastError();
+  std::lock_guard<std::mutex> g(c.mu);
+  c.pinned[p] = reg;
+  return p;
+}
+
+void host_block_free(void* p, size_t bytes) {
+  if (!p) return;
+  HostCache& c = host_cache();
+  const size_t cls = host_class(bytes);
+  std::lock_guard<std::mutex> g(c.mu);
+  c.idle[cls].push_back(p);
+  c.idle_bytes += cls;
+  // over the cap: unmap idle blocks, largest classes first
+  for (auto it = c.idle.rbegin(); c.idle_bytes > c.cap && it != c.idle.rend(); ++it)
+    while (c.idle_bytes > c.cap && !it->second.empty()) {
+      c.unmap(it->second.back(), it->first);
+      it->second.pop_back();
+      c.idle_bytes -= it->first;
+    }
+}
+
+void pool_stats(DevPool* pool, int64_t* live_bytes, int64_t* idle_bytes) {
+  std::lock_guard<std::mutex> g(pool->mu);
+  int64_t l = 0;
+  for (auto& kv : pool->live) l += (int64_t)kv.second;
+  if (live_bytes) *live_bytes = l;
+  if (idle_bytes) *idle_bytes = (int64_t)pool->idle_bytes;
+}
+
+}  // namespace ign

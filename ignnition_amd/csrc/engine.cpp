@@ -75,6 +75,7 @@ int ensure_device(ign_plan* p) {
     HIP_TRY(hipMemsetAsync(p->d_params, 0, std::max<int64_t>(p->n_params, 1) * sizeof(float), p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
   }
+  if (!p->pool) p->pool = pool_create(p->device);
   return IGN_OK;
 }
 
@@ -87,8 +88,8 @@ hipStream_t upload_stream() {
 int dev_alloc(ign_batch* b, float** out, int64_t n) {
   void* p = nullptr;
   // +256 floats of slack: kernels may read a whole (masked-off) row at index 0 of an empty table
-  hipError_t e = hipMalloc(&p, (std::max<int64_t>(n, 0) + 256) * sizeof(float));
-  if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%lld floats): %s", (long long)n, hipGetErrorString(e));
+  hipError_t e = pool_alloc(b->pool.get(), &p, (std::max<int64_t>(n, 0) + 256) * sizeof(float), true);
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "device alloc (%lld floats): %s", (long long)n, hipGetErrorString(e));
   b->allocs.push_back(p);
   *out = static_cast<float*>(p);
   return IGN_OK;
@@ -100,7 +101,7 @@ int act_ok(int a) { return a >= IGN_ACT_LINEAR && a <= IGN_ACT_TANH; }
 // equal length; the longest sequences start first).  Measured faster than per-graph orders with
 // XCD-aware tiles for both the ordered and the sum updates (profiles/r02/seq_experiments).  A
 // counting sort (counts are small): O(n), the same order as std::stable_sort.
-void sort_order(std::vector<int32_t>& order, const std::vector<int64_t>& cnt) {
+void sort_order(hvec<int32_t>& order, const hvec<int64_t>& cnt) {
   const int64_t n = (int64_t)order.size();
   int64_t mx = 0;
   for (int32_t r : order) mx = std::max(mx, cnt[r]);
@@ -108,10 +109,10 @@ void sort_order(std::vector<int32_t>& order, const std::vector<int64_t>& cnt) {
     std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
     return;
   }
-  std::vector<int64_t> start(mx + 2, 0);   // bucket c holds count mx - c (descending)
+  hvec<int64_t> start(mx + 2, 0);   // bucket c holds count mx - c (descending)
   for (int32_t r : order) start[mx - cnt[r] + 1]++;
   for (int64_t c = 0; c <= mx; ++c) start[c + 1] += start[c];
-  std::vector<int32_t> out(n);
+  hvec<int32_t> out(n);
   for (int32_t r : order) out[start[mx - cnt[r]]++] = r;
   order.swap(out);
 }
@@ -529,6 +530,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   if (rc) return rc;
   std::unique_ptr<ign_batch, void (*)(ign_batch*)> b(new ign_batch(), ign_batch_destroy);
   b->plan = p;
+  b->pool = p->pool;
   b->G = G;
   b->rows.assign(E, 0);
   b->row_off.assign(E, std::vector<int64_t>(G + 1, 0));
@@ -554,14 +556,14 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   for (int e = 0; e < E; ++e)
     if (b->rows[e] + b->halo[e] >= (int64_t)IGN_ROW_MASK) return fail(IGN_ERR_UNSUPPORTED, "entity %d: too many rows", e);
   // edge offsets per adjacency
-  std::vector<std::vector<int64_t>> eoff(p->n_adj, std::vector<int64_t>(G + 1, 0));
+  std::vector<hvec<int64_t>> eoff(p->n_adj, hvec<int64_t>(G + 1, 0));
   for (int a = 0; a < p->n_adj; ++a)
     for (int g = 0; g < G; ++g) {
       int64_t n = d->adj_edges[(int64_t)g * p->n_adj + a];
       if (n < 0) return fail(IGN_ERR_INVALID, "negative edge count");
       eoff[a][g + 1] = eoff[a][g] + n;
     }
-  std::vector<std::vector<int64_t>> ioff(p->n_il, std::vector<int64_t>(G + 1, 0));
+  std::vector<hvec<int64_t>> ioff(p->n_il, hvec<int64_t>(G + 1, 0));
   for (int i = 0; i < p->n_il; ++i)
     for (int g = 0; g < G; ++g) ioff[i][g + 1] = ioff[i][g] + d->interleave_len[(int64_t)g * p->n_il + i];
 
@@ -574,7 +576,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     const int H = p->ents[e].hidden_dim, F = p->ents[e].feature_total;
     if (F > 0) {
       if (!d->features || !d->features[e]) return fail(IGN_ERR_INVALID, "entity %d: features missing", e);
-      std::vector<float> f(d->features[e], d->features[e] + b->rows[e] * F);
+      hvec<float> f(d->features[e], d->features[e] + b->rows[e] * F);
       if ((rc = dev_upload(b.get(), &b->d_feat[e], f))) return rc;
     }
     const int64_t sr = (b->rows[e] + b->halo[e]) * H;
@@ -594,18 +596,18 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     mb.sorted = mp.sorted;
     mb.n_dst = ND;
     // messages: (dst row, position, code), in source order then edge order
-    std::vector<int64_t> mdst;
-    std::vector<int64_t> mpos;
-    std::vector<uint32_t> mcode;
+    hvec<int32_t> mdst;   // rows < IGN_ROW_MASK
+    hvec<int32_t> mpos;   // < total_slots (checked)
+    hvec<uint32_t> mcode;
     int64_t tot = 0;
     for (int s = 0; s < S; ++s) tot += eoff[mp.src[s].adjacency][G];
     mdst.reserve(tot);
     mpos.reserve(tot);
     mcode.reserve(tot);
-    std::vector<int64_t> flen(ND, 0);
+    hvec<int64_t> flen(ND, 0);
     for (int g = 0; g < G; ++g) {
       int64_t slot_off = 0;  // sum of Lmax of previous sources in this graph (GM:533)
-      std::vector<int64_t> ilflat;
+      hvec<int64_t> ilflat;
       if (mp.aggr == IGN_AGGR_INTERLEAVE) {
         // tf.stack([indices_a, indices_b]) then reshape [-1,1] (GM:518, AUX:433)
         int64_t len0 = -1;
@@ -620,7 +622,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         }
       }
       int64_t total_slots = 0;
-      std::vector<int64_t> lmax(S, 0);
+      hvec<int64_t> lmax(S, 0);
       for (int s = 0; s < S; ++s) {
         const int a = mp.src[s].adjacency;
         const int64_t e0 = eoff[a][g], e1 = eoff[a][g + 1];
@@ -636,6 +638,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         lmax[s] = mx + 1;
         total_slots += lmax[s];
       }
+      if (total_slots >= INT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "graph %d: sequences too long", g);
       if (mp.feature_concat) {   // tf.concat on axis 2 needs every source's [N, Lmax] to match
         for (int s = 1; s < S; ++s)
           if (lmax[s] != lmax[0])
@@ -653,7 +656,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         const int64_t nsrc = b->row_off[se][g + 1] - b->row_off[se][g] + b->halo[se];   // halo: G == 1
         const int64_t ndst = b->row_off[dst][g + 1] - b->row_off[dst][g];
         // attention: comb_seq of source s > 0 is seq + that source's own in-degree (GM:539-540)
-        std::vector<int64_t> lens_s;
+        hvec<int64_t> lens_s;
         if (mp.aggr == IGN_AGGR_ATTENTION && s > 0) {
           lens_s.assign(ndst, 0);
           for (int64_t k = e0; k < e1; ++k) {
@@ -712,7 +715,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       const int a = mp.src[s].adjacency, se = mp.src[s].entity;
       const int64_t ne = eoff[a][G];
       if (ne >= (int64_t)IGN_ROW_MASK) return fail(IGN_ERR_UNSUPPORTED, "too many edges for a message network");
-      std::vector<int32_t> es(ne), ed(ne);
+      hvec<int32_t> es(ne), ed(ne);
       for (int g = 0; g < G; ++g)
         for (int64_t k = eoff[a][g]; k < eoff[a][g + 1]; ++k) {
           es[k] = (int32_t)(b->row_off[se][g] + d->adj_src[a][k]);
@@ -723,7 +726,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       if (std::find(nn.inputs.begin(), nn.inputs.end(), (int)IGN_MSG_EDGE_PARAMS) != nn.inputs.end()) {
         if (!d->adj_params || !d->adj_params[a])
           return fail(IGN_ERR_INVALID, "message network of mp %zu reads edge_params but params_<adj> is missing", mi);
-        std::vector<float> prm(d->adj_params[a], d->adj_params[a] + ne * nn.param_dim);
+        hvec<float> prm(d->adj_params[a], d->adj_params[a] + ne * nn.param_dim);
         if ((rc = dev_upload(b.get(), &mb.d_edge_params[s], prm))) return rc;
       }
       if ((rc = dev_alloc(b.get(), &mb.d_msg_in[s], ne * nn.din_pad))) return rc;
@@ -739,7 +742,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     const CellP& cp = p->cells[mp.cell];
     const int H = cp.H, DIN = mp.din;
 
-    std::vector<int32_t> order(ND);
+    hvec<int32_t> order(ND);
     std::iota(order.begin(), order.end(), 0);
     if (mp.sorted) {
       for (int64_t r = 0; r < ND; ++r)
@@ -766,8 +769,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       // are dropped (the masked RNN never reads them).  Multi rows are numbered in slot order and
       // list their messages in message order.  maxL + 8 trailing zero-row slots: the kernels read
       // codes past a row's end unconditionally.
-      std::vector<int32_t> len(ND), step_ptr(ND), multi_ptr(1, 0);
-      std::vector<int32_t> where(ND);
+      hvec<int32_t> len(ND), step_ptr(ND), multi_ptr(1, 0);
+      hvec<int32_t> where(ND);
       int64_t steps = 0, maxL = 0;
       for (int64_t i = 0; i < ND; ++i) {
         const int64_t r = order[i];
@@ -778,8 +781,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         steps += flen[r];
       }
       if (steps >= INT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
-      std::vector<uint32_t> scode((size_t)(steps + maxL + 8), (uint32_t)mb.zero_row);
-      std::vector<int32_t> slot_of(mdst.size(), -1), scount(steps, 0);
+      hvec<uint32_t> scode((size_t)(steps + maxL + 8), (uint32_t)mb.zero_row);
+      hvec<int32_t> slot_of(mdst.size(), -1), scount(steps, 0);
       int64_t n_msgs = 0;
       for (size_t k = 0; k < mdst.size(); ++k) {
         const int64_t r = mdst[k];
@@ -789,8 +792,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if (++scount[slot] == 1) scode[slot] = (uint32_t)table_row(mcode[k]);
         ++n_msgs;
       }
-      std::vector<uint32_t> multi_rows;
-      std::vector<int32_t> multi_of(steps, -1);
+      hvec<uint32_t> multi_rows;
+      hvec<int32_t> multi_of(steps, -1);
       for (int64_t slot = 0; slot < steps; ++slot)
         if (scount[slot] > 1) {
           multi_of[slot] = (int32_t)mb.n_multi;
@@ -800,7 +803,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         }
       if (mb.n_multi) {
         multi_rows.resize(multi_ptr.back());
-        std::vector<int32_t> fill(multi_ptr.begin(), multi_ptr.end() - 1);
+        hvec<int32_t> fill(multi_ptr.begin(), multi_ptr.end() - 1);
         for (size_t k = 0; k < mdst.size(); ++k)
           if (slot_of[k] >= 0 && multi_of[slot_of[k]] >= 0)
             multi_rows[fill[multi_of[slot_of[k]]]++] = (uint32_t)table_row(mcode[k]);
@@ -834,7 +837,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     } else {
       sort_order(order, flen);
       // edge-cut partitions: destinations reading a halo row go last (they wait for the exchange)
-      std::vector<char> bnd(ND, 0);
+      hvec<char> bnd(ND, 0);
       for (size_t k = 0; k < mdst.size(); ++k) {
         const uint32_t c = mcode[k];
         const int se = mp.src[c >> IGN_SLOT_SHIFT].entity;
@@ -842,38 +845,39 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       }
       std::stable_partition(order.begin(), order.end(), [&](int32_t r) { return !bnd[r]; });
       mb.n_interior = std::count(bnd.begin(), bnd.end(), 0);
-      std::vector<int32_t> where(ND);
+      hvec<int32_t> where(ND);
       for (int64_t i = 0; i < ND; ++i) where[order[i]] = (int32_t)i;
-      std::vector<int32_t> ptr(ND + 1, 0);
+      hvec<int32_t> ptr(ND + 1, 0);
       for (size_t k = 0; k < mdst.size(); ++k) ptr[where[mdst[k]] + 1]++;
       for (int64_t i = 0; i < ND; ++i) ptr[i + 1] += ptr[i];
-      std::vector<uint32_t> msrc(mdst.size());
-      std::vector<int32_t> csr_pos(mdst.size());
+      hvec<uint32_t> msrc(mdst.size());
+      hvec<int32_t> csr_pos(mp.aggr == IGN_AGGR_ATTENTION ? mdst.size() : 0);   // message -> CSR slot
       {
-        std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
+        hvec<int32_t> fill(ptr.begin(), ptr.end() - 1);
         for (size_t k = 0; k < mdst.size(); ++k) {
-          csr_pos[k] = fill[where[mdst[k]]]++;
-          msrc[csr_pos[k]] = mcode[k];
+          const int32_t q = fill[where[mdst[k]]]++;
+          if (!csr_pos.empty()) csr_pos[k] = q;
+          msrc[q] = mcode[k];
         }
       }
       if (mp.aggr == IGN_AGGR_ATTENTION) {
         // dense (destination, position) cells of the scatter_nd (AUX:327-331); duplicates share one
         // cell.  Groups = (graph, position): the softmax runs over a graph's destinations (AUX:336)
-        std::vector<int> gof(ND);
+        hvec<int> gof(ND);
         for (int g = 0; g < G; ++g)
           for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r) gof[r] = g;
-        std::vector<int64_t> key(mdst.size());
-        std::vector<int64_t> gmax(G, 0);
-        for (size_t k = 0; k < mdst.size(); ++k) gmax[gof[mdst[k]]] = std::max(gmax[gof[mdst[k]]], mpos[k] + 1);
-        std::vector<int64_t> gbase(G + 1, 0);   // group index base per graph
+        hvec<int64_t> key(mdst.size());
+        hvec<int64_t> gmax(G, 0);
+        for (size_t k = 0; k < mdst.size(); ++k) gmax[gof[mdst[k]]] = std::max<int64_t>(gmax[gof[mdst[k]]], mpos[k] + 1);
+        hvec<int64_t> gbase(G + 1, 0);   // group index base per graph
         for (int g = 0; g < G; ++g) gbase[g + 1] = gbase[g] + gmax[g];
-        std::vector<size_t> ord(mdst.size());
+        hvec<size_t> ord(mdst.size());
         std::iota(ord.begin(), ord.end(), 0);
         std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) {
           const int64_t gx = gbase[gof[mdst[x]]] + mpos[x], gy = gbase[gof[mdst[y]]] + mpos[y];
           return gx != gy ? gx < gy : mdst[x] < mdst[y];
         });
-        std::vector<int32_t> group_ptr(gbase[G] + 1, 0), group_empty(gbase[G], 0), cell_dst, cell_ptr(1, 0), cell_msgs;
+        hvec<int32_t> group_ptr(gbase[G] + 1, 0), group_empty(gbase[G], 0), cell_dst, cell_ptr(1, 0), cell_msgs;
         for (size_t q = 0; q < ord.size();) {
           const size_t k = ord[q];
           const int64_t grp = gbase[gof[mdst[k]]] + mpos[k];
@@ -921,21 +925,21 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       if (window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
-        std::vector<int64_t> dstart(ND + 1, 0);
+        hvec<int64_t> dstart(ND + 1, 0);
         for (size_t k = 0; k < mdst.size(); ++k) dstart[mdst[k] + 1]++;
         for (int64_t r = 0; r < ND; ++r) dstart[r + 1] += dstart[r];
-        std::vector<int32_t> rows_by(mdst.size());
+        hvec<int32_t> rows_by(mdst.size());
         {
-          std::vector<int64_t> fill(dstart.begin(), dstart.end() - 1);
+          hvec<int64_t> fill(dstart.begin(), dstart.end() - 1);
           for (size_t k = 0; k < mdst.size(); ++k) rows_by[fill[mdst[k]]++] = (int32_t)(mcode[k] & IGN_ROW_MASK);
         }
         for (int64_t r = 0; r < ND; ++r) std::sort(rows_by.begin() + dstart[r], rows_by.begin() + dstart[r + 1]);
-        std::vector<int64_t> wg;
-        std::vector<int32_t> wdst, wptr(1, 0), wsrc;
+        hvec<int64_t> wg;
+        hvec<int32_t> wdst, wptr(1, 0), wsrc;
         wdst.reserve(ND);
         wsrc.reserve(mdst.size());
         for (int g = 0; g < G; ++g) {
-          std::vector<int32_t> ds;
+          hvec<int32_t> ds;
           for (int64_t r = b->row_off[dst][g]; r < b->row_off[dst][g + 1]; ++r) ds.push_back((int32_t)r);
           std::stable_sort(ds.begin(), ds.end(), [&](int32_t x, int32_t y) { return flen[x] > flen[y]; });
           for (size_t c0 = 0; c0 < ds.size(); c0 += 256) {
@@ -952,8 +956,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
             }
           }
         }
-        std::vector<int32_t> id_ptr(ND + 1);
-        std::vector<uint32_t> id_src(ND);
+        hvec<int32_t> id_ptr(ND + 1);
+        hvec<uint32_t> id_src(ND);
         for (int64_t i = 0; i <= ND; ++i) id_ptr[i] = (int32_t)i;
         for (int64_t i = 0; i < ND; ++i) id_src[i] = (uint32_t)order[i];   // slot 0: the x table
         mb.n_win_wg = (int64_t)wg.size() / 4;
@@ -1004,7 +1008,7 @@ void ign_batch_destroy(ign_batch* b) {
   }
   if (b->graph) hipGraphExecDestroy(b->graph);
   if (b->train) train_state_destroy(b->train);
-  for (void* a : b->allocs) hipFree(a);
+  if (b->pool) pool_release(b->pool.get(), b->allocs, b->plan ? b->plan->stream : nullptr);
   delete b;
 }
 

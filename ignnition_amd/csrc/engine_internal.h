@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdint>
+#include <memory>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -18,6 +21,48 @@ void train_state_destroy(TrainState* t);
 namespace ign {
 
 int fail(int code, const char* fmt, ...);
+
+// devpool.cpp: the plan's device-memory cache (batch and training buffers).  Blocks handed back by
+// pool_release are reused once an event recorded on `after` has completed.  scratch: a block the
+// caller does not fill on allocation (IGN_POOL_POISON=1 fills it with NaN, via the upload stream).
+struct DevPool;
+std::shared_ptr<DevPool> pool_create(int device);
+hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch);
+void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t after);
+void pool_stats(DevPool* pool, int64_t* live_bytes, int64_t* idle_bytes);
+
+// devpool.cpp: process-wide cache of large host blocks (>= kHostBlockMin bytes) for the batch
+// builders' index tables.  A batch touches ~10^8 bytes of fresh host memory; straight from malloc
+// that is mmap + page faults on every batch and munmap on destroy, serialised on the process's
+// address-space lock across the input workers.  Cached blocks keep their pages (transparent huge
+// pages where the kernel allows) and are pinned for DMA uploads where the runtime allows.
+constexpr size_t kHostBlockMin = (size_t)1 << 20;
+void* host_block_alloc(size_t bytes);
+void host_block_free(void* p, size_t bytes);
+template <class T>
+struct HostAlloc {
+  using value_type = T;
+  HostAlloc() = default;
+  template <class U>
+  HostAlloc(const HostAlloc<U>&) {}
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    void* p = bytes >= kHostBlockMin ? host_block_alloc(bytes) : std::malloc(std::max<size_t>(bytes, 1));
+    if (!p) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes >= kHostBlockMin) host_block_free(p, bytes);
+    else std::free(p);
+  }
+  template <class U>
+  bool operator==(const HostAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const HostAlloc<U>&) const { return false; }
+};
+template <class T>
+using hvec = std::vector<T, HostAlloc<T>>;
 #define HIP_TRY(expr)                                                                             \
   do {                                                                                            \
     hipError_t _e = (expr);                                                                       \
@@ -129,8 +174,8 @@ struct MPB {
   uint32_t* d_id_src = nullptr;
   double flops = 0, bytes = 0;    // algorithmic, per launch
   // host copies of the index tables (the training path builds their transposes)
-  std::vector<int32_t> h_order, h_len, h_step_ptr, h_msg_ptr, h_multi_ptr;
-  std::vector<uint32_t> h_step_code, h_msg_src, h_multi_rows;
+  hvec<int32_t> h_order, h_len, h_step_ptr, h_msg_ptr, h_multi_ptr;
+  hvec<uint32_t> h_step_code, h_msg_src, h_multi_rows;
 };
 
 // readout program (GM:611-655): tensors on row spaces, operations before predict
@@ -219,6 +264,7 @@ struct ign_plan {
   double* d_red = nullptr;        // loss reductions (training)
   bool use_graph = true;          // replay ign_forward as one captured hipGraph; IGN_HIP_GRAPH=0 disables
   ign_stats_t stats{};
+  std::shared_ptr<DevPool> pool;  // batch / training buffers (created with the stream, ensure_device)
 };
 
 struct ign_batch {
@@ -240,7 +286,8 @@ struct ign_batch {
   float* d_pred = nullptr;
   int64_t n_pred = 0, out_units = 1;
   int64_t edges_per_forward = 0, gru_steps = 0;
-  std::vector<void*> allocs;
+  std::vector<void*> allocs;                    // blocks of pool (returned on destroy)
+  std::shared_ptr<DevPool> pool;                // the plan's (outlives the plan if need be)
   TrainState* train = nullptr;                  // ign_batch_enable_training
   // captured ign_forward (init .. readout) for replay; the event slots it records
   hipGraphExec_t graph = nullptr;
@@ -276,12 +323,12 @@ int64_t space_rows(const ign_plan* p, const ign_batch* b, const RoTensor& t);
 // worker thread does not wait for, or serialise with, the GPU step running on the engine's stream
 // (the training input pipeline overlaps them, ignnition_amd/training.py BatchPrefetcher).
 hipStream_t upload_stream();
-template <typename T>
-int dev_upload(ign_batch* b, T** out, const std::vector<T>& host) {
+template <typename T, typename A>
+int dev_upload(ign_batch* b, T** out, const std::vector<T, A>& host) {
   size_t n = std::max<size_t>(host.size(), 1);
   void* p = nullptr;
-  hipError_t e = hipMalloc(&p, n * sizeof(T));
-  if (e != hipSuccess) return fail(IGN_ERR_OOM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+  hipError_t e = pool_alloc(b->pool.get(), &p, n * sizeof(T), false);
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "device alloc (%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
   b->allocs.push_back(p);
   hipStream_t us = upload_stream();
   if (!host.empty()) HIP_TRY(hipMemcpyAsync(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, us));

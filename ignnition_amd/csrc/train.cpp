@@ -36,7 +36,7 @@ struct MPTrain {
   std::vector<int32_t*> asptr, asidx;   // attention MPs, per slot: source row -> CSR messages
   int64_t hs_rows = 0;
   std::vector<int32_t*> tptr, tidx;   // per source slot: source row -> steps (sorted) / dst rows (sum)
-  std::vector<int64_t> trows;         // (a source with a message network: its rows are the edges)
+  hvec<int64_t> trows;         // (a source with a message network: its rows are the edges)
   // message networks, per source slot: state row -> its edges (ascending), for the hs_source /
   // hs_dest columns of the network's input gradient
   int32_t* nsrc_ptr[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
@@ -52,7 +52,7 @@ struct MPRec {
 
 struct TrainState {
   std::vector<std::vector<float*>> ver;   // [entity][version] hidden states
-  std::vector<int> cur;                   // current version per entity (after the forward)
+  hvec<int> cur;                   // current version per entity (after the forward)
   std::vector<MPTrain> mp;
   std::vector<MPRec> recs;
   float* ga = nullptr;
@@ -81,12 +81,14 @@ struct TrainState {
   float* rties = nullptr;
   std::vector<int32_t*> rx_ptr, rx_idx;   // extend ops: per op 2 transposed CSRs (input row -> edges)
   bool forward_done = false;
-  std::vector<void*> allocs;
+  std::vector<void*> allocs;               // blocks of pool
+  DevPool* pool = nullptr;                 // the batch's (outlives this state)
+  hipStream_t stream = nullptr;            // the plan stream, for the release fence
 };
 
 void train_state_destroy(TrainState* t) {
   if (!t) return;
-  for (void* a : t->allocs) hipFree(a);
+  if (t->pool) pool_release(t->pool, t->allocs, t->stream);
   delete t;
 }
 
@@ -94,20 +96,20 @@ namespace {
 
 int talloc(TrainState* t, float** out, int64_t n) {
   void* p = nullptr;
-  hipError_t e = hipMalloc(&p, (std::max<int64_t>(n, 0) + 256) * sizeof(float));
-  if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: hipMalloc(%lld floats): %s", (long long)n,
+  hipError_t e = pool_alloc(t->pool, &p, (std::max<int64_t>(n, 0) + 256) * sizeof(float), true);
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: device alloc (%lld floats): %s", (long long)n,
                                    hipGetErrorString(e));
   t->allocs.push_back(p);
   *out = static_cast<float*>(p);
   return IGN_OK;
 }
 
-template <typename T>
-int tupload(TrainState* t, T** out, const std::vector<T>& h) {
+template <typename T, typename A>
+int tupload(TrainState* t, T** out, const std::vector<T, A>& h) {
   void* p = nullptr;
   size_t n = std::max<size_t>(h.size(), 1);
-  hipError_t e = hipMalloc(&p, n * sizeof(T));
-  if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: hipMalloc: %s", hipGetErrorString(e));
+  hipError_t e = pool_alloc(t->pool, &p, n * sizeof(T), h.empty());
+  if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: device alloc: %s", hipGetErrorString(e));
   t->allocs.push_back(p);
   if (!h.empty()) {
     HIP_TRY(hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, upload_stream()));
@@ -118,14 +120,32 @@ int tupload(TrainState* t, T** out, const std::vector<T>& h) {
 }
 
 // CSR of (key, value) pairs over n_keys keys, values kept in insertion order per key
-void build_csr(int64_t n_keys, const std::vector<std::pair<int64_t, int32_t>>& kv, std::vector<int32_t>& ptr,
-               std::vector<int32_t>& idx) {
+void build_csr(int64_t n_keys, const hvec<std::pair<int64_t, int32_t>>& kv, hvec<int32_t>& ptr,
+               hvec<int32_t>& idx) {
   ptr.assign(n_keys + 1, 0);
   for (auto& p : kv) ptr[p.first + 1]++;
   for (int64_t k = 0; k < n_keys; ++k) ptr[k + 1] += ptr[k];
   idx.resize(kv.size());
-  std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
+  hvec<int32_t> fill(ptr.begin(), ptr.end() - 1);
   for (auto& p : kv) idx[fill[p.first]++] = p.second;
+}
+
+// Per source slot s, the CSR of the (row, value) pairs visit() emits, values in emission order
+// per row: one counting pass and one filling pass over the same visit, no pair list.
+template <class Visit>
+void build_csrs(int S, const int64_t* n_keys, Visit visit, std::vector<hvec<int32_t>>& ptr,
+                std::vector<hvec<int32_t>>& idx) {
+  ptr.assign(S, hvec<int32_t>());
+  idx.assign(S, hvec<int32_t>());
+  for (int s = 0; s < S; ++s) ptr[s].assign(n_keys[s] + 1, 0);
+  visit([&](int s, int64_t key, int32_t) { ptr[s][key + 1]++; });
+  std::vector<hvec<int32_t>> fill(S);
+  for (int s = 0; s < S; ++s) {
+    for (int64_t k = 0; k < n_keys[s]; ++k) ptr[s][k + 1] += ptr[s][k];
+    idx[s].resize(ptr[s][n_keys[s]]);
+    fill[s].assign(ptr[s].begin(), ptr[s].end() - 1);
+  }
+  visit([&](int s, int64_t key, int32_t v) { idx[s][fill[s][key]++] = v; });
 }
 
 int check_train(ign_plan* p, ign_batch* b) {
@@ -221,9 +241,11 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       return fail(IGN_ERR_UNSUPPORTED, "no backward kernel for GRU shape (input %d, units %d)", cp.din, cp.H);
   }
   std::unique_ptr<TrainState, void (*)(TrainState*)> t(new TrainState(), train_state_destroy);
+  t->pool = b->pool.get();
+  t->stream = p->stream;
   const int64_t P = b->n_pred;
   // hidden-state versions: 1 + T x (MPs updating the entity)
-  std::vector<int> nver(E, 1);
+  hvec<int> nver(E, 1);
   for (auto& mp : p->mps) nver[mp.dst] += p->T;
   t->ver.resize(E);
   t->cur.assign(E, 0);
@@ -251,7 +273,11 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     const CellP& cp = p->cells[mp.cell];
     const int H = cp.H, DIN = mp.din, S = (int)mp.src.size();
     MPTrain mt;
-    std::vector<std::vector<std::pair<int64_t, int32_t>>> kv(S);
+    // transposed CSRs (source row -> steps / destinations reading it), built below
+    std::vector<hvec<int32_t>> tptr, tidx;
+    int64_t tkeys[IGN_MAX_SLOTS] = {0, 0, 0, 0};
+    for (int s = 0; s < S; ++s)
+      tkeys[s] = mp.nn[s].layers.empty() ? b->rows[mp.src[s].entity] : mb.n_edges[s];
     if (mb.sorted) {
       mt.hs_rows = mb.n_steps + mb.n_dst;
       for (int it = 0; it < p->T; ++it) {
@@ -260,24 +286,26 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         mt.hs.push_back(f);
       }
       // source row -> steps whose input contains it (directly or through a pre-summed row)
-      auto add_row = [&](uint32_t trow, int32_t step) {
-        for (int s = S - 1; s >= 0; --s)
-          if ((int64_t)trow >= mb.src_off[s]) {
-            kv[s].push_back({(int64_t)trow - mb.src_off[s], step});
-            return;
+      build_csrs(S, tkeys, [&](auto&& emit) {
+        auto add_row = [&](uint32_t trow, int32_t step) {
+          for (int s = S - 1; s >= 0; --s)
+            if ((int64_t)trow >= mb.src_off[s]) {
+              emit(s, (int64_t)trow - mb.src_off[s], step);
+              return;
+            }
+        };
+        for (int64_t pos = 0; pos < mb.n_dst; ++pos)
+          for (int32_t tt = 0; tt < mb.h_len[pos]; ++tt) {
+            const int32_t i = mb.h_step_ptr[pos] + tt;
+            const uint32_t code = mb.h_step_code[i];
+            if ((int64_t)code < mb.zero_row) {
+              add_row(code, i);
+            } else if ((int64_t)code > mb.zero_row) {
+              const int64_t k = code - mb.zero_row - 1;
+              for (int32_t m = mb.h_multi_ptr[k]; m < mb.h_multi_ptr[k + 1]; ++m) add_row(mb.h_multi_rows[m], i);
+            }
           }
-      };
-      for (int64_t pos = 0; pos < mb.n_dst; ++pos)
-        for (int32_t tt = 0; tt < mb.h_len[pos]; ++tt) {
-          const int32_t i = mb.h_step_ptr[pos] + tt;
-          const uint32_t code = mb.h_step_code[i];
-          if ((int64_t)code < mb.zero_row) {
-            add_row(code, i);
-          } else if ((int64_t)code > mb.zero_row) {
-            const int64_t k = code - mb.zero_row - 1;
-            for (int32_t m = mb.h_multi_ptr[k]; m < mb.h_multi_ptr[k + 1]; ++m) add_row(mb.h_multi_rows[m], i);
-          }
-        }
+      }, tptr, tidx);
       ga_n = std::max(ga_n, mb.n_steps * 3 * H);
       gu_n = std::max(gu_n, mt.hs_rows * 3 * H);
       need_part(mt.hs_rows, H, 3 * H);
@@ -297,16 +325,16 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         }
       }
       if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343: message -> destination row, row -> messages
-        std::vector<int32_t> mdst(mb.n_msgs);
+        hvec<int32_t> mdst(mb.n_msgs);
         for (int64_t pos = 0; pos < mb.n_dst; ++pos)
           for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) mdst[m] = mb.h_order[pos];
         if ((rc = tupload(t.get(), &mt.amdst, mdst))) return rc;
-        std::vector<std::vector<std::pair<int64_t, int32_t>>> am(S);
+        std::vector<hvec<std::pair<int64_t, int32_t>>> am(S);
         for (int64_t m = 0; m < mb.n_msgs; ++m)
           am[mb.h_msg_src[m] >> IGN_SLOT_SHIFT].push_back({(int64_t)(mb.h_msg_src[m] & IGN_ROW_MASK), (int32_t)m});
         for (int s = 0; s < S; ++s) {
           const int64_t rows_s = b->rows[mp.src[s].entity];
-          std::vector<int32_t> ptr, idx;
+          hvec<int32_t> ptr, idx;
           build_csr(rows_s, am[s], ptr, idx);
           int32_t *dp = nullptr, *di = nullptr;
           if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
@@ -320,18 +348,20 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         need_part(mb.n_dst, H, 1);
       }
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
-        std::vector<float> deg(mb.n_dst, 0.f);
+        hvec<float> deg(mb.n_dst, 0.f);
         for (int64_t pos = 0; pos < mb.n_dst; ++pos)
           deg[mb.h_order[pos]] = (float)(mb.h_msg_ptr[pos + 1] - mb.h_msg_ptr[pos]);
         if ((rc = tupload(t.get(), &mt.deg, deg))) return rc;
         dtab_n = std::max(dtab_n, 2 * mb.n_dst * DIN);   // du and d(sum) of the convolution
         need_part(mb.n_dst, DIN, DIN);
       }
-      for (int64_t pos = 0; pos < mb.n_dst; ++pos)
-        for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) {
-          const uint32_t code = mb.h_msg_src[m];
-          kv[code >> IGN_SLOT_SHIFT].push_back({(int64_t)(code & IGN_ROW_MASK), mb.h_order[pos]});
-        }
+      build_csrs(S, tkeys, [&](auto&& emit) {
+        for (int64_t pos = 0; pos < mb.n_dst; ++pos)
+          for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) {
+            const uint32_t code = mb.h_msg_src[m];
+            emit((int)(code >> IGN_SLOT_SHIFT), (int64_t)(code & IGN_ROW_MASK), mb.h_order[pos]);
+          }
+      }, tptr, tidx);
       ga_n = std::max(ga_n, mb.n_dst * 3 * H);
       gu_n = std::max(gu_n, mb.n_dst * 3 * H);
       dx_n = std::max(dx_n, mb.n_dst * DIN);
@@ -341,11 +371,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     for (int s = 0; s < S; ++s) {
       const int se = mp.src[s].entity;
       const MsgNN& nn = mp.nn[s];
-      const int64_t rows_s = nn.layers.empty() ? b->rows[se] : mb.n_edges[s];
-      std::vector<int32_t> ptr, idx;
-      build_csr(rows_s, kv[s], ptr, idx);
+      const int64_t rows_s = tkeys[s];
       int32_t *dp = nullptr, *di = nullptr;
-      if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
+      if ((rc = tupload(t.get(), &dp, tptr[s])) || (rc = tupload(t.get(), &di, tidx[s]))) return rc;
       mt.tptr.push_back(dp);
       mt.tidx.push_back(di);
       mt.trows.push_back(rows_s);
@@ -360,16 +388,16 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       dmsg_n = std::max(dmsg_n, ne * nn.dout());
       mz_n = std::max(mz_n, ne * widest);
       mdin_n = std::max(mdin_n, ne * nn.din);
-      std::vector<int32_t> es(ne), ed(ne);
+      hvec<int32_t> es(ne), ed(ne);
       HIP_TRY(hipMemcpyAsync(es.data(), mb.d_edge_src[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost, upload_stream()));
       HIP_TRY(hipMemcpyAsync(ed.data(), mb.d_edge_dst[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost, upload_stream()));
       HIP_TRY(hipStreamSynchronize(upload_stream()));
-      std::vector<std::pair<int64_t, int32_t>> ks(ne), kd(ne);
+      hvec<std::pair<int64_t, int32_t>> ks(ne), kd(ne);
       for (int64_t e = 0; e < ne; ++e) {
         ks[e] = {es[e], (int32_t)e};
         kd[e] = {ed[e], (int32_t)e};
       }
-      std::vector<int32_t> p1, i1, p2, i2;
+      hvec<int32_t> p1, i1, p2, i2;
       build_csr(b->rows[se], ks, p1, i1);
       build_csr(b->rows[mp.dst], kd, p2, i2);
       if ((rc = tupload(t.get(), &mt.nsrc_ptr[s], p1)) || (rc = tupload(t.get(), &mt.nsrc_idx[s], i1)) ||
@@ -431,9 +459,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       } else if (op.type == IGN_RO_EXTEND) {
         for (int j = 0; j < 2; ++j) {
           const std::vector<int32_t>& ix = bo.h_idx[j];
-          std::vector<std::pair<int64_t, int32_t>> kv(ix.size());
+          hvec<std::pair<int64_t, int32_t>> kv(ix.size());
           for (size_t e2 = 0; e2 < ix.size(); ++e2) kv[e2] = {ix[e2], (int32_t)e2};
-          std::vector<int32_t> ptr, idx;
+          hvec<int32_t> ptr, idx;
           build_csr(space_rows(p, b, p->ro_t[op.in[j]]), kv, ptr, idx);
           int32_t *dp = nullptr, *di = nullptr;
           if ((rc = tupload(t.get(), &dp, ptr)) || (rc = tupload(t.get(), &di, idx))) return rc;
@@ -447,6 +475,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       return rc;
   }
   if ((rc = talloc(t.get(), &t->part, part_n)) || (rc = talloc(t.get(), &t->bsum, (32 + 1) * 3 * 32))) return rc;
+  HIP_TRY(hipStreamSynchronize(upload_stream()));   // IGN_POOL_POISON fills have landed
   b->train = t.release();
   return IGN_OK;
 }
@@ -564,7 +593,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
   const int64_t P = b->n_pred;
   set_tsgemm_bf(p->tsgemm_bf);
   HIP_TRY(hipMemsetAsync(grads, 0, p->n_params * sizeof(float), st));
-  std::vector<int> dcur(E, 0);
+  hvec<int> dcur(E, 0);
   for (int e = 0; e < E; ++e)
     HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, b->rows[e] * p->ents[e].hidden_dim * sizeof(float), st));
 

@@ -25,11 +25,12 @@ def _need_gpu():
         pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
 
 
-def _engine_grads(desc, dims, graphs, labels, prm):
-    mi = Model_information(copy.deepcopy(desc), dims)
-    plan = MPPlan.from_model_info(mi)
-    eng = Engine(plan, 0)
-    eng.set_params(prm)
+def _engine_grads(desc, dims, graphs, labels, prm, eng=None):
+    if eng is None:
+        mi = Model_information(copy.deepcopy(desc), dims)
+        plan = MPPlan.from_model_info(mi)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
     b = Batch(eng, graphs)
     b.enable_training()
     pred = b.forward_train()
@@ -248,3 +249,35 @@ def test_split_bf16_backward_matches_f32(monkeypatch, switch):
     g0 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
     assert not np.array_equal(g0, g1)   # the switch took effect
     assert np.linalg.norm(g1.astype(np.float64) - g0) <= 1e-5 * np.linalg.norm(g0)
+
+
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_pooled_buffers_reused_and_poisoned(monkeypatch, kind):
+    """Batch and training buffers come from the plan's device-memory cache (devpool.cpp): a batch
+    built after another was destroyed reuses its blocks.  With IGN_POOL_POISON=1 every scratch
+    block starts as NaN, so predictions and gradients bitwise equal to those on uncached hipMalloc
+    blocks (IGN_POOL=0) show that no kernel reads scratch it has not written, and that a reused
+    block carries nothing over from the batch before (a smaller one in between)."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, "synth50", 6)
+    prm = MPPlan.from_model_info(mi).init_params(17, bias_scale=0.1)
+    monkeypatch.setenv("IGN_POOL", "0")
+    _, b0, p0, l0, _, g0 = _engine_grads(desc, dims, graphs, labels, prm)
+    f0 = b0.forward()
+    g0 = g0.cpu().numpy()
+    b0.close()
+    monkeypatch.setenv("IGN_POOL", "1")
+    monkeypatch.setenv("IGN_POOL_POISON", "1")
+    eng = Engine(MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims)), 0)
+    eng.set_params(prm)
+    for rep in range(3):
+        gs, ls = (graphs, labels) if rep != 1 else (graphs[:2], labels[:2])
+        _, b, pred, loss, _, g = _engine_grads(desc, dims, gs, ls, prm, eng=eng)
+        fwd = b.forward()
+        if rep != 1:
+            np.testing.assert_array_equal(pred, p0)
+            np.testing.assert_array_equal(fwd, f0)
+            np.testing.assert_array_equal(g.cpu().numpy(), g0)
+            assert loss == l0
+        else:
+            assert np.isfinite(pred).all() and np.isfinite(g.cpu().numpy()).all()
+        b.close()

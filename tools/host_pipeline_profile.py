@@ -1,9 +1,11 @@
 """Per-stage host time of the training input pipeline for one 512 x synth50 batch (GPU box):
 the native reader's gather, normalisation, ign_batch_create, ign_batch_enable_training, the
-label copy.  python tools/host_pipeline_profile.py [graphs]"""
+label copy.  python tools/host_pipeline_profile.py [graphs]; env REPS (per thread), THREADS (concurrent
+builders, like the prefetch workers)."""
 import os
 import sys
 import tempfile
+import threading
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -33,27 +35,46 @@ def main():
     ds = NativeDataset.for_model(os.path.join(tmp, "train"), mi)
     print("open + parse %.3f s" % (time.perf_counter() - t))
     keys = plan_keys(plan)
-    rng = np.random.default_rng(0)
-    for rep in range(3):
-        ids = rng.permutation(n)
-        t0 = time.perf_counter()
-        bg, labels = ds.batch(ids, keys)
-        t1 = time.perf_counter()
-        for f in mi.get_all_features():
-            if str(f.normalization) != "None" and f.name in bg:
-                v, lens = bg.get(f.name)
-                bg.arrays[f.name] = (np.asarray(gm._resolve(f.normalization)(v, f.name), np.float32), lens)
-        t2 = time.perf_counter()
-        b = Batch(eng, bg)
-        t3 = time.perf_counter()
-        b.enable_training()
-        t4 = time.perf_counter()
-        b.close()
-        t5 = time.perf_counter()
-        print("rep %d: gather %.1f ms, normalise %.1f ms, batch_create %.1f ms, enable_training %.1f ms, "
-              "destroy %.1f ms" % (rep, 1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2), 1e3 * (t4 - t3),
-                                   1e3 * (t5 - t4)))
+    reps = int(os.environ.get("REPS", "3"))
+    threads = int(os.environ.get("THREADS", "1"))
+    stages = ("gather", "normalise", "batch_create", "enable_training", "destroy")
+    times = {k: [] for k in stages}
+    lock = threading.Lock()
 
+    def work(seed):
+        rng = np.random.default_rng(seed)
+        for rep in range(reps):
+            ids = rng.permutation(n)
+            t = [time.perf_counter()]
+            bg, labels = ds.batch(ids, keys)
+            t.append(time.perf_counter())
+            for f in mi.get_all_features():
+                if str(f.normalization) != "None" and f.name in bg:
+                    v, lens = bg.get(f.name)
+                    bg.arrays[f.name] = (np.asarray(gm._resolve(f.normalization)(v, f.name), np.float32), lens)
+            t.append(time.perf_counter())
+            b = Batch(eng, bg)
+            t.append(time.perf_counter())
+            b.enable_training()
+            t.append(time.perf_counter())
+            b.close()
+            t.append(time.perf_counter())
+            with lock:
+                for k, a, c in zip(stages, t[:-1], t[1:]):
+                    times[k].append(1e3 * (c - a))
+                if threads == 1:
+                    print("rep %d: " % rep + ", ".join("%s %.1f ms" % (k, times[k][-1]) for k in stages))
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    wall = time.perf_counter() - t0
+    print("threads %d: %.1f ms per batch (wall / batches); mean per stage: %s" % (
+        threads, 1e3 * wall / (threads * reps),
+        ", ".join("%s %.1f" % (k, np.mean(times[k][threads:] or times[k])) for k in stages)))
 
 if __name__ == "__main__":
     main()
