@@ -127,8 +127,17 @@ def cpu_baseline(desc, dims, prm, graphs, budget_s, what="synth50 graphs"):
     _cpu_worker((desc, dims, prm, graphs[:1], time.time()))   # imports, before the clock starts
     t0 = time.time()
     jobs = [(desc, dims, prm, graphs[k::n], t0 + budget_s) for k in range(n)]
-    with mproc.get_context("fork").Pool(n) as pool:
+    # close + join, not the context manager's terminate(): SIGTERM to the workers hangs them under
+    # rocprofv3 (its preloaded signal handler), and the profile pass runs this same command
+    pool = mproc.get_context("fork").Pool(n)
+    try:
         res = pool.map(_cpu_worker, jobs)
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     dt = time.time() - t0
     done = sum(r[0] for r in res)
     edges = sum(r[1] for r in res)
