@@ -670,18 +670,19 @@ __device__ __forceinline__ void split_mfma_rt(const bf8* __restrict__ afrag, int
   bf8 w[3];
 #pragma unroll
   for (int pu = 0; pu < 3; ++pu) w[pu] = afrag[pu * stride];
+  // the row tiles innermost: consecutive MFMAs accumulate into different tiles (a dependent
+  // MFMA waits for the previous one's result)
 #pragma unroll
-  for (int t = 0; t < RT; ++t)
+  for (int pu = 2; pu >= 0; --pu)
 #pragma unroll
-    for (int pu = 2; pu >= 0; --pu)
+    for (int ph = 2; ph >= 0; --ph) {
+      if (PASSES == 6 && pu + ph > 2) continue;
 #pragma unroll
-      for (int ph = 2; ph >= 0; --ph) {
-        if (PASSES == 6 && pu + ph > 2) continue;
-        acc[t] = MFMA_BF(w[pu], b[t][s][ph], acc[t]);
-      }
+      for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF(w[pu], b[t][s][ph], acc[t]);
+    }
 }
 
-template <int DIN, int ACT, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32), int RT = 1>
+template <int DIN, int ACT, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32), int RT = 1, bool PERSIST = false>
 __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, const bf8* __restrict__ W1f,
                                                                  const bf8* __restrict__ W2f) {
   constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
@@ -701,8 +702,12 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
   }
   for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
+  // PERSIST: the block loops over row groups with W1 staged once; the chunk loop's wrap-around
+  // prefetch leaves chunk 0 in sw2[0] for the next group
+  const int64_t n_groups = (a.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
+  for (int64_t grp = blockIdx.x; grp < n_groups; grp += PERSIST ? (int64_t)gridDim.x : n_groups) {
   // RT row tiles of 16 per wave: tile t covers rows r0 + 16t .. +16
-  const int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * (16 * RT) + j;
+  const int64_t r0 = (grp * WAVES + wave) * (16 * RT) + j;
   // layer-1 input fragments: lane (row j, group g) holds x[row][32s + 8g .. +8) (natural k order)
   bf8 xf[RT][KS1][3];
 #pragma unroll
@@ -802,6 +807,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
       a.y[r] = act_apply(yt + b3, a.act3);
     }
   }
+  }  // row groups
 }
 
 
@@ -926,17 +932,24 @@ hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStrea
   return hipGetLastError();
 }
 
-template <int DIN, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32), int RT = 1>
+template <int DIN, int ACT, int WAVES, int PASSES, int CT, bool W1L, int RT, bool PERSIST>
+static void readout_bf_launch(const Readout3Args& args, const bf8* w1, const bf8* w2, hipStream_t st) {
+  auto k = readout_bf_kernel<DIN, ACT, WAVES, PASSES, CT, W1L, RT, PERSIST>;
+  const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
+  const int64_t grid = PERSIST ? persistent_grid(k, groups, 64 * WAVES) : groups;
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * WAVES), 0, st, args, w1, w2);
+}
+
+template <int DIN, int WAVES, int PASSES, int CT, bool W1L = (DIN == 32), int RT = 1, bool PERSIST = false>
 static hipError_t readout_bf_din(const Readout3Args& args, const void* W1f, const void* W2f, hipStream_t st) {
-  const dim3 grid((unsigned)((args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES))), block(64 * WAVES);
   const bf8* w1 = static_cast<const bf8*>(W1f);
   const bf8* w2 = static_cast<const bf8*>(W2f);
   switch (args.act1) {
-    case IGN_K_ACT_SELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_RELU: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_TANH: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
-    case IGN_K_ACT_SIGMOID: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
-    default: hipLaunchKernelGGL((readout_bf_kernel<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT, W1L, RT>), grid, block, 0, st, args, w1, w2); break;
+    case IGN_K_ACT_SELU: readout_bf_launch<DIN, IGN_K_ACT_SELU, WAVES, PASSES, CT, W1L, RT, PERSIST>(args, w1, w2, st); break;
+    case IGN_K_ACT_RELU: readout_bf_launch<DIN, IGN_K_ACT_RELU, WAVES, PASSES, CT, W1L, RT, PERSIST>(args, w1, w2, st); break;
+    case IGN_K_ACT_TANH: readout_bf_launch<DIN, IGN_K_ACT_TANH, WAVES, PASSES, CT, W1L, RT, PERSIST>(args, w1, w2, st); break;
+    case IGN_K_ACT_SIGMOID: readout_bf_launch<DIN, IGN_K_ACT_SIGMOID, WAVES, PASSES, CT, W1L, RT, PERSIST>(args, w1, w2, st); break;
+    default: readout_bf_launch<DIN, IGN_K_ACT_LINEAR, WAVES, PASSES, CT, W1L, RT, PERSIST>(args, w1, w2, st); break;
   }
   return hipGetLastError();
 }
@@ -952,8 +965,10 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   // default (passes 6): two 16-row tiles per wave sharing every W2 fragment read, 8-wave blocks
   // (246 VGPRs, 2 waves/SIMD): 1.03-1.05 ms against 1.13-1.16 ms for one tile per wave in 12-wave
   // blocks, 1.18 ms with 32-unit W2 chunks, 1.39-1.41 ms with 4-wave blocks (512 x synth50, round 1)
+  // persistent blocks (W1 staged once per block, W2 chunk 0 carried over): 3.54-3.56 vs 3.58-3.59
+  // ms/step on one box (tools/ab_env.sh, round 2)
   if (din == 32)
-    return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2>(args, W1f, W2f, st);
+    return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
   return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 8, 6, 1, false, 2>(args, W1f, W2f, st);
 }
 
