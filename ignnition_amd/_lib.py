@@ -99,9 +99,9 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_batch_enable_training", "ign_forward_train", "ign_backward", "ign_mse_loss", "ign_l2_loss",
            "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get", "ign_dataset_batch_create",
-           "ign_dataset_batch_get", "ign_dataset_batch_destroy"]
+           "ign_dataset_batch_get", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json"]
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -162,6 +162,8 @@ def _load():
         "ign_dataset_batch_create": (C.c_int, [VP, P(i64), i32, P(VP)]),
         "ign_dataset_batch_get": (C.c_int, [VP, C.c_char_p, P(i32), P(VP), P(i64), P(P(i64))]),
         "ign_dataset_batch_destroy": (None, [VP]),
+        "ign_plan_create_json": (C.c_int, [C.c_char_p, C.c_char_p, i32, P(VP)]),
+        "ign_plan_describe_json": (C.c_int, [VP, C.c_char_p, i64, P(i64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

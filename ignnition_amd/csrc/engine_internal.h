@@ -265,6 +265,7 @@ struct ign_plan {
   bool use_graph = true;          // replay ign_forward as one captured hipGraph; IGN_HIP_GRAPH=0 disables
   ign_stats_t stats{};
   std::shared_ptr<DevPool> pool;  // batch / training buffers (created with the stream, ensure_device)
+  std::string describe;           // ign_plan_create_json: ign_plan_describe_json's document
 };
 
 struct ign_batch {

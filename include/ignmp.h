@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 7
+#define IGN_ABI_VERSION 8
 
 enum ign_status {
   IGN_OK = 0,
@@ -211,6 +211,17 @@ const char* ign_last_error(void);
 int  ign_device_count(int32_t* n);
 
 int  ign_plan_create(const ign_plan_desc* desc, int32_t device, ign_plan** out);
+/* The same plan from the files the reference reads (ComnetModel.__init__ over Model_information,
+ * GM:235-382 / JO:128-149): model_description.json text and the dataset dimensions as a JSON
+ * object {feature or adjacency name: size} (JO:162-180).  Lowered in C++ (csrc/plan_json.cpp)
+ * exactly as ignnition_amd/engine.py MPPlan.from_model_info + to_desc; IGN_ERR_UNSUPPORTED for a
+ * model the engine does not lower (same messages), IGN_ERR_INVALID for one the reference rejects. */
+int  ign_plan_create_json(const char* model_json, const char* dims_json, int32_t device, ign_plan** out);
+/* For a plan from ign_plan_create_json: a JSON document with the entity / feature order, every
+ * adjacency slot's input keys (src_<adj>, dst_<adj>, seq_<src>_<dst>, GM:127-158), the interleave
+ * keys (indices_<src>_to_<dst>), the label and the parameter tensors' Keras-style names and shapes
+ * in ign_plan_param_tensor order.  *needed = bytes incl. the terminating NUL; buf may be NULL. */
+int  ign_plan_describe_json(const ign_plan* plan, char* buf, int64_t size, int64_t* needed);
 void ign_plan_destroy(ign_plan* plan);
 int  ign_plan_num_params(const ign_plan* plan, int64_t* n_floats);
 int  ign_plan_num_param_tensors(const ign_plan* plan, int32_t* n);

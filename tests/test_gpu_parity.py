@@ -485,3 +485,24 @@ def test_pooling_many_chunks(kind):
     out, ref, b, _ = _run(desc, dims, graphs, seed=5, bias=0.1)
     _close(out, ref)
     assert out.size == 1
+
+
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_json_plan_forward_matches_python_plan(kind):
+    """A plan from ign_plan_create_json (the C++ lowering of model_description.json) runs the
+    same forward as the Python-lowered plan: bitwise-equal predictions."""
+    import ctypes as C
+    import json
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(kind, "nsfnet", 2)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(3, bias_scale=0.1)
+    e1 = Engine(plan, 0)
+    e1.set_params(prm)
+    ref = Batch(e1, graphs).forward()
+    e2 = Engine(plan, 0)
+    h = C.c_void_p()
+    _lib.check(_lib.lib.ign_plan_create_json(json.dumps(desc).encode(), json.dumps(dims).encode(), 0, C.byref(h)))
+    _lib.lib.ign_plan_destroy(e2.handle)
+    e2.handle = h
+    e2.set_params(prm)
+    np.testing.assert_array_equal(Batch(e2, graphs).forward(), ref)
