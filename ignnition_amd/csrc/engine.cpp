@@ -544,9 +544,13 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   }
   b->halo.assign(E, 0);
   if (d->halo_rows) {
+    // a partition holds only its own destinations: the attention softmax normalises over all of the
+    // graph's destinations per position (AUX:327-336), and the sorted updates pad per graph
+    // (GM:477-543).  Sum / convolution MPs, with or without message networks, are destination-local.
     for (auto& mp : p->mps)
-      for (auto& nn : mp.nn)
-        if (!nn.layers.empty()) return fail(IGN_ERR_UNSUPPORTED, "edge-cut partitions with message networks");
+      if (mp.aggr == IGN_AGGR_ATTENTION || mp.sorted)
+        return fail(IGN_ERR_UNSUPPORTED, "edge-cut partitions support sum and convolution MPs only (attention "
+                    "normalises over the whole graph, AUX:327-336; ordered updates pad per graph, GM:477-543)");
     for (int e = 0; e < E; ++e) {
       if (d->halo_rows[e] < 0) return fail(IGN_ERR_INVALID, "entity %d: negative halo_rows", e);
       b->halo[e] = d->halo_rows[e];
@@ -837,8 +841,14 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     } else {
       sort_order(order, flen);
       // edge-cut partitions: destinations reading a halo row go last (they wait for the exchange)
-      hvec<char> bnd(ND, 0);
-      for (size_t k = 0; k < mdst.size(); ++k) {
+      // (a message network's codes address edges, and its per-edge pass reads every source row
+      // before any destination runs: no interior destinations then)
+      bool nets = false;
+      for (auto& nn : mp.nn) nets = nets || !nn.layers.empty();
+      bool halo = false;
+      for (auto& sd : mp.src) halo = halo || b->halo[sd.entity] > 0;
+      hvec<char> bnd(ND, nets && halo ? 1 : 0);
+      for (size_t k = 0; k < mdst.size() && !nets; ++k) {
         const uint32_t c = mcode[k];
         const int se = mp.src[c >> IGN_SLOT_SHIFT].entity;
         if ((int64_t)(c & IGN_ROW_MASK) >= b->rows[se]) bnd[mdst[k]] = 1;

@@ -62,9 +62,16 @@ class LocalPart:
 
 def _check_plan(plan: MPPlan):
     for m in plan.mps:
-        if m["aggr"] != "sum":
-            raise ValueError("edge-cut partitioning supports sum MPs only (ordered/interleave pad per graph, "
-                             "GM:477-543); shard such batches by graph")
+        if m["aggr"] not in ("sum", "convolution"):
+            raise ValueError("edge-cut partitioning supports sum and convolution MPs only (ordered/interleave/concat "
+                             "pad per graph, GM:477-543; attention normalises over all of a graph's destinations, "
+                             "AUX:327-336); shard such batches by graph")
+
+
+def _overlappable(m) -> bool:
+    """Interior destinations can run beside the exchange: a plain sum MP.  A message network reads
+    every source row (halo ones included) in its per-edge pass before any destination runs."""
+    return m["aggr"] == "sum" and not any(m.get("nets", []))
 
 
 def local_part(inputs: dict, plan: MPPlan, rank: int, world: int) -> LocalPart:
@@ -92,6 +99,10 @@ def local_part(inputs: dict, plan: MPPlan, rank: int, world: int) -> LocalPart:
         dlo, dhi = ranges[slot.dst][rank], ranges[slot.dst][rank + 1]
         keep = (d >= dlo) & (d < dhi)            # owner computes: every in-edge of an owned destination
         s, d, q = s[keep], d[keep] - dlo, q[keep]
+        kp = "params_" + slot.adj                # per-edge parameters (message networks, GEN:156-163)
+        if kp in inputs:
+            prm = np.asarray(inputs[kp], np.float32)
+            out[kp] = prm.reshape(len(keep), -1)[keep]
         slo, shi = ranges[slot.src][rank], ranges[slot.src][rank + 1]
         rem = (s < slo) | (s >= shi)
         remote[slot.src].append(s[rem])
@@ -261,7 +272,7 @@ class EdgeCutForward:
         for _ in range(self.plan.iterations):      # GM:406
             for mi, m in enumerate(self.plan.mps):
                 need = [n for n in self.mp_sources[mi] if n in stale]
-                if need and self.overlap:
+                if need and self.overlap and _overlappable(m):
                     works = [self._exchange(n, True) for n in need]
                     for b in self.batches:
                         b.run_mp(mi, "interior")

@@ -167,3 +167,25 @@ def test_edge_cut_gloo_world2():
         assert (n_owned, n_halo, sc, rc) == (h.n_owned, h.n_halo, h.send_counts, h.recv_counts)
         # what r sends to q is what q receives from r
         assert sc[1 - r] == res[1 - r][3][r]
+
+
+def test_edge_cut_carries_edge_parameters():
+    """A partition keeps the per-edge parameters (params_<adj>, GEN:156-163) of the in-edges it
+    keeps, in their original order (message networks reading edge_params)."""
+    from ignnition_amd.engine import MPPlan as _P
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=400, hidden=32, iterations=2, window=16)
+    plan = _P.from_model_info(mi)
+    x = dict(graphs[0])
+    E = len(x["src_adj_nodes_nodes"])
+    x["params_adj_nodes_nodes"] = np.arange(2 * E, dtype=np.float32).reshape(E, 2)
+    world = 3
+    kept = []
+    for r in range(world):
+        p = partition.local_part(x, plan, r, world)
+        prm = p.inputs["params_adj_nodes_nodes"]
+        assert prm.shape == (len(p.inputs["src_adj_nodes_nodes"]), 2)
+        kept.append(prm[:, 0] / 2)
+    ids = np.concatenate(kept).astype(np.int64)
+    assert sorted(ids.tolist()) == list(range(E))   # every edge exactly once
+    for k in kept:
+        assert np.all(np.diff(k) > 0)                # original order within a partition
