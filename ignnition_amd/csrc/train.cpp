@@ -226,11 +226,6 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   const int E = (int)p->ents.size();
   for (int e = 0; e < E; ++e)
     if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
-  for (auto& mp : p->mps) {
-    if (mp.aggr == IGN_AGGR_ATTENTION)
-      for (auto& nn : mp.nn)
-        if (!nn.layers.empty()) return fail(IGN_ERR_UNSUPPORTED, "no backward for attention over message networks");
-  }
   for (size_t c = 0; c < p->cells.size(); ++c) {
     const CellP& cp = p->cells[c];
     if (!cp.used) continue;
@@ -333,7 +328,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         for (int64_t m = 0; m < mb.n_msgs; ++m)
           am[mb.h_msg_src[m] >> IGN_SLOT_SHIFT].push_back({(int64_t)(mb.h_msg_src[m] & IGN_ROW_MASK), (int32_t)m});
         for (int s = 0; s < S; ++s) {
-          const int64_t rows_s = b->rows[mp.src[s].entity];
+          // a message network's codes address its edges (the per-edge message rows)
+          const int64_t rows_s = mp.nn[s].layers.empty() ? b->rows[mp.src[s].entity] : mb.n_edges[s];
           hvec<int32_t> ptr, idx;
           build_csr(rows_s, am[s], ptr, idx);
           int32_t *dp = nullptr, *di = nullptr;
@@ -788,10 +784,15 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
         HIP_TRY(hipMemsetAsync(t->adw12, 0, 2 * p->attn_F * sizeof(float), st));
         HIP_TRY(launch_attn_bwd_parts(aa, t->dx, mt.amdst, sb, F, mb.n_msgs, t->adw, t->adv, st));
         for (size_t s = 0; s < mp.src.size(); ++s) {
-          const int64_t rows_s = b->rows[mp.src[s].entity];
+          // over a message network the source rows are its per-edge messages: their gradient goes
+          // through the network's backward to the states it read (GM:440-475)
+          const bool net = !mp.nn[s].layers.empty();
+          const int64_t rows_s = net ? mb.n_edges[s] : b->rows[mp.src[s].entity];
+          if (net) HIP_TRY(hipMemsetAsync(t->dmsg, 0, rows_s * F * sizeof(float), st));
           HIP_TRY(launch_attn_src_bwd(rows_s, mt.asptr[s], mt.asidx[s], mb.d_msg_w, t->adv, mt.amdst, t->dx, w12, F,
-                                      src_grad(s), t->ads_src, st));
+                                      net ? t->dmsg : src_grad(s), t->ads_src, st));
           HIP_TRY(launch_tsgemm_add(srcs[s], F, t->ads_src, 1, rows_s, F, 1, t->part, t->adw12, nullptr, st));
+          if (net && (rc = msg_net_backward(p, b, t, mp, mb, mt, (int)s, src_grad(s), dh_out, grads, st))) return rc;
         }
         HIP_TRY(launch_attn_dst_bwd(mb.n_dst, mb.d_order, mb.d_msg_ptr, t->adv, w12 + p->attn_F, H, dh_out, t->ads_dst,
                                     st));

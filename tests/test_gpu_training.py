@@ -156,6 +156,17 @@ def test_gradients_message_networks(inputs, units, act, ordered, l2):
     _check(desc, dims, graphs, labels, prm)
 
 
+@pytest.mark.parametrize("inputs", [("hs_source", "hs_dest"), ("hs_dest", "hs_source", "edge_params")])
+def test_gradients_attention_over_message_network(inputs):
+    """Attention (AUX:287-343) whose source rows are a message network's per-edge outputs
+    (GM:440-475): the score and weighted-message gradients of each edge flow back through the
+    network to the states it read."""
+    desc, dims, graphs, labels, prm = _msg_net_case(inputs, (32,), "tanh")
+    desc["message_passing"]["stages"][1]["stage_mp"][0]["aggregation"] = {"type": "attention"}
+    prm = MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims)).init_params(8, bias_scale=0.1)
+    _check(desc, dims, graphs, labels, prm)
+
+
 @pytest.mark.parametrize("aggr", [{"type": "convolution"}, {"type": "convolution", "activation_function": "tanh"},
                                   {"type": "convolution", "activation_function": "selu"}])
 def test_gradients_convolution(aggr):
