@@ -18,6 +18,8 @@ Extra objects on the JSON line:
   cpu_baseline  the dense-padded oracle (oracle/dense_forward.py, float32 numpy, the TF op
                 sequence incl. padded work) on a bounded sample of the same workload, rank 0, N=1,
                 one process per CPU this process may use (CPU model and count on the line).
+  cpu_baseline_cxx  the second CPU line: the C++/OpenMP float32 restatement
+                (oracle/cpu_forward.cpp) on the same sample and CPUs.
 """
 
 import argparse
@@ -148,6 +150,35 @@ def cpu_baseline(desc, dims, prm, graphs, budget_s, what="synth50 graphs"):
                       % (done, what, len(set(map(id, graphs))), dt, n)}
 
 
+def cpu_baseline_cxx(plan, mi, prm, graphs, budget_s, what="synth50 graphs"):
+    """SURVEY §8(d)'s second CPU line: the C++/OpenMP float32 restatement (oracle/cpu_forward.cpp,
+    packed per destination, no padded work) on the same sample, OpenMP over graphs (or over the
+    destinations of one large graph) on every CPU this process may use.  None if it cannot be built."""
+    from ignnition_amd import workloads
+    try:
+        from oracle import cpu_oracle
+        cpu_oracle.build()
+    except Exception as e:   # no g++ / OpenMP on the host: report why instead of failing the bench
+        return {"value": None, "unit": "edges/s", "kind": "port", "error": str(e)[:200]}
+    n = _cpu_share()
+    graphs = list(graphs)
+    per = max(2 * n, 32) if len(graphs) > 1 else 1
+    chunks = [graphs[k:k + per] for k in range(0, len(graphs), per)]
+    chunk_edges = [workloads.edges_per_forward(mi, c) for c in chunks]
+    cpu_oracle.cpu_forward(plan, chunks[0][:1], prm, n)   # load + first touch, before the clock
+    t0 = time.time()
+    done = edges = k = 0
+    while time.time() - t0 < budget_s or done == 0:
+        cpu_oracle.cpu_forward(plan, chunks[k % len(chunks)], prm, n)
+        edges += chunk_edges[k % len(chunks)]
+        done += len(chunks[k % len(chunks)])
+        k += 1
+    dt = time.time() - t0
+    return {"value": edges / dt, "unit": "edges/s", "cores": n, "kind": "port", "cpu_model": _cpu_model(),
+            "sample": "%d forwards of %s (full T=8 each) in %.1f s, OpenMP %d threads, C++ float32 restatement "
+                      "(oracle/cpu_forward.cpp: packed per destination, no padded work)" % (done, what, dt, n)}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -191,15 +222,17 @@ def main():
                                                                      first_id=ids[0])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(seed=0, bias_scale=0.05)
-    cpu = None
+    cpu = cpu_cxx = None
     if world == 1 and not args.no_cpu and not args.train:
         # before anything touches the GPU: the baseline's worker processes are forked
         if synthetic:
             # bounded sample: 25k-node graphs from the same generator (same degree law and locality)
             sd, sdims, _, sg, _ = workloads.make_synthetic_inputs(n_nodes=25_000)
             cpu = cpu_baseline(sd, sdims, prm, sg, args.cpu_seconds, "a 25k-node / 250k-edge synthetic graph")
+            cpu_cxx = cpu_baseline_cxx(plan, mi, prm, sg, args.cpu_seconds, "a 25k-node / 250k-edge synthetic graph")
         else:
             cpu = cpu_baseline(desc, dims, prm, graphs, args.cpu_seconds)
+            cpu_cxx = cpu_baseline_cxx(plan, mi, prm, graphs, args.cpu_seconds)
     eng = Engine(plan, device if world > 1 else 0)
     eng.set_params(prm)
     t_build = time.perf_counter()
@@ -378,6 +411,7 @@ def main():
                    "samples_per_s": round(args.graphs * world * args.steps / dt, 1)},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "cpu_baseline_cxx": cpu_cxx,
     }
     print(json.dumps(line))
     if dist is not None:

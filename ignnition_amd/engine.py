@@ -503,6 +503,63 @@ class BatchedGraphs:
         return key in self.arrays
 
 
+def batch_desc(p: "MPPlan", graphs, halo_rows: dict = None):
+    """The ``ign_batch_desc`` of a list of feature dicts or a ``BatchedGraphs`` for plan ``p``:
+    (desc, arrays the desc points into, (G, E, num [G, E], edge counts [G, A], halo or None))."""
+    bg = graphs if isinstance(graphs, BatchedGraphs) else BatchedGraphs.from_dicts(graphs)
+    G = bg.num_graphs
+    E = len(p.entities)
+    num = np.zeros((G, E), np.int64)
+    for e, name in enumerate(p.entities):
+        v, _ = bg.get("num_" + name)
+        num[:, e] = np.asarray(v, np.int64).reshape(G)
+    feats = []
+    for e, name in enumerate(p.entities):
+        cols = []
+        for fname, size in p.features[e]:
+            v, lens = bg.get(fname)
+            if not np.array_equal(np.asarray(lens, np.int64), num[:, e] * size):
+                raise ValueError("feature %s: %s values per graph for %s nodes of size %d"
+                                 % (fname, list(lens), list(num[:, e]), size))
+            cols.append(np.asarray(v, np.float32).reshape(-1, size))
+        feats.append(np.ascontiguousarray(np.concatenate(cols, 1)) if cols else None)
+    A = len(p.adj_slots)
+    cnt = np.zeros((G, A), np.int64)
+    srcs, dsts, seqs = [], [], []
+    for a, slot in enumerate(p.adj_slots):
+        ks, kd, kq = slot.keys
+        (s, ls), (d, ld), (q, lq) = bg.get(ks), bg.get(kd), bg.get(kq)
+        if not (np.array_equal(ls, ld) and np.array_equal(ls, lq)):
+            raise ValueError("%s/%s/%s have different lengths" % (ks, kd, kq))
+        cnt[:, a] = ls
+        srcs.append(_i64(s)), dsts.append(_i64(d)), seqs.append(_i64(q))
+    I = len(p.il_slots)
+    il_len = np.zeros((G, max(I, 1)), np.int64)
+    ils = []
+    for i, key in enumerate(p.il_slots):
+        v, lens = bg.get(key)
+        il_len[:, i] = lens
+        ils.append(_i64(v))
+    fp = C.POINTER(C.c_float)
+    lp = C.POINTER(C.c_int64)
+    feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
+    mk = lambda arrs: (lp * max(len(arrs), 1))(*[a.ctypes.data_as(lp) for a in arrs])
+    prm_arrays = []
+    for slot in p.adj_slots:
+        key = "params_" + slot.adj
+        prm_arrays.append(np.ascontiguousarray(np.asarray(bg.get(key)[0], np.float32)) if key in bg else None)
+    halo = None
+    if halo_rows:
+        halo = np.array([int(halo_rows.get(name, 0)) for name in p.entities], np.int64)
+    ptrs = (feat_ptrs, mk(srcs), mk(dsts), mk(seqs), mk(ils), (fp * max(A, 1))(*[a.ctypes.data_as(fp) if a is not None
+                                                                                 else fp() for a in prm_arrays]))
+    desc = _lib.BatchDesc(G, num.ctypes.data_as(lp), ptrs[0], cnt.ctypes.data_as(lp), ptrs[1], ptrs[2], ptrs[3],
+                          il_len.ctypes.data_as(lp), ptrs[4], halo.ctypes.data_as(lp) if halo is not None else lp(),
+                          ptrs[5])
+    keep = (num, feats, cnt, srcs, dsts, seqs, il_len, ils, prm_arrays, halo, ptrs)
+    return desc, keep, (G, E, num, cnt, halo)
+
+
 class Batch:
     """A disjoint-union batch of graphs on the device (``ign_batch``).
 
@@ -515,58 +572,9 @@ class Batch:
         edge-cut partition (see partition.py)."""
         p = engine.plan
         self.engine = engine
-        bg = graphs if isinstance(graphs, BatchedGraphs) else BatchedGraphs.from_dicts(graphs)
-        G = bg.num_graphs
-        E = len(p.entities)
-        num = np.zeros((G, E), np.int64)
-        for e, name in enumerate(p.entities):
-            v, _ = bg.get("num_" + name)
-            num[:, e] = np.asarray(v, np.int64).reshape(G)
-        feats = []
-        for e, name in enumerate(p.entities):
-            cols = []
-            for fname, size in p.features[e]:
-                v, lens = bg.get(fname)
-                if not np.array_equal(np.asarray(lens, np.int64), num[:, e] * size):
-                    raise ValueError("feature %s: %s values per graph for %s nodes of size %d"
-                                     % (fname, list(lens), list(num[:, e]), size))
-                cols.append(np.asarray(v, np.float32).reshape(-1, size))
-            feats.append(np.ascontiguousarray(np.concatenate(cols, 1)) if cols else None)
-        A = len(p.adj_slots)
-        cnt = np.zeros((G, A), np.int64)
-        srcs, dsts, seqs = [], [], []
-        for a, slot in enumerate(p.adj_slots):
-            ks, kd, kq = slot.keys
-            (s, ls), (d, ld), (q, lq) = bg.get(ks), bg.get(kd), bg.get(kq)
-            if not (np.array_equal(ls, ld) and np.array_equal(ls, lq)):
-                raise ValueError("%s/%s/%s have different lengths" % (ks, kd, kq))
-            cnt[:, a] = ls
-            srcs.append(_i64(s)), dsts.append(_i64(d)), seqs.append(_i64(q))
-        I = len(p.il_slots)
-        il_len = np.zeros((G, max(I, 1)), np.int64)
-        ils = []
-        for i, key in enumerate(p.il_slots):
-            v, lens = bg.get(key)
-            il_len[:, i] = lens
-            ils.append(_i64(v))
-        self._arrays = (num, feats, cnt, srcs, dsts, seqs, il_len, ils)   # (may view bg's buffers)
-        fp = C.POINTER(C.c_float)
-        lp = C.POINTER(C.c_int64)
-        feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
-        mk = lambda arrs: (lp * max(len(arrs), 1))(*[a.ctypes.data_as(lp) for a in arrs])
-        prm_arrays = []
-        for slot in p.adj_slots:
-            key = "params_" + slot.adj
-            prm_arrays.append(np.ascontiguousarray(np.asarray(bg.get(key)[0], np.float32)) if key in bg else None)
-        halo = None
-        if halo_rows:
-            halo = np.array([int(halo_rows.get(name, 0)) for name in p.entities], np.int64)
+        desc, keep, (G, E, num, cnt, halo) = batch_desc(p, graphs, halo_rows)
+        self._arrays = keep                 # (may view the caller's buffers) until the engine copied them
         self.halo = [0] * E if halo is None else [int(v) for v in halo]
-        desc = _lib.BatchDesc(G, num.ctypes.data_as(lp), feat_ptrs, cnt.ctypes.data_as(lp), mk(srcs), mk(dsts),
-                              mk(seqs), il_len.ctypes.data_as(lp), mk(ils),
-                              halo.ctypes.data_as(lp) if halo is not None else lp(),
-                              (fp * max(A, 1))(*[a.ctypes.data_as(fp) if a is not None else fp() for a in prm_arrays]))
-        self._prm_arrays = prm_arrays
         h = C.c_void_p()
         check(lib.ign_batch_create(engine.handle, C.byref(desc), C.byref(h)))
         self.handle = h
@@ -588,7 +596,6 @@ class Batch:
         else:
             self.graph_predictions = cnt[:, space[1]].copy()
         self._arrays = None  # the engine copied what it needs
-        self._prm_arrays = None
         self._bound = {}
 
     # ---- stepped forward (edge-cut partitions) -----------------------------------

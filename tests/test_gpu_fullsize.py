@@ -1,7 +1,9 @@
 """BASELINE.json's two headline workloads at their stated sizes (MI355X only).
 
 configs[4] — the synthetic 1M-node / 10M-edge graph, H=64, T=8:
-  * the whole graph on one GPU: finite, and bitwise deterministic run to run;
+  * the whole graph on one GPU: finite, and bitwise deterministic run to run; all 1M predictions
+    against the C++/OpenMP float32 restatement (oracle/cpu_forward.cpp, itself checked against
+    the float64 dense oracle in tests/test_cpu_oracle.py);
   * the 8-way edge-cut the driver's 8-GPU bench runs (contiguous id ranges, halo rows,
     interior/boundary overlap), all 8 partitions in this process over LoopbackComm: the
     concatenated predictions equal the whole-graph run bit for bit (each destination keeps its
@@ -11,7 +13,8 @@ configs[4] — the synthetic 1M-node / 10M-edge graph, H=64, T=8
 
 configs[2] — RouteNet on 512 synth50-size graphs batched into one CSR (the default bench):
   * deterministic; three graphs of the batch equal the same graph run alone (GM:712-724: the
-    reference runs the model per graph); two graphs against the float64 oracle.
+    reference runs the model per graph); two graphs against the float64 oracle, and every
+    prediction of the batch against the C++ restatement.
 
 Tolerance: |engine - oracle| <= 1e-4 * max(1, |oracle|).
 """
@@ -24,6 +27,7 @@ import torch
 from ignnition_amd import partition, workloads
 from ignnition_amd.engine import Batch, Engine, MPPlan, device_count
 from ignnition_amd.json_operations import Model_information
+from oracle import cpu_oracle
 from oracle.dense_forward import DenseOracle
 
 pytestmark = pytest.mark.gpu
@@ -56,12 +60,12 @@ def big_graph():
     edges = whole.edges_per_forward
     out2 = whole.forward().reshape(-1)
     whole.close()
-    yield x, plan, eng, out, out2, edges
+    yield x, plan, eng, out, out2, edges, prm
     eng.close()
 
 
 def test_1m_whole_graph_finite_and_deterministic(big_graph):
-    x, plan, eng, out, out2, edges = big_graph
+    x, plan, eng, out, out2, edges, _ = big_graph
     assert out.size == 1_000_000
     assert np.all(np.isfinite(out))
     assert edges == 8 * len(x["src_adj_nodes_nodes"])
@@ -70,7 +74,7 @@ def test_1m_whole_graph_finite_and_deterministic(big_graph):
 
 def test_1m_eight_partition_edge_cut_bit_identical(big_graph):
     """The 8-rank layout of `bench.py --model synthetic --gpus 8`, in one process."""
-    x, plan, eng, out, _, edges = big_graph
+    x, plan, eng, out, _, edges, _ = big_graph
     world = 8
     parts = [partition.local_part(x, plan, r, world) for r in range(world)]
     comm = partition.LoopbackComm(world)
@@ -87,6 +91,16 @@ def test_1m_eight_partition_edge_cut_bit_identical(big_graph):
     finally:
         fw.close()
         torch.cuda.synchronize()
+
+
+def test_1m_whole_graph_matches_cpu_restatement(big_graph):
+    """Every one of the 1M predictions (H=64, T=8, 10M edges) against the C++ restatement
+    (float32, the box's CPU share)."""
+    x, plan, eng, out, _, _, prm = big_graph
+    ref = cpu_oracle.cpu_forward(plan, [x], prm, 0)
+    err = _scaled_err(out, ref)
+    print("1M synthetic vs C++ restatement: max scaled error %.3g" % err)
+    assert err <= TOL
 
 
 def test_synthetic_full_model_25k_matches_oracle():
@@ -134,4 +148,7 @@ def test_routenet_512_synth50_batch():
     for gi in (7, 400):
         err = _scaled_err(o1[off[gi]:off[gi + 1]], ora.forward([graphs[gi]]))
         assert err <= TOL, (gi, err)
+    err = _scaled_err(o1, cpu_oracle.cpu_forward(plan, graphs, prm, 0))
+    print("512 x synth50 vs C++ restatement: max scaled error %.3g" % err)
+    assert err <= TOL
     eng.close()
