@@ -6,7 +6,8 @@
 //
 // It reads the engine's own input structures (include/ignmp.h: the lowered plan and one batch
 // of graphs) and the parameters in Keras layout, and computes graph by graph exactly what the
-// TF op sequence computes, in float32 like TF on the CPU:
+// TF op sequence computes, in float32 like TF on the CPU (the bench line) or in float64 (the
+// checker of the engine's full-size outputs):
 //   hidden states   AUX:146-159  [features | zeros]
 //   per MP          GM:423-543   messages = source states gathered per edge (GM:432); position of
 //                                a message = the previous sources' per-graph max(seq)+1 plus seq
@@ -44,12 +45,14 @@ int err(int code, const char* msg) {
   return code;
 }
 
-inline float act(float x, int a) {
+template <typename T>
+inline T act(T x, int a) {
+  const T lam = T(1.0507009873554805), alpha = T(1.6732632423543772);
   switch (a) {
-    case IGN_ACT_RELU: return x > 0.f ? x : 0.f;
+    case IGN_ACT_RELU: return x > T(0) ? x : T(0);
     case IGN_ACT_SELU:   // exp of min(x, 0): both arms stay finite (-ffast-math)
-      return x > 0.f ? 1.0507009873554805f * x : 1.0507009873554805f * 1.6732632423543772f * (std::exp(std::min(x, 0.f)) - 1.f);
-    case IGN_ACT_SIGMOID: return 1.f / (1.f + std::exp(-std::min(80.f, std::max(-80.f, x))));
+      return x > T(0) ? lam * x : lam * alpha * (std::exp(std::min(x, T(0))) - T(1));
+    case IGN_ACT_SIGMOID: return T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), x))));
     case IGN_ACT_TANH: return std::tanh(x);
     default: return x;
   }
@@ -64,62 +67,64 @@ struct Cell {
 // vectorises them (libmvec expf / tanhf under -ffast-math) and, for the compile-time widths of
 // the example models, keeps the 3H accumulators in registers across the k loop: this is the
 // timed CPU line.
-template <int DIN, int H>
-void gru_step_t(const Cell& c, const float* __restrict__ x, const float* __restrict__ h, float* __restrict__ out) {
+template <int DIN, int H, typename T>
+void gru_step_t(const Cell& c, const T* __restrict__ x, const T* __restrict__ h, T* __restrict__ out) {
   constexpr int H3 = 3 * H;
-  float mx[H3], mh[H3];
+  T mx[H3], mh[H3];
   for (int j = 0; j < H3; ++j) {
     mx[j] = c.b[j];
     mh[j] = c.b[H3 + j];
   }
   for (int k = 0; k < DIN; ++k) {
-    const float xv = x[k];
+    const T xv = x[k];
     const float* __restrict__ w = c.W + k * H3;
 #pragma GCC unroll 16
     for (int j = 0; j < H3; ++j) mx[j] += xv * w[j];
   }
   for (int k = 0; k < H; ++k) {
-    const float hv = h[k];
+    const T hv = h[k];
     const float* __restrict__ u = c.U + k * H3;
 #pragma GCC unroll 16
     for (int j = 0; j < H3; ++j) mh[j] += hv * u[j];
   }
   // z | r; the argument is clamped to +-80 so that no exp overflows (-ffast-math assumes finite
   // values; sigmoid is saturated there: exp(-80) is below float32's resolution of 1)
-  for (int j = 0; j < 2 * H; ++j) mx[j] = 1.f / (1.f + std::exp(-std::min(80.f, std::max(-80.f, mx[j] + mh[j]))));
+  for (int j = 0; j < 2 * H; ++j) mx[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), mx[j] + mh[j]))));
   for (int j = 0; j < H; ++j) mh[j] = std::tanh(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);
-  for (int j = 0; j < H; ++j) out[j] = mx[j] * h[j] + (1.f - mx[j]) * mh[j];
+  for (int j = 0; j < H; ++j) out[j] = mx[j] * h[j] + (T(1) - mx[j]) * mh[j];
 }
 
-void gru_step_any(const Cell& c, const float* __restrict__ x, const float* __restrict__ h, float* __restrict__ out,
-                  float* __restrict__ mx, float* __restrict__ mh) {
+template <typename T>
+void gru_step_any(const Cell& c, const T* __restrict__ x, const T* __restrict__ h, T* __restrict__ out,
+                  T* __restrict__ mx, T* __restrict__ mh) {
   const int H3 = 3 * c.H, H = c.H;
   for (int j = 0; j < H3; ++j) {
     mx[j] = c.b[j];
     mh[j] = c.b[H3 + j];
   }
   for (int k = 0; k < c.din; ++k) {
-    const float xv = x[k];
+    const T xv = x[k];
     const float* __restrict__ w = c.W + (int64_t)k * H3;
     for (int j = 0; j < H3; ++j) mx[j] += xv * w[j];
   }
   for (int k = 0; k < H; ++k) {
-    const float hv = h[k];
+    const T hv = h[k];
     const float* __restrict__ u = c.U + (int64_t)k * H3;
     for (int j = 0; j < H3; ++j) mh[j] += hv * u[j];
   }
   // z | r; the argument is clamped to +-80 so that no exp overflows (-ffast-math assumes finite
   // values; sigmoid is saturated there: exp(-80) is below float32's resolution of 1)
-  for (int j = 0; j < 2 * H; ++j) mx[j] = 1.f / (1.f + std::exp(-std::min(80.f, std::max(-80.f, mx[j] + mh[j]))));
+  for (int j = 0; j < 2 * H; ++j) mx[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), mx[j] + mh[j]))));
   for (int j = 0; j < H; ++j) mh[j] = std::tanh(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);
-  for (int j = 0; j < H; ++j) out[j] = mx[j] * h[j] + (1.f - mx[j]) * mh[j];
+  for (int j = 0; j < H; ++j) out[j] = mx[j] * h[j] + (T(1) - mx[j]) * mh[j];
 }
 
-inline void gru_step(const Cell& c, const float* x, const float* h, float* out, float* mx, float* mh) {
-  if (c.din == 32 && c.H == 32) return gru_step_t<32, 32>(c, x, h, out);
-  if (c.din == 64 && c.H == 64) return gru_step_t<64, 64>(c, x, h, out);
-  if (c.din == 16 && c.H == 16) return gru_step_t<16, 16>(c, x, h, out);
-  gru_step_any(c, x, h, out, mx, mh);
+template <typename T>
+inline void gru_step(const Cell& c, const T* x, const T* h, T* out, T* mx, T* mh) {
+  if (c.din == 32 && c.H == 32) return gru_step_t<32, 32, T>(c, x, h, out);
+  if (c.din == 64 && c.H == 64) return gru_step_t<64, 64, T>(c, x, h, out);
+  if (c.din == 16 && c.H == 16) return gru_step_t<16, 16, T>(c, x, h, out);
+  gru_step_any<T>(c, x, h, out, mx, mh);
 }
 
 struct Graph {            // graph-local views of one graph of the batch
@@ -142,10 +147,11 @@ struct Model {
 };
 
 // The forward of one graph; par: parallelise over the destinations of each MP (one big graph)
+template <typename T>
 int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::string& msg) {
   const ign_plan_desc* p = m.p;
   const int E = p->num_entities;
-  std::vector<std::vector<float>> S(E), S2(E);
+  std::vector<std::vector<T>> S(E), S2(E);
   for (int e = 0; e < E; ++e) {
     const int H = p->entities[e].hidden_dim, F = p->entities[e].feature_total;
     S[e].assign(g.n[e] * H, 0.f);
@@ -219,18 +225,18 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
         }
         if (mxl < total) { msg = "sequence_mask(final_len) narrower than the padded sequence (AUX:785-790)"; return IGN_ERR_INVALID; }
       }
-      std::vector<float>& out_s = S2[dst];
-      out_s.assign(ND * H, 0.f);
+      std::vector<T>& out_s = S2[dst];
+      out_s.assign(ND * H, T(0));
       const int DIN = c.din;
-      auto run = [&](int64_t d, std::vector<float>& x, std::vector<float>& h, std::vector<float>& hn,
-                     std::vector<float>& mx, std::vector<float>& mh) {
-        const float* h0 = S[dst].data() + d * H;
+      auto run = [&](int64_t d, std::vector<T>& x, std::vector<T>& h, std::vector<T>& hn,
+                     std::vector<T>& mx, std::vector<T>& mh) {
+        const T* h0 = S[dst].data() + d * H;
         if (!sorted) {
-          std::fill(x.begin(), x.end(), 0.f);
+          std::fill(x.begin(), x.end(), T(0));
           for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
             const Msg& q = msgs[i];
             const int se = mp.sources[q.s].entity;
-            const float* v = S[se].data() + q.row * p->entities[se].hidden_dim;
+            const T* v = S[se].data() + q.row * p->entities[se].hidden_dim;
             for (int k = 0; k < DIN; ++k) x[k] += v[k];
           }
           gru_step(c, x.data(), h0, out_s.data() + d * H, mx.data(), mh.data());
@@ -238,7 +244,7 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
         }
         std::copy(h0, h0 + H, h.begin());
         for (int64_t t = 0; t < flen[d]; ++t) {
-          std::fill(x.begin(), x.end(), 0.f);
+          std::fill(x.begin(), x.end(), T(0));
           for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
             const Msg& q = msgs[i];
             if (q.pos != t) continue;
@@ -247,7 +253,7 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
             int col = 0;
             if (axis2)
               for (int s2 = 0; s2 < q.s; ++s2) col += p->entities[mp.sources[s2].entity].hidden_dim;
-            const float* v = S[se].data() + q.row * w;
+            const T* v = S[se].data() + q.row * w;
             for (int k = 0; k < w; ++k) x[col + k] += v[k];
           }
           gru_step(c, x.data(), h.data(), hn.data(), mx.data(), mh.data());
@@ -258,12 +264,12 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
       if (par) {
 #pragma omp parallel
         {
-          std::vector<float> x(DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
+          std::vector<T> x(DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
 #pragma omp for schedule(dynamic, 64)
           for (int64_t d = 0; d < ND; ++d) run(d, x, h, hn, mx, mh);
         }
       } else {
-        std::vector<float> x(DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
+        std::vector<T> x(DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
         for (int64_t d = 0; d < ND; ++d) run(d, x, h, hn, mx, mh);
       }
       std::swap(S[dst], S2[dst]);   // GM:602: the destination's state is overwritten
@@ -273,7 +279,7 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
   const int64_t R = g.n[p->readout_inputs[0]];
   int width = 0;
   for (int i = 0; i < p->num_readout_inputs; ++i) width += p->entities[p->readout_inputs[i]].hidden_dim;
-  std::vector<float> a(width), b2;
+  std::vector<T> a(width), b2;
   for (int64_t r = 0; r < R; ++r) {
     int col = 0;
     for (int i = 0; i < p->num_readout_inputs; ++i) {
@@ -281,23 +287,23 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
       std::copy(S[e].begin() + r * H, S[e].begin() + (r + 1) * H, a.begin() + col);
       col += H;
     }
-    std::vector<float> cur = a;
+    std::vector<T> cur = a;
     for (const auto& L : m.dense) {
-      b2.assign(L.out, 0.f);
+      b2.assign(L.out, T(0));
       for (int j0 = 0; j0 < L.out; j0 += 64) {   // 64 output columns at a time (register-resident)
         const int nj = std::min(64, L.out - j0);
-        float acc[64];
-        for (int j = 0; j < 64; ++j) acc[j] = j < nj && L.b ? L.b[j0 + j] : 0.f;
+        T acc[64];
+        for (int j = 0; j < 64; ++j) acc[j] = j < nj && L.b ? T(L.b[j0 + j]) : T(0);
         if (nj == 64) {
           for (int k = 0; k < L.in; ++k) {
-            const float v = cur[k];
+            const T v = cur[k];
             const float* __restrict__ w = L.W + (int64_t)k * L.out + j0;
 
             for (int j = 0; j < 64; ++j) acc[j] += v * w[j];
           }
         } else {
           for (int k = 0; k < L.in; ++k) {
-            const float v = cur[k];
+            const T v = cur[k];
             const float* w = L.W + (int64_t)k * L.out + j0;
             for (int j = 0; j < nj; ++j) acc[j] += v * w[j];
           }
@@ -306,7 +312,7 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
       }
       cur.swap(b2);
     }
-    std::copy(cur.begin(), cur.end(), out + r * (int64_t)cur.size());
+    for (size_t j = 0; j < cur.size(); ++j) out[r * (int64_t)cur.size() + j] = (float)cur[j];
   }
   return IGN_OK;
 }
@@ -319,8 +325,9 @@ const char* ign_oracle_last_error(void) { return g_err; }
 
 // params: the parameter tensors in MPPlan.param_specs order (Keras layout), n_params of them.
 // out: the predictions of every graph, concatenated (model_fn's flattened order, GM:712-724).
+// precision: 0 = float32 (TF's arithmetic on the CPU; the bench line), 1 = float64 (the checker)
 int ign_oracle_forward(const ign_plan_desc* p, const ign_batch_desc* d, const float* const* params, int32_t n_params,
-                       float* out, int32_t threads) {
+                       float* out, int32_t threads, int32_t precision) {
   if (!p || !d || !params || !out) return err(IGN_ERR_INVALID, "null argument");
   if (p->num_readout_ops) return err(IGN_ERR_UNSUPPORTED, "oracle: readout operations before predict are not restated in C++");
   if (p->num_readout_inputs < 1) return err(IGN_ERR_INVALID, "no predict inputs");
@@ -387,7 +394,8 @@ int ign_oracle_forward(const ign_plan_desc* p, const ign_batch_desc* d, const fl
 #pragma omp parallel for schedule(dynamic, 1)
     for (int g = 0; g < G; ++g) {
       std::string m2;
-      const int r = graph_forward(m, gs[g], out + out_off[g], false, m2);
+      const int r = precision ? graph_forward<double>(m, gs[g], out + out_off[g], false, m2)
+                              : graph_forward<float>(m, gs[g], out + out_off[g], false, m2);
       if (r) {
 #pragma omp critical
         {
@@ -397,7 +405,9 @@ int ign_oracle_forward(const ign_plan_desc* p, const ign_batch_desc* d, const fl
       }
     }
   } else {
-    for (int g = 0; g < G && !rc; ++g) rc = graph_forward(m, gs[g], out + out_off[g], true, msg);
+    for (int g = 0; g < G && !rc; ++g)
+      rc = precision ? graph_forward<double>(m, gs[g], out + out_off[g], true, msg)
+                     : graph_forward<float>(m, gs[g], out + out_off[g], true, msg);
   }
   if (rc) return err(rc, ("oracle: " + msg).c_str());
   return IGN_OK;

@@ -3,7 +3,7 @@ C++/OpenMP restatement in oracle/cpu_forward.cpp.  Nothing under ignnition_amd/ 
 
     python -m oracle.cpu_oracle        # build oracle/_build/libign_oracle.so (g++ -O3 -fopenmp)
 
-``cpu_forward(plan, graphs, params, threads)`` runs the float32 restatement of ComnetModel.call
+``cpu_forward(plan, graphs, params, threads, float64)`` runs the float32 (or float64) restatement of ComnetModel.call
 (GM:384-658) on the host for the lowered plan (ignnition_amd.engine.MPPlan) and a list of feature
 dicts or a BatchedGraphs, with the parameters by their Keras-style names."""
 import ctypes as C
@@ -42,7 +42,7 @@ def _load():
         lib = C.CDLL(LIB)
         lib.ign_oracle_forward.restype = C.c_int
         lib.ign_oracle_forward.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.c_void_p,
-                                           C.c_int32]
+                                           C.c_int32, C.c_int32]
         lib.ign_oracle_last_error.restype = C.c_char_p
         _lib = lib
     return _lib
@@ -52,7 +52,9 @@ class OracleError(RuntimeError):
     pass
 
 
-def cpu_forward(plan, graphs, params: dict, threads: int = 0) -> np.ndarray:
+def cpu_forward(plan, graphs, params: dict, threads: int = 0, float64: bool = False) -> np.ndarray:
+    """float64=False: float32 arithmetic (TF's on the CPU; bench.py's line); True: float64 (the
+    checker: float32 runs of this model differ from float64 by up to ~2e-4 on outliers)."""
     from ignnition_amd.engine import batch_desc
     lib = _load()
     pd, pkeep = plan.to_desc()
@@ -63,7 +65,8 @@ def cpu_forward(plan, graphs, params: dict, threads: int = 0) -> np.ndarray:
     e = plan.readout_inputs[0]
     units = plan.dense[-1][1]
     out = np.empty(int(num[:, e].sum()) * units, np.float32)
-    rc = lib.ign_oracle_forward(C.byref(pd), C.byref(bd), ptrs, len(arrs), out.ctypes.data, int(threads))
+    rc = lib.ign_oracle_forward(C.byref(pd), C.byref(bd), ptrs, len(arrs), out.ctypes.data, int(threads),
+                                int(bool(float64)))
     if rc:
         raise OracleError("%d: %s" % (rc, lib.ign_oracle_last_error().decode()))
     return out

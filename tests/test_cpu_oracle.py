@@ -1,6 +1,9 @@
-"""The C++/OpenMP restatement (oracle/cpu_forward.cpp, float32) against the float64 dense
-oracle (CPU): the models of the benchmark configurations and the concat / interleave variants,
-and the same run-time errors (K.rnn mask width, gather_nd(-1))."""
+"""The C++/OpenMP restatement (oracle/cpu_forward.cpp) against the float64 dense oracle (CPU):
+the models of the benchmark configurations and the concat / interleave variants, and the same
+run-time errors (K.rnn mask width, gather_nd(-1)).  Its float64 mode (the checker of the
+engine's full-size outputs) agrees to float32 output rounding; its float32 mode (bench.py's
+second CPU line) within plain float32 error of this model (the float32 dense oracle itself is
+up to ~2e-4 off float64 on outlier predictions of 64 synth50 graphs)."""
 import copy
 
 import numpy as np
@@ -12,7 +15,8 @@ from ignnition_amd.json_operations import Model_information
 from oracle import cpu_oracle
 from oracle.dense_forward import DenseOracle
 
-TOL = 1e-4   # float32 vs float64, scaled by max(1, |y|), as the engine's parity tolerance
+TOL64 = 1e-6   # float64 restatement, float32 outputs
+TOL32 = 5e-4   # float32 restatement (plain float32 arithmetic, see above)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -20,27 +24,32 @@ def _built():
     cpu_oracle.build()
 
 
-def _close(got, ref):
+def _close(got, ref, tol):
     err = np.abs(got.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))
-    assert got.shape == ref.shape and err.max() <= TOL, err.max()
+    assert got.shape == ref.shape and err.max() <= tol, err.max()
 
 
-def _run(desc, dims, graphs, seed=2, threads=4):
+def _check(desc, dims, graphs, seed=2, threads=4):
     plan = MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims))
     prm = plan.init_params(seed, bias_scale=0.1)
-    return cpu_oracle.cpu_forward(plan, graphs, prm, threads), DenseOracle(desc, dims, prm).forward(graphs)
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    got64 = cpu_oracle.cpu_forward(plan, graphs, prm, threads, float64=True)
+    got32 = cpu_oracle.cpu_forward(plan, graphs, prm, threads)
+    assert np.all(np.isfinite(got32)) and np.all(np.isfinite(got64))
+    _close(got64, ref, TOL64)
+    _close(got32, ref, TOL32)
 
 
 @pytest.mark.parametrize("kind,topo,n", [("routenet", "nsfnet", 3), ("qsize", "nsfnet", 2), ("routenet", "geant2", 2)])
 def test_examples_match_dense_oracle(kind, topo, n):
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs(kind, topo, n)
-    _close(*_run(desc, dims, graphs))
+    _check(desc, dims, graphs)
 
 
 @pytest.mark.parametrize("threads", [1, 3])
 def test_one_large_graph_parallel_over_destinations(threads):
     desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=2000, iterations=3, window=64)
-    _close(*_run(desc, dims, graphs, threads=threads))
+    _check(desc, dims, graphs, threads=threads)
 
 
 @pytest.mark.parametrize("axis", [1, 2])
@@ -49,7 +58,7 @@ def test_concat(axis):
     _, dims, _ = workloads.model("qsize")
     mi = Model_information(copy.deepcopy(desc), dims)
     graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet", g, qsize=True) for g in range(2)])
-    _close(*_run(desc, dims, graphs))
+    _check(desc, dims, graphs)
 
 
 def test_batch_is_per_graph():
@@ -85,6 +94,4 @@ def test_saturated_gates_stay_finite():
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
     big = [dict(g, traffic=np.asarray(g["traffic"], np.float32) * 400.0,
                 link_capacity=np.asarray(g["link_capacity"], np.float32) * 400.0) for g in graphs]
-    got, ref = _run(desc, dims, big, seed=5)
-    assert np.all(np.isfinite(got))
-    _close(got, ref)
+    _check(desc, dims, big, seed=5)
