@@ -99,9 +99,11 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_batch_enable_training", "ign_forward_train", "ign_backward", "ign_mse_loss", "ign_l2_loss",
            "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get", "ign_dataset_batch_create",
-           "ign_dataset_batch_get", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json"]
+           "ign_dataset_batch_get", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json", "ign_forward_train_begin", "ign_forward_train_mp",
+           "ign_forward_train_end", "ign_backward_begin", "ign_backward_mp", "ign_backward_end",
+           "ign_batch_train_buffers"]
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -164,6 +166,13 @@ def _load():
         "ign_dataset_batch_destroy": (None, [VP]),
         "ign_plan_create_json": (C.c_int, [C.c_char_p, C.c_char_p, i32, P(VP)]),
         "ign_plan_describe_json": (C.c_int, [VP, C.c_char_p, i64, P(i64)]),
+        "ign_forward_train_begin": (C.c_int, [VP, VP]),
+        "ign_forward_train_mp": (C.c_int, [VP, VP]),
+        "ign_forward_train_end": (C.c_int, [VP, VP, VP]),
+        "ign_backward_begin": (C.c_int, [VP, VP, VP, VP, f32]),
+        "ign_backward_mp": (C.c_int, [VP, VP]),
+        "ign_backward_end": (C.c_int, [VP, VP]),
+        "ign_batch_train_buffers": (C.c_int, [VP, i32, P(VP), P(VP)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

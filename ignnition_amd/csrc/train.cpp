@@ -81,6 +81,15 @@ struct TrainState {
   float* rties = nullptr;
   std::vector<int32_t*> rx_ptr, rx_idx;   // extend ops: per op 2 transposed CSRs (input row -> edges)
   bool forward_done = false;
+  // stepped forward / backward (ign_forward_train_begin .. _end, ign_backward_begin .. _end): the
+  // edge-cut driver exchanges halo rows between the steps
+  int f_it = 0, f_mi = 0;
+  bool f_open = false;
+  int b_ri = -1;
+  bool b_open = false;
+  hvec<int> dcur;                          // backward: current gradient buffer per entity
+  float* grads = nullptr;                  // backward: the caller's gradient vector
+  float l2_scale = 1.f;                    // backward: weight of the l2 terms (1/ranks under edge-cut)
   std::vector<void*> allocs;               // blocks of pool
   DevPool* pool = nullptr;                 // the batch's (outlives this state)
   hipStream_t stream = nullptr;            // the plan stream, for the release fence
@@ -203,7 +212,8 @@ int msg_net_backward(ign_plan* p, ign_batch* b, TrainState* t, const MPP& mp, co
   for (size_t q = 0; q < nn.inputs.size(); ++q) {
     const int w = nn.widths[q];
     if (nn.inputs[q] == IGN_MSG_HS_SOURCE)
-      HIP_TRY(launch_csr_gather_cols_add(dsrc, b->rows[mp.src[s].entity], mt.nsrc_ptr[s], mt.nsrc_idx[s], t->mdin,
+      HIP_TRY(launch_csr_gather_cols_add(dsrc, b->rows[mp.src[s].entity] + b->halo[mp.src[s].entity], mt.nsrc_ptr[s],
+                                         mt.nsrc_idx[s], t->mdin,
                                          nn.din, col, w, 1, st));
     else if (nn.inputs[q] == IGN_MSG_HS_DEST)
       HIP_TRY(launch_csr_gather_cols_add(ddst, b->rows[mp.dst], mt.ndst_ptr[s], mt.ndst_idx[s], t->mdin, nn.din,
@@ -224,8 +234,6 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   int rc = ensure_device(p);
   if (rc) return rc;
   const int E = (int)p->ents.size();
-  for (int e = 0; e < E; ++e)
-    if (b->halo[e]) return fail(IGN_ERR_UNSUPPORTED, "training on an edge-cut partition is not supported yet");
   for (size_t c = 0; c < p->cells.size(); ++c) {
     const CellP& cp = p->cells[c];
     if (!cp.used) continue;
@@ -245,7 +253,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   t->ver.resize(E);
   t->cur.assign(E, 0);
   for (int e = 0; e < E; ++e) {
-    const int64_t n = b->rows[e] * p->ents[e].hidden_dim;
+    const int64_t n = (b->rows[e] + b->halo[e]) * p->ents[e].hidden_dim;   // owned rows, then halo rows
     for (int v = 0; v < nver[e]; ++v) {
       float* f = nullptr;
       if ((rc = talloc(t.get(), &f, n))) return rc;
@@ -272,7 +280,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     std::vector<hvec<int32_t>> tptr, tidx;
     int64_t tkeys[IGN_MAX_SLOTS] = {0, 0, 0, 0};
     for (int s = 0; s < S; ++s)
-      tkeys[s] = mp.nn[s].layers.empty() ? b->rows[mp.src[s].entity] : mb.n_edges[s];
+      tkeys[s] = mp.nn[s].layers.empty() ? b->rows[mp.src[s].entity] + b->halo[mp.src[s].entity] : mb.n_edges[s];
     if (mb.sorted) {
       mt.hs_rows = mb.n_steps + mb.n_dst;
       for (int it = 0; it < p->T; ++it) {
@@ -394,7 +402,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         kd[e] = {ed[e], (int32_t)e};
       }
       hvec<int32_t> p1, i1, p2, i2;
-      build_csr(b->rows[se], ks, p1, i1);
+      build_csr(b->rows[se] + b->halo[se], ks, p1, i1);   // sources may be halo rows (edge-cut)
       build_csr(b->rows[mp.dst], kd, p2, i2);
       if ((rc = tupload(t.get(), &mt.nsrc_ptr[s], p1)) || (rc = tupload(t.get(), &mt.nsrc_idx[s], i1)) ||
           (rc = tupload(t.get(), &mt.ndst_ptr[s], p2)) || (rc = tupload(t.get(), &mt.ndst_idx[s], i2)))
@@ -476,20 +484,32 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   return IGN_OK;
 }
 
-int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
+int ign_forward_train_begin(ign_plan* p, ign_batch* b) {
   int rc = check_train(p, b);
   if (rc) return rc;
   TrainState* t = b->train;
   hipStream_t st = p->stream;
   const int E = (int)p->ents.size();
-  for (int e = 0; e < E; ++e) {   // GM:396-400
+  for (int e = 0; e < E; ++e) {   // GM:396-400 (owned rows; an edge-cut driver fills the halo rows)
     HIP_TRY(launch_init_state(t->ver[e][0], b->d_feat[e], b->rows[e], p->ents[e].hidden_dim,
                               p->ents[e].feature_total, st));
     t->cur[e] = 0;
   }
   t->recs.clear();
-  for (int it = 0; it < p->T; ++it) {
-    for (int mi = 0; mi < (int)p->mps.size(); ++mi) {
+  t->f_it = t->f_mi = 0;
+  t->f_open = true;
+  t->forward_done = false;
+  return IGN_OK;
+}
+
+int ign_forward_train_mp(ign_plan* p, ign_batch* b) {
+  int rc = check_train(p, b);
+  if (rc) return rc;
+  TrainState* t = b->train;
+  if (!t->f_open || t->f_it >= p->T) return fail(IGN_ERR_INVALID, "ign_forward_train_mp outside begin .. end");
+  hipStream_t st = p->stream;
+  const int it = t->f_it, mi = t->f_mi;
+  {
       const MPP& mp = p->mps[mi];
       const MPB& mb = b->mp[mi];
       const CellP& cp = p->cells[mp.cell];
@@ -539,8 +559,22 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
       }
       t->cur[mp.dst] = rec.v_in + 1;
       t->recs.push_back(rec);
-    }
   }
+  if (++t->f_mi == (int)p->mps.size()) {
+    t->f_mi = 0;
+    ++t->f_it;
+  }
+  return IGN_OK;
+}
+
+int ign_forward_train_end(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = check_train(p, b);
+  if (rc) return rc;
+  TrainState* t = b->train;
+  if (!t->f_open || t->f_it != p->T) return fail(IGN_ERR_INVALID, "ign_forward_train_end before every MP ran");
+  t->f_open = false;
+  hipStream_t st = p->stream;
+  const int E = (int)p->ents.size();
   // readout operations, then the predict stack with every activation kept (GM:605-629)
   std::vector<const float*> ent(E);
   for (int e = 0; e < E; ++e) ent[e] = t->ver[e][t->cur[e]];
@@ -578,7 +612,13 @@ int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
   return IGN_OK;
 }
 
-int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
+int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
+  int rc = ign_forward_train_begin(p, b);
+  for (int k = 0; !rc && k < p->T * (int)p->mps.size(); ++k) rc = ign_forward_train_mp(p, b);
+  return rc ? rc : ign_forward_train_end(p, b, pred_out);
+}
+
+int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* grads, float l2_scale) {
   int rc = check_train(p, b);
   if (rc) return rc;
   if (!dpred || !grads) return fail(IGN_ERR_INVALID, "null argument");
@@ -589,9 +629,11 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
   const int64_t P = b->n_pred;
   set_tsgemm_bf(p->tsgemm_bf);
   HIP_TRY(hipMemsetAsync(grads, 0, p->n_params * sizeof(float), st));
-  hvec<int> dcur(E, 0);
-  for (int e = 0; e < E; ++e)
-    HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, b->rows[e] * p->ents[e].hidden_dim * sizeof(float), st));
+  t->grads = grads;
+  t->l2_scale = l2_scale;
+  t->dcur.assign(E, 0);
+  for (int e = 0; e < E; ++e)   // owned and halo rows (edge-cut: peers' gradients arrive in the owned rows)
+    HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, (b->rows[e] + b->halo[e]) * p->ents[e].hidden_dim * sizeof(float), st));
 
   // ---- readout (GM:605-629) in reverse: predict, then the operations before it
   for (size_t id = 0; id < t->dT.size(); ++id)
@@ -608,7 +650,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     const float* A = l == 0 ? X : t->act[l - 1];
     HIP_TRY(launch_tsgemm_add(A, d.in, t->dz[zi], d.out, P, d.in, d.out, t->part, grads + d.off_w,
                               d.use_bias ? grads + d.off_b : nullptr, st));
-    if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)d.in * d.out, st));
+    if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * l2_scale, (int64_t)d.in * d.out, st));
     float* out;
     int act = -1, acc = 0;
     const float* aprev = nullptr;
@@ -655,7 +697,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
           const float* A = l > 0 ? bo.tmp[l - 1] : op.in.size() > 1 ? bo.cat : tensor(op.in[0]);
           HIP_TRY(launch_tsgemm_add(A, K, t->rz[rz], d.out, n, K, d.out, t->part, grads + d.off_w,
                                     d.use_bias ? grads + d.off_b : nullptr, st));
-          if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)K * d.out, st));
+          if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * l2_scale, (int64_t)K * d.out, st));
           if (l > 0) {
             HIP_TRY(launch_row_gemm_t_generic(t->rz[rz], n, d.out, p->d_params + d.off_w, K, t->rz[1 - rz], 0,
                                               op.layers[l - 1].act, bo.tmp[l - 1], st));
@@ -700,9 +742,21 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
       }
     }
   }
+  t->b_ri = (int)t->recs.size() - 1;
+  t->b_open = true;
+  return IGN_OK;
+}
 
-  // ---- MP instances in reverse (GM:404-603)
-  for (int ri = (int)t->recs.size() - 1; ri >= 0; --ri) {
+int ign_backward_mp(ign_plan* p, ign_batch* b) {
+  int rc = check_train(p, b);
+  if (rc) return rc;
+  TrainState* t = b->train;
+  if (!t->b_open || t->b_ri < 0) return fail(IGN_ERR_INVALID, "ign_backward_mp outside begin .. end");
+  hipStream_t st = p->stream;
+  hvec<int>& dcur = t->dcur;
+  float* grads = t->grads;
+  const int ri = t->b_ri--;
+  {
     const MPRec& rec = t->recs[ri];
     const MPP& mp = p->mps[rec.mi];
     const MPB& mb = b->mp[rec.mi];
@@ -711,6 +765,8 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     const int dst = mp.dst, H = cp.H, DIN = mp.din, H3 = 3 * cp.H;
     float* dh_in = t->dS[dcur[dst]][dst];
     float* dh_out = t->dS[1 - dcur[dst]][dst];
+    if (b->halo[dst])   // a self-loop MP's source gradient lands in dh_out's halo rows too
+      HIP_TRY(hipMemsetAsync(dh_out + b->rows[dst] * H, 0, b->halo[dst] * H * sizeof(float), st));
     const float* srcs[IGN_MAX_SLOTS] = {nullptr, nullptr, nullptr, nullptr};
     for (size_t s = 0; s < mp.src.size(); ++s) srcs[s] = t->ver[mp.src[s].entity][rec.src_v[s]];
     for (size_t s = 0; s < mp.src.size(); ++s) {   // recompute this instance's message networks
@@ -801,7 +857,7 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
                                       p->d_params + p->off_att, p->attn_F, grads + p->off_k1, grads + p->off_k2,
                                       grads + p->off_att, st));
         dcur[dst] = 1 - dcur[dst];
-        continue;
+        return IGN_OK;
       }
       const float* dmsgs = t->dx;   // gradient of the aggregated messages, by destination row
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
@@ -822,14 +878,40 @@ int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
     }
     dcur[dst] = 1 - dcur[dst];
   }
+  return IGN_OK;
+}
+
+int ign_backward_end(ign_plan* p, ign_batch* b) {
+  int rc = check_train(p, b);
+  if (rc) return rc;
+  TrainState* t = b->train;
+  if (!t->b_open || t->b_ri >= 0) return fail(IGN_ERR_INVALID, "ign_backward_end before every MP instance ran");
+  t->b_open = false;
+  hipStream_t st = p->stream;
+  float* grads = t->grads;
   for (auto& mp : p->mps)   // message-network l2 terms (AUX:833-834), once per step
     for (auto& nn : mp.nn)
       for (size_t l = 0; l < nn.layers.size(); ++l) {
         const DenseP& d = nn.layers[l];
         const int K = l == 0 ? nn.din : nn.layers[l - 1].out;
-        if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2, (int64_t)K * d.out, st));
+        if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * t->l2_scale, (int64_t)K * d.out, st));
       }
   return IGN_OK;
+}
+
+int ign_batch_train_buffers(const ign_batch* b, int32_t e, float** state, float** grad) {
+  if (!b || !b->train) return fail(IGN_ERR_INVALID, "training not enabled on this batch");
+  const TrainState* t = b->train;
+  if (e < 0 || e >= (int)t->ver.size()) return fail(IGN_ERR_INVALID, "entity %d out of range", e);
+  if (state) *state = t->ver[e][t->cur[e]];
+  if (grad) *grad = t->dS[t->dcur.empty() ? 0 : t->dcur[e]][e];
+  return IGN_OK;
+}
+
+int ign_backward(ign_plan* p, ign_batch* b, const float* dpred, float* grads) {
+  int rc = ign_backward_begin(p, b, dpred, grads, 1.f);
+  while (!rc && b->train->b_ri >= 0) rc = ign_backward_mp(p, b);
+  return rc ? rc : ign_backward_end(p, b);
 }
 
 int ign_mse_loss(ign_plan* p, const float* pred, const float* labels, int64_t n, float* dpred, double* loss) {

@@ -635,6 +635,35 @@ class Batch:
                                     out.ctypes.data_as(C.c_void_p) if to_host else None))
         return out
 
+    # stepped training step (edge-cut partitions: partition.EdgeCutTraining exchanges between steps)
+    def forward_train_begin(self):
+        check(lib.ign_forward_train_begin(self.engine.handle, self.handle))
+
+    def forward_train_mp(self):
+        check(lib.ign_forward_train_mp(self.engine.handle, self.handle))
+
+    def forward_train_end(self, to_host: bool = True):
+        out = np.empty((self.predictions, self.output_units), np.float32) if to_host else None
+        check(lib.ign_forward_train_end(self.engine.handle, self.handle,
+                                        out.ctypes.data_as(C.c_void_p) if to_host else None))
+        return out
+
+    def backward_begin(self, dpred, grads, l2_scale: float = 1.0):
+        check(lib.ign_backward_begin(self.engine.handle, self.handle, _ptr(dpred), _ptr(grads), float(l2_scale)))
+
+    def backward_mp(self):
+        check(lib.ign_backward_mp(self.engine.handle, self.handle))
+
+    def backward_end(self):
+        check(lib.ign_backward_end(self.engine.handle, self.handle))
+
+    def train_buffers(self, entity: str):
+        """(state, gradient) device pointers of the entity's current version, [rows + halo][H]."""
+        st, gr = C.c_void_p(), C.c_void_p()
+        check(lib.ign_batch_train_buffers(self.handle, self.engine.plan.entities.index(entity), C.byref(st),
+                                          C.byref(gr)))
+        return st.value, gr.value
+
     def predictions_ptr(self) -> int:
         p = C.c_void_p()
         check(lib.ign_batch_predictions(self.handle, C.byref(p)))

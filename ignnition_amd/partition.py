@@ -294,3 +294,159 @@ class EdgeCutForward:
     def close(self):
         for b in self.batches:
             b.close()
+
+
+# ---------------------------------------------------------------------------------------------
+class _DeviceRows:
+    """A device buffer the engine owns, seen by torch without a copy (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, rows: int, cols: int):
+        self.__cuda_array_interface__ = {"shape": (rows, cols), "typestr": "<f4", "data": (int(ptr), False),
+                                         "version": 2, "strides": None}
+
+
+class EdgeCutTraining:
+    """One training step (model_fn TRAIN, GM:697-830) on a partitioned graph, through the stepped
+    C ABI (ign_forward_train_* / ign_backward_*).
+
+    Forward: every state version keeps owned + halo rows; before an MP reads an entity whose halo
+    rows are stale, the owners send them (as EdgeCutForward does, into the version's halo rows).
+    Backward: the gradient of a halo row belongs to its owner -- after each MP instance, the halo
+    rows of every source entity's current gradient go back to their owners (the reverse all-to-all),
+    who add them to their rows (peer by peer: deterministic), and are zeroed.  The loss is the MSE
+    over every rank's predictions, the parameter gradients are summed over ranks (each rank's l2
+    terms weighted 1/ranks), so one step equals the whole graph's step up to summation order."""
+
+    def __init__(self, engine: Engine, parts: list, comm):
+        import torch
+        self.torch = torch
+        self.engine, self.parts, self.comm = engine, parts, comm
+        plan = engine.plan
+        self.plan = plan
+        for m in plan.mps:
+            if m["aggr"] not in ("sum", "convolution"):
+                raise ValueError("edge-cut training supports sum and convolution MPs")
+        engine.set_stream(torch.cuda.current_stream().cuda_stream)
+        srcs = {s.src for s in plan.adj_slots}
+        self.halo_ents = [n for n in plan.entities if n in srcs] if comm.world > 1 else []
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.batches, self.send_idx, self.recv_idx = [], [], []
+        for p in parts:
+            b = Batch(engine, [p.inputs], halo_rows={n: p.halos[n].n_halo for n in plan.entities})
+            b.enable_training()
+            self.batches.append(b)
+            sidx, ridx = {}, {}
+            for n in self.halo_ents:
+                h = p.halos[n]
+                sidx[n] = torch.from_numpy(np.ascontiguousarray(h.send_rows, np.int64)).to(self.dev)
+                offs = np.cumsum([0] + list(h.send_counts))
+                ridx[n] = [(int(offs[q]), int(offs[q + 1])) for q in range(len(h.send_counts))]
+            self.send_idx.append(sidx)
+            self.recv_idx.append(ridx)
+        self.mp_sources = [sorted({plan.entities[s[0]] for s in m["sources"]}) for m in plan.mps]
+        self.grads = [torch.zeros(engine.n_params, dtype=torch.float32, device=self.dev) for _ in parts]
+
+    def _rows(self, i, name, ptr):
+        h = self.parts[i].halos[name]
+        H = self.plan.hidden[self.plan.entities.index(name)]
+        return self.torch.as_tensor(_DeviceRows(ptr, h.n_owned + h.n_halo, H), device=self.dev)
+
+    def _exchange_states(self, name):
+        sends, recvs, sc, rc = [], [], [], []
+        for i, p in enumerate(self.parts):
+            h = p.halos[name]
+            state = self._rows(i, name, self.batches[i].train_buffers(name)[0])
+            sends.append(state.index_select(0, self.send_idx[i][name]).contiguous())
+            recvs.append(state[h.n_owned:])
+            sc.append(h.send_counts)
+            rc.append(h.recv_counts)
+        self.comm.exchange(sends, sc, recvs, rc, False).wait()
+
+    def _return_gradients(self, name):
+        """Halo rows' gradients back to their owners, added there, zeroed here."""
+        torch = self.torch
+        grads, sends, recvs, sc, rc = [], [], [], [], []
+        for i, p in enumerate(self.parts):
+            h = p.halos[name]
+            g = self._rows(i, name, self.batches[i].train_buffers(name)[1])
+            grads.append(g)
+            sends.append(g[h.n_owned:].contiguous())
+            recvs.append(torch.empty((len(h.send_rows), g.shape[1]), dtype=torch.float32, device=self.dev))
+            sc.append(h.recv_counts)      # what this rank received from each peer goes back to it
+            rc.append(h.send_counts)
+        self.comm.exchange(sends, sc, recvs, rc, False).wait()
+        for i, p in enumerate(self.parts):
+            h = p.halos[name]
+            for q, (a, b) in enumerate(self.recv_idx[i][name]):   # peer by peer: unique rows, fixed order
+                if b > a:
+                    grads[i].index_add_(0, self.send_idx[i][name][a:b], recvs[i][a:b])
+            grads[i][h.n_owned:].zero_()
+
+    def step(self, labels: list):
+        """Forward + loss + backward; ``labels``: per partition, its owned predictions' labels.
+        Returns (loss over all ranks, summed parameter gradient, per-partition predictions)."""
+        torch = self.torch
+        plan, M = self.plan, len(self.plan.mps)
+        for b in self.batches:
+            b.forward_train_begin()
+        stale = set(self.halo_ents)
+        for _ in range(plan.iterations):                      # GM:406
+            for mi, m in enumerate(plan.mps):
+                for n in [n for n in self.mp_sources[mi] if n in stale]:
+                    self._exchange_states(n)
+                    stale.discard(n)
+                for b in self.batches:
+                    b.forward_train_mp()
+                dst = plan.entities[m["dst"]]
+                if dst in self.halo_ents:
+                    stale.add(dst)
+        preds = [b.forward_train_end(to_host=True) for b in self.batches]
+        ys = [torch.from_numpy(np.ascontiguousarray(np.asarray(l, np.float32).reshape(-1))).to(self.dev)
+              for l in labels]
+        n_local = sum(int(y.numel()) for y in ys)
+        n_total = self._sum_scalar(float(n_local))
+        loss = 0.0
+        dpreds = []
+        for b, y in zip(self.batches, ys):
+            d = torch.empty_like(y)
+            loss += self.engine.mse_loss(b.predictions_ptr(), y, d) * y.numel() / n_total
+            dpreds.append(d * (y.numel() / n_total))   # d(mean over every rank) = d(local mean) n_local / N
+        loss = self._sum_scalar(loss)
+        world = self.comm.world
+        for b, d, g in zip(self.batches, dpreds, self.grads):
+            b.backward_begin(d, g, 1.0 / world)
+        for k in range(plan.iterations * M - 1, -1, -1):      # MP instances in reverse
+            for b in self.batches:
+                b.backward_mp()
+            for n in self.mp_sources[k % M]:
+                if n in self.halo_ents:
+                    self._return_gradients(n)
+        for b in self.batches:
+            b.backward_end()
+        total = self.grads[0].clone()
+        for g in self.grads[1:]:
+            total += g
+        total = self._sum_tensor(total)
+        return loss, total, preds
+
+    def _sum_scalar(self, v: float) -> float:
+        if isinstance(self.comm, LoopbackComm):
+            return v
+        dev = "cpu" if self.comm.host_staged else self.dev
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=dev)
+        self.comm.dist.all_reduce(t, group=self.comm.group)
+        return float(t.item())
+
+    def _sum_tensor(self, g):
+        if isinstance(self.comm, LoopbackComm):
+            return g
+        if self.comm.host_staged:
+            h = g.cpu()
+            self.comm.dist.all_reduce(h, group=self.comm.group)
+            return h.to(g.device)
+        self.comm.dist.all_reduce(g, group=self.comm.group)
+        return g
+
+    def close(self):
+        for b in self.batches:
+            b.close()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 8
+#define IGN_ABI_VERSION 9
 
 enum ign_status {
   IGN_OK = 0,
@@ -290,6 +290,24 @@ int  ign_batch_enable_training(ign_plan* plan, ign_batch* batch);
 int  ign_forward_train(ign_plan* plan, ign_batch* batch, float* pred_out);
 /* grads[n_params] = dLoss/dparams for dLoss/dpredictions = dpred[predictions * output_units] */
 int  ign_backward(ign_plan* plan, ign_batch* batch, const float* dpred, float* grads);
+/* The same two calls in steps, for a training step on an edge-cut partition (ABI 9): the caller
+ * exchanges halo rows between the steps (ignnition_amd/partition.py EdgeCutTraining).
+ *   ign_forward_train_begin; then T x num_mps times ign_forward_train_mp (MP instances in order:
+ *   before one, the current version of each source entity must hold its peers' halo rows);
+ *   ign_forward_train_end (readout, predictions).
+ *   ign_backward_begin (readout backward; l2_scale weights the kernel_regularizer terms, e.g.
+ *   1/ranks when the ranks' gradients are summed); then ign_backward_mp once per MP instance
+ *   (reverse order: after one, the halo rows of each source entity's current gradient hold
+ *   gradient for peers' rows: send them to their owners, add, zero them); ign_backward_end.
+ * ign_batch_train_buffers: the current state version and gradient buffer of an entity,
+ * [owned rows | halo rows][hidden] each. */
+int  ign_forward_train_begin(ign_plan* plan, ign_batch* batch);
+int  ign_forward_train_mp(ign_plan* plan, ign_batch* batch);
+int  ign_forward_train_end(ign_plan* plan, ign_batch* batch, float* pred_out);
+int  ign_backward_begin(ign_plan* plan, ign_batch* batch, const float* dpred, float* grads, float l2_scale);
+int  ign_backward_mp(ign_plan* plan, ign_batch* batch);
+int  ign_backward_end(ign_plan* plan, ign_batch* batch);
+int  ign_batch_train_buffers(const ign_batch* batch, int32_t entity, float** state, float** grad);
 /* MeanSquaredError: loss = mean((pred - labels)^2) (host, may be NULL), dpred = 2 (pred - labels) / n */
 int  ign_mse_loss(ign_plan* plan, const float* pred, const float* labels, int64_t n, float* dpred, double* loss);
 /* sum over Dense layers of l2 * sum(W^2) for the current parameters (the regularization loss) */

@@ -129,3 +129,47 @@ def test_attention_partition_rejected():
     plan = MPPlan.from_model_info(Model_information(copy.deepcopy(d), dims))
     with pytest.raises(ValueError, match="attention"):
         partition.local_part(graphs[0], plan, 0, 2)
+
+
+@pytest.mark.parametrize("variant,world", [("sum", 2), ("sum", 3), ("msgnet", 2), ("convolution", 2)])
+def test_partitioned_training_step_equals_whole(variant, world):
+    """One training step on edge-cut partitions (partition.EdgeCutTraining: halo rows of every
+    state version from their owners before each MP, halo-row gradients back to their owners after
+    each MP instance, gradients summed over ranks): the predictions equal the whole graph's bit for
+    bit, the loss and the parameter gradient agree to float32 summation order."""
+    if device_count() == 0:
+        pytest.fail("no GPU visible")
+    base, dims, _, graphs, labels = workloads.make_synthetic_inputs(n_nodes=2500, hidden=32, iterations=2, window=96)
+    desc = base if variant == "sum" else _variant(base, variant)
+    plan = MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims))
+    prm = plan.init_params(12, bias_scale=0.1)
+    eng = Engine(plan, 0)
+    eng.set_params(prm)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    b = Batch(eng, graphs)
+    b.enable_training()
+    pred = b.forward_train().reshape(-1)
+    y = torch.from_numpy(np.asarray(labels[0], np.float32).reshape(-1)).cuda()
+    dpred = torch.empty_like(y)
+    loss = eng.mse_loss(b.predictions_ptr(), y, dpred)
+    g_whole = torch.zeros(eng.n_params, dtype=torch.float32, device="cuda")
+    b.backward(dpred, g_whole)
+    torch.cuda.synchronize()
+    b.close()
+    x = graphs[0]
+    parts = [partition.local_part(x, plan, r, world) for r in range(world)]
+    comm = partition.LoopbackComm(world)
+    partition.exchange_requests(parts, comm)
+    ranges = parts[0].ranges["node"]
+    lab = np.asarray(labels[0], np.float32).reshape(-1)
+    tr = partition.EdgeCutTraining(eng, parts, comm)
+    try:
+        loss_p, g_p, preds = tr.step([lab[ranges[r]:ranges[r + 1]] for r in range(world)])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(np.concatenate([p.reshape(-1) for p in preds]), pred)
+        assert loss_p == pytest.approx(loss, rel=1e-6)
+        gw, gp = g_whole.double(), g_p.double()
+        assert float(torch.linalg.norm(gp - gw)) <= 1e-5 * float(torch.linalg.norm(gw))
+    finally:
+        tr.close()
+        torch.cuda.synchronize()
