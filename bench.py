@@ -247,11 +247,27 @@ def main():
             comm = partition.TorchComm(dist, None, host_staged=True)
         part = partition.local_part(graphs[0], plan, rank, world)
         partition.exchange_requests([part], comm)
-        fw = partition.EdgeCutForward(eng, [part], comm)
-        step = lambda: fw.forward(to_host=False)
-        edges = fw.edges_per_forward
-        gru_steps = fw.batches[0].gru_steps_per_forward
         halo_rows = part.halos[plan.entities[0]].n_halo
+        if args.train:   # one optimizer step of the partitioned graph (halo states / gradients exchanged)
+            tr = partition.EdgeCutTraining(eng, [part], comm)
+            r = part.ranges[plan.entities[0]]
+            lab = np.asarray(labels[0], np.float32).reshape(-1)[r[rank]:r[rank + 1]]
+            m_state = torch.zeros(eng.n_params, dtype=torch.float32, device=tr.dev)
+            v_state = torch.zeros_like(m_state)
+            it_box = [0]
+
+            def step():
+                _, g, _ = tr.step([lab], to_host=False)
+                eng.adam_step(g, m_state, v_state, it_box[0], 1e-3)
+                it_box[0] += 1
+            edges = tr.batches[0].edges_per_forward
+            gru_steps = tr.batches[0].gru_steps_per_forward
+            cleanup.append(tr.close)
+        else:
+            fw = partition.EdgeCutForward(eng, [part], comm)
+            step = lambda: fw.forward(to_host=False)
+            edges = fw.edges_per_forward
+            gru_steps = fw.batches[0].gru_steps_per_forward
     elif args.train and args.fresh_batches:
         # the real input pipeline: write the rank's graphs as a tar.gz dataset in the reference
         # layout, then every step reads a new shuffled batch through the native reader
