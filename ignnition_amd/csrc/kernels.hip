@@ -36,6 +36,23 @@ __global__ void init_state_kernel(float* __restrict__ state, const float* __rest
   }
 }
 
+// The same with one float4 per thread and the row width a compile-time constant (H = 4 HQ): no
+// 64-bit division per element, 16-B stores.
+template <int HQ>
+__global__ void init_state4_kernel(f4* __restrict__ state, const float* __restrict__ feats, int64_t n, int F) {
+  const int64_t total = n * HQ;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / HQ;
+    const int c = 4 * (int)(i - row * HQ);
+    f4 v = f4{0, 0, 0, 0};
+    if (c < F && feats) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = c + q < F ? feats[row * F + c + q] : 0.0f;
+    }
+    state[i] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // GRU weight packing.  Keras GRUCell v2 layout: kernel [DIN][3H], recurrent_kernel [H][3H],
 // bias [2][3H]; gate column order z, r, h (AUX:748-749).
@@ -846,6 +863,14 @@ static inline int grid_for(int64_t n, int per_block) { return (int)((n + per_blo
 
 hipError_t launch_init_state(float* state, const float* feats, int64_t n, int H, int F, hipStream_t st) {
   int64_t total = n * (int64_t)H;
+  if ((H == 16 || H == 32 || H == 64) && (reinterpret_cast<uintptr_t>(state) & 15) == 0) {
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total / 4 + 255) / 256, 16384));
+    f4* s4 = reinterpret_cast<f4*>(state);
+    if (H == 16) hipLaunchKernelGGL(init_state4_kernel<4>, dim3(blocks), dim3(256), 0, st, s4, feats, n, F);
+    else if (H == 32) hipLaunchKernelGGL(init_state4_kernel<8>, dim3(blocks), dim3(256), 0, st, s4, feats, n, F);
+    else hipLaunchKernelGGL(init_state4_kernel<16>, dim3(blocks), dim3(256), 0, st, s4, feats, n, F);
+    return hipGetLastError();
+  }
   int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(init_state_kernel, dim3(blocks), dim3(256), 0, st, state, feats, n, H, F);
