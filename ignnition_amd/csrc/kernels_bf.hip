@@ -692,6 +692,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
   constexpr int NCH = U2 / CT;
   constexpr bool W1_LDS = W1L;   // W1 pieces in LDS (DIN 32) or read from L2 per wave
   constexpr int W1F = W1_LDS ? U1 * KS1 * 3 * 64 : 1;
+  static_assert(CT == 1 && CHF % NTH == 0, "chunk layout: one 16-unit tile, whole 1 KB pieces per wave");
   __shared__ bf8 sw2[2][CHF];
   __shared__ bf8 sw1[W1F];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -762,38 +763,58 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
       w3[c] = ld4(a.w3 + 16 * (CT * v + c) + 4 * g);
     }
     const int nv = (v + 1) % NCH;
-    constexpr int PER = (CHF + NTH - 1) / NTH;
-    u4v stage[PER];
+    // chunk v+1 goes straight into the other buffer by LDS-DMA (its readers passed the previous
+    // barrier).  Issued as asm: the compiler cannot tell the DMA's target from the buffer read
+    // below and would hold every ds_read of this chunk behind vmcnt(0), i.e. behind the DMA.  M0
+    // (the DMA's LDS base) has no other user in this kernel (checked in the ISA).
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = tid + NTH * k;
-      if (CHF % NTH == 0 || i < CHF) stage[k] = W2v[(int64_t)nv * CHF + i];   // (no branch when it divides)
+    for (int k = 0; k < CHF / NTH; ++k) {
+      const int piece = wave + WAVES * k;   // 1 KB pieces, one per wave and k
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(sw2[cur ^ 1] + piece * 64));
+      const u4v* src = W2v + (int64_t)nv * CHF + piece * 64 + lane;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // M0 is reserved: see above and tests/test_isa.py
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+#pragma clang diagnostic pop
     }
     __builtin_amdgcn_sched_barrier(0);
     // opaque lane offset: the LDS reads must not be hoisted out of the chunk loop (registers)
     int lofs = lane;
     asm volatile("" : "+v"(lofs));
-    f4 acc[CT][RT];
+    const bf8* wbase = sw2[cur] + lofs;
+    f4 acc[RT];
 #pragma unroll
-    for (int c = 0; c < CT; ++c)
+    for (int t = 0; t < RT; ++t) acc[t] = b[0];
+    // the three weight pieces of k-step s+1 are read while k-step s's MFMAs run
+    bf8 wn[3];
 #pragma unroll
-      for (int t = 0; t < RT; ++t) acc[c][t] = b[c];
+    for (int pu = 0; pu < 3; ++pu) wn[pu] = wbase[pu * 64];
 #pragma unroll
-    for (int s = 0; s < KS2; ++s)
+    for (int s = 0; s < KS2; ++s) {
+      bf8 w[3];
 #pragma unroll
-      for (int c = 0; c < CT; ++c)
-        split_mfma_rt<PASSES, RT, KS2>(sw2[cur] + (c * KS2 + s) * 3 * 64 + lofs, 64, hf, s, acc[c]);
+      for (int pu = 0; pu < 3; ++pu) w[pu] = wn[pu];
+      if (s + 1 < KS2) {
 #pragma unroll
-    for (int c = 0; c < CT; ++c)
+        for (int pu = 0; pu < 3; ++pu) wn[pu] = wbase[((s + 1) * 3 + pu) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < RT; ++t)
+      for (int pu = 2; pu >= 0; --pu)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) y[t] += w3[c][q] * act_t<ACT>(acc[c][t][q]);
+        for (int ph = 2; ph >= 0; --ph) {
+          if (PASSES == 6 && pu + ph > 2) continue;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = tid + NTH * k;
-      if (CHF % NTH == 0 || i < CHF) reinterpret_cast<u4v*>(sw2[cur ^ 1])[i] = stage[k];
+          for (int t = 0; t < RT; ++t) acc[t] = MFMA_BF(w[pu], hf[t][s][ph], acc[t]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[t] += w3[0][q] * act_t<ACT>(acc[t][q]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed (for every wave: barrier)
     __syncthreads();
   }
 #pragma unroll
@@ -967,6 +988,8 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   // blocks, 1.18 ms with 32-unit W2 chunks, 1.39-1.41 ms with 4-wave blocks (512 x synth50, round 1)
   // persistent blocks (W1 staged once per block, W2 chunk 0 carried over): 3.54-3.56 vs 3.58-3.59
   // ms/step on one box (tools/ab_env.sh, round 2)
+  // W2 chunks by LDS-DMA + weight pieces read one k-step ahead: 1.025-1.031 vs 1.079-1.109 ms per
+  // launch, 3.51 vs 3.58-3.59 ms/step (same box, round 2)
   if (din == 32)
     return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
   // DIN 64 (the 1M-node graph): W1's pieces (96 KB) in LDS beside the W2 double buffer (48 KB),

@@ -1,0 +1,54 @@
+"""ISA checks of the readout kernel (CPU: hipcc cross-compiles gfx950 to assembly, no GPU).
+
+readout_bf_kernel issues its W2-chunk LDS-DMA as inline asm that loads M0, a register the compiler
+reserves (csrc/kernels_bf.hip): that is only sound while nothing else in the kernel uses M0.  The
+default DIN-32 instance must also stay free of register spills (its chunk loop runs at 254 VGPRs)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+HIPCC = "/opt/rocm/bin/hipcc"
+SRC = os.path.join(os.path.dirname(__file__), "..", "ignnition_amd", "csrc", "kernels_bf.hip")
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "kernels_bf.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", "-amdgpu-mfma-vgpr-form",
+                    "--cuda-device-only", "-S", "-I", os.path.dirname(SRC), SRC, "-o", str(out)],
+                   check=True, capture_output=True, timeout=600)
+    return out.read_text()
+
+
+def _functions(asm, pattern):
+    for name in re.findall(r"^(%s\w*):" % pattern, asm, re.M):
+        i = asm.index("\n" + name + ":")
+        j = asm.index(".Lfunc_end", i)
+        yield name, asm[i:j], asm[j:j + 4000]
+
+
+def test_readout_m0_only_feeds_the_lds_dma(asm):
+    seen = 0
+    for name, body, _ in _functions(asm, "_Z17readout_bf_kernel"):
+        lines = [l.strip() for l in body.splitlines() if l.startswith("\t") and not l.strip().startswith((";", "."))]
+        for k, l in enumerate(lines):
+            if "m0" not in l:
+                continue
+            assert re.match(r"s_mov_b32 m0, s\d+$", l), (name, l)
+            nxt = next(x for x in lines[k + 1:] if not x.startswith("s_nop"))
+            assert nxt.startswith("global_load_lds_dwordx4"), (name, l, nxt)
+            seen += 1
+    assert seen > 0
+
+
+def test_default_readout_has_no_spills(asm):
+    found = False
+    for name, body, meta in _functions(asm, r"_Z17readout_bf_kernelILi32ELi2ELi8ELi6ELi1ELb1ELi2ELb1E"):
+        found = True
+        scratch = re.search(r"ScratchSize: (\d+)", meta)
+        assert scratch and int(scratch.group(1)) == 0, name
+    assert found
