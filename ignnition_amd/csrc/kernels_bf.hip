@@ -695,6 +695,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
   static_assert(CT == 1 && CHF % NTH == 0, "chunk layout: one 16-unit tile, whole 1 KB pieces per wave");
   __shared__ bf8 sw2[2][CHF];
   __shared__ bf8 sw1[W1F];
+  __shared__ f4 sbias[3 * 64];   // b1 | b2 | w3 (256 floats each): LDS reads, no vmcnt waits in the loops
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int j = lane & 15, g = lane >> 4;
   const u4v* W2v = reinterpret_cast<const u4v*>(W2f);
@@ -703,6 +704,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
   }
   for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
+  for (int i = tid; i < 3 * 64; i += NTH) sbias[i] = ld4((i < 64 ? a.b1 : i < 128 ? a.b2 : a.w3) + 4 * (i & 63));
   // PERSIST: the block loops over row groups with W1 staged once; the chunk loop's wrap-around
   // prefetch leaves chunk 0 in sw2[0] for the next group
   const int64_t n_groups = (a.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     for (int half = 0; half < 2; ++half) {
       const int u = 2 * s2 + half;
       f4 acc[RT];
-      const f4 bias = ld4(a.b1 + 16 * u + 4 * g);
+      const f4 bias = sbias[4 * u + g];
 #pragma unroll
       for (int t = 0; t < RT; ++t) acc[t] = bias;
 #pragma unroll
@@ -756,12 +758,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 #pragma unroll 1
   for (int v = 0; v < NCH; ++v) {
     const int cur = v & 1;
-    f4 b[CT], w3[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      b[c] = ld4(a.b2 + 16 * (CT * v + c) + 4 * g);
-      w3[c] = ld4(a.w3 + 16 * (CT * v + c) + 4 * g);
-    }
+    const f4 b = sbias[64 + 4 * v + g];
     const int nv = (v + 1) % NCH;
     // chunk v+1 goes straight into the other buffer by LDS-DMA (its readers passed the previous
     // barrier).  Issued as asm: the compiler cannot tell the DMA's target from the buffer read
@@ -785,7 +782,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
     const bf8* wbase = sw2[cur] + lofs;
     f4 acc[RT];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) acc[t] = b[0];
+    for (int t = 0; t < RT; ++t) acc[t] = b;
     // the three weight pieces of k-step s+1 are read while k-step s's MFMAs run
     bf8 wn[3];
 #pragma unroll
@@ -810,10 +807,11 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
         }
       __builtin_amdgcn_sched_barrier(0);
     }
+    const f4 w3 = sbias[128 + 4 * v + g];
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) y[t] += w3[0][q] * act_t<ACT>(acc[t][q]);
+      for (int q = 0; q < 4; ++q) y[t] += w3[q] * act_t<ACT>(acc[t][q]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed (for every wave: barrier)
     __syncthreads();
   }
@@ -989,7 +987,8 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   // persistent blocks (W1 staged once per block, W2 chunk 0 carried over): 3.54-3.56 vs 3.58-3.59
   // ms/step on one box (tools/ab_env.sh, round 2)
   // W2 chunks by LDS-DMA + weight pieces read one k-step ahead: 1.025-1.031 vs 1.079-1.109 ms per
-  // launch, 3.51 vs 3.58-3.59 ms/step (same box, round 2)
+  // launch, 3.51 vs 3.58-3.59 ms/step (same box, round 2); b1/b2/w3 read from LDS (no vmcnt wait in the
+  // loops, which would also have waited for the DMA): 0.983-0.989 vs 1.020-1.042 ms
   if (din == 32)
     return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
   // DIN 64 (the 1M-node graph): W1's pieces (96 KB) in LDS beside the W2 double buffer (48 KB),

@@ -5,8 +5,9 @@ VAR=$1; VALS=$2; REPS=${3:-2}; shift 3
 mkdir -p gpurun_out/ab
 for r in $(seq $REPS); do
   for v in $VALS; do
-    env $VAR=$v timeout -k 10 200 python -u bench.py --no-cpu "$@" > gpurun_out/ab/$VAR-$v-$r.json 2> gpurun_out/ab/$VAR-$v-$r.err || { echo "run $v failed"; exit 1; }
-    python - "$VAR=$v" gpurun_out/ab/$VAR-$v-$r.json <<'PY'
+    f=gpurun_out/ab/$VAR-${v//\//_}-$r
+    env $VAR=$v timeout -k 10 200 python -u bench.py --no-cpu "$@" > $f.json 2> $f.err || { echo "run $v failed"; exit 1; }
+    python - "$VAR=$v" $f.json <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 wk = d["roofline"]["warmup_kernels"]
