@@ -360,7 +360,7 @@ def main():
         bf = v["mfma_bf16"] >= v["mfma_f32"]
         tf = (v["mfma_bf16"] if bf else v["mfma_f32"]) / (v["ms"] / 1e3) / 1e12
         peak = PEAK_BF16_MFMA_TFLOPS if bf else PEAK_FP32_MFMA_TFLOPS
-        return {"dtype": "bf16" if bf else "f32", "achieved_tflops": round(tf, 2), "peak_tflops": peak,
+        return {"dtype": "bf16|f16" if bf else "f32", "achieved_tflops": round(tf, 2), "peak_tflops": peak,
                 "frac": round(tf / peak, 4)}
 
     workload = "%s_%s_x%d%s" % (args.model, args.topology, args.graphs,
@@ -395,15 +395,18 @@ def main():
                                        "alg_gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1),
                                        "mfma_pipe": pipe(v)}
                                    for k, v in warm.items() if v["launches"]}}
-    seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "4"))
-    ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "2"))
+    seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "6"))
+    ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "4"))
     sum_v = int(os.environ.get("IGN_SUM_VARIANT", "7"))
-    split = lambda v, six: ("split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
-                            % (6 if six else 9)) if v else "f32 MFMA"
-    contraction = {"ordered_update_hU": split(seq_v >= 4, seq_v == 4),
-                   "readout": split(ro_v in (2, 3, 4), ro_v != 3),
+    BF = "split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
+    H16 = ("split-fp16: power-of-two-scaled 2-piece fp16 operands (RNE, 2^-22 relative), %d products, "
+           "fp32 accumulate")
+    seq_c = {2: "f32 MFMA", 4: BF % 6, 5: BF % 9, 6: H16 % 3, 7: H16 % 4}
+    ro_c = {1: "f32 MFMA", 2: BF % 6, 3: BF % 9, 4: "layer 1 " + BF % 6 + "; layer 2 " + H16 % 3}
+    contraction = {"ordered_update_hU": seq_c.get(seq_v, "f32 MFMA") if plan.hidden[0] in (32, 64) else "f32 MFMA",
+                   "readout": ro_c.get(ro_v, BF % 6),
                    # sum variant 7 (default): split-bf16 x.W / h.U for plain sums at DIN = H = 32 or 64
-                   "sum_update": split(plan.hidden[0] in (32, 64) and sum_v == 7, True),
+                   "sum_update": BF % 6 if plan.hidden[0] in (32, 64) and sum_v == 7 else "f32 MFMA",
                    "projection": "f32 MFMA"}
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,

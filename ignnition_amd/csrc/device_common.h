@@ -25,6 +25,26 @@ typedef short bf8 __attribute__((ext_vector_type(8)));      // 8 bf16: A/B fragm
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 #define MFMA_BF(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
+// ---- split-fp16 contraction (scaled two-piece fp16 operands, 3 products) --------------------------
+// fp16 carries 11 significand bits: x' = s x (s a power of two putting max |x'| below 2^15) is
+// rounded to hi = fp16(x') (RNE), the exact remainder to lo = fp16(x' - hi), so
+// |x' - hi - lo| <= 2^-22 |x'| (plus 2^-25 absolute where lo falls below the fp16 normal range,
+// i.e. for values 2^-18 below the operand's scale).  Three products hi*hi + hi*lo + lo*hi drop
+// lo*lo (< 2^-22 |ab|): per product about 3 * 2^-22, the same class as the x6 bf16 split
+// (2^-21.2 measured), from half the MFMAs and two pieces instead of three.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));    // 8 fp16: A/B fragment of 16x16x32
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+#define MFMA_H(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
+
+// (hi, lo) fp16 pieces of the pair (a, b), packed [a | b << 16] (v_cvt_pk_f16_f32, RNE)
+__device__ __forceinline__ void split2h(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const h2 p = __builtin_convertvector((f2){a, b}, h2);
+  const h2 q = __builtin_convertvector((f2){a - (float)p[0], b - (float)p[1]}, h2);
+  hi = __builtin_bit_cast(uint32_t, p);
+  lo = __builtin_bit_cast(uint32_t, q);
+}
+
 __device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {
   hi = __uint_as_float(__float_as_uint(x) & 0xFFFF0000u);
   const float r1 = x - hi;

@@ -130,6 +130,7 @@ int ign::repack(ign_plan* p) {
                             p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, cp.din, cp.H,
                             p->stream));
     if (cp.pk_ubf >= 0) HIP_TRY(launch_pack_u_bf16(p->d_params + cp.off_rk, p->d_packed + cp.pk_ubf, cp.H, p->stream));
+    if (cp.pk_uh >= 0) HIP_TRY(launch_pack_u_f16(p->d_params + cp.off_rk, p->d_packed + cp.pk_uh, cp.H, p->stream));
     if (cp.pk_wbf >= 0)
       HIP_TRY(launch_pack_w_bf16(p->d_params + cp.off_k, p->d_packed + cp.pk_wbf, cp.din, cp.H, p->stream));
     if (cp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
@@ -156,6 +157,11 @@ int ign::repack(ign_plan* p) {
   if (p->pk_w12 >= 0)
     HIP_TRY(launch_attn_vectors(p->d_params + p->off_k1, p->d_params + p->off_k2, p->d_params + p->off_att, p->attn_F,
                                 p->d_packed + p->pk_w12, p->stream));
+  if (p->dense.size() >= 2 && p->dense[1].pk_h >= 0) {
+    const DenseP &l1 = p->dense[0], &l2 = p->dense[1];
+    HIP_TRY(launch_pack_readout_h16(p->d_params + l1.off_w, l1.use_bias ? p->d_params + l1.off_b : nullptr,
+                                    p->d_params + l2.off_w, p->d_packed + l2.pk_h, l1.in, l1.out, l2.out, p->stream));
+  }
   for (auto& dp : p->dense) {
     if (dp.pk_w >= 0) HIP_TRY(launch_pack_dense(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in, dp.out, p->stream));
     if (dp.pk_bf >= 0)   // layer 1 reads its input from memory (natural k), layer 2 chains from registers
@@ -192,7 +198,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(5, std::max(2, atoi(v)));
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(7, std::max(2, atoi(v)));
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 ? 7 : 3;
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
@@ -200,7 +206,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TSGEMM_BF")) p->tsgemm_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
-  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(3, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(4, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -381,6 +387,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.pk_u = pk; pk = align(pk + 3LL * cp.H * cp.H);
     cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
     if (pack_u_bf16_floats(cp.H)) { cp.pk_ubf = pk; pk = align(pk + pack_u_bf16_floats(cp.H)); }
+    if (pack_u_f16_floats(cp.H)) { cp.pk_uh = pk; pk = align(pk + pack_u_f16_floats(cp.H)); }
     if ((cp.din == 64 && cp.H == 64) || (cp.din == 32 && cp.H == 32)) { cp.pk_wbf = pk; pk = align(pk + pack_w_bf16_floats(cp.din, cp.H)); }
   }
   for (size_t l = 0; l < p->dense.size(); ++l) {
@@ -393,6 +400,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
         readout_bf_supported(p->dense[0].in, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act)) {
       dp.pk_bf = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
+      if (l == 1) { dp.pk_h = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64); }
     }
     if (dense_bf_supported(dp.in, dp.out)) {
       dp.pk_bfn = pk;
@@ -1185,12 +1193,15 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     SeqGruArgs a{hin, hout, mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                  p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
     if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
-    {   // MFMAs per wave step: split-bf16 (variants 4 / 5, H = 32 / 64) passes x 3 gates x H/16 x H/32;
-        // f32 (seq_gru2) 3 gates x H/16 x H/4
-      const bool bf = (p->seq_variant == 4 || p->seq_variant == 5) && (cp.H == 32 || cp.H == 64) && a.Ubf;
+    if (cp.pk_uh >= 0) a.Uh = p->d_packed + cp.pk_uh;
+    {   // MFMAs per wave step: split-fp16 / split-bf16 (variants 6, 7 / 4, 5; H = 32 / 64) passes x
+        // 3 gates x H/16 x H/32 on the 16x16x32 pipe; f32 (seq_gru2) 3 gates x H/16 x H/4
+      const int v = p->seq_variant;
+      const int passes = v == 6 ? 3 : v == 7 ? 4 : v == 5 ? 9 : 6;
+      const bool bf = v >= 4 && (cp.H == 32 || cp.H == 64) && a.Ubf;
       const double ws = (double)mb.wave_steps;
       tm.begin(K_SEQ, mb.flops, mb.bytes,
-               bf ? ws * (p->seq_variant == 5 ? 9 : 6) * 3 * (cp.H / 16) * (cp.H / 32) * kMfmaBf16Flops : 0,
+               bf ? ws * passes * 3 * (cp.H / 16) * (cp.H / 32) * kMfmaBf16Flops : 0,
                bf ? 0 : ws * 3 * (cp.H / 16) * (cp.H / 4) * kMfmaF32Flops);
     }
     HIP_TRY(launch_seq_gru(a, cp.H, p->seq_variant, st));
@@ -1300,15 +1311,20 @@ int readout(ign_plan* p, ign_batch* b) {
     if (!a.b1 || !a.b2) return fail(IGN_ERR_UNSUPPORTED, "fused readout requires use_bias on hidden layers");
     double flops = 2.0 * P * ((double)l1.in * l1.out + (double)l2.in * l2.out + l3.in);
     const bool bf = p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0;
+    const bool h16 = p->readout_variant == 4 && bf && l2.pk_h >= 0;
     const double tiles = (double)((P + 15) / 16);
     // per 16-row tile: layer 1 out/16 x in/32 and layer 2 out/16 x in/32 MFMAs of 16x16x32, x6 or x9
     // products (readout_bf); f32 (readout3): out/16 x in/4 each of 16x16x4
     const double k1 = (double)(l1.out / 16) * (l1.in / 32) + (double)(l2.out / 16) * (l2.in / 32);
     const double k1f = (double)(l1.out / 16) * (l1.in / 4) + (double)(l2.out / 16) * (l2.in / 4);
+    // variant 4: layer 1 x6, layer 2 x3 (16x16x32 f16, the bf16 rate)
+    const double kh = 6.0 * (l1.out / 16) * (l1.in / 32) + 3.0 * (l2.out / 16) * (l2.in / 32);
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0),
-             bf ? tiles * k1 * (p->readout_variant == 3 ? 9 : 6) * kMfmaBf16Flops : 0,
+             h16 ? tiles * kh * kMfmaBf16Flops : bf ? tiles * k1 * (p->readout_variant == 3 ? 9 : 6) * kMfmaBf16Flops : 0,
              bf ? 0 : tiles * k1f * kMfmaF32Flops);
-    if (bf)
+    if (h16)
+      HIP_TRY(launch_readout_h16(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_h, l1.in, st));
+    else if (bf)
       HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
                                 p->readout_variant == 3 ? 9 : 6, st));
     else

@@ -91,6 +91,7 @@ struct CellP {
   int64_t pk_wt = -1, pk_ut = -1; // backward: unscaled W^T / U^T fragments (pack_a)
   int64_t pk_wbf = -1;            // split-bf16 input-kernel fragments (sum variant 7, DIN = H = 64)
   int64_t pk_ubf = -1;            // split-bf16 recurrent-kernel fragments (seq variants 4/5)
+  int64_t pk_uh = -1;             // split-fp16 recurrent-kernel fragments + scale (seq variants 6/7)
   bool used = false;
 };
 
@@ -100,6 +101,7 @@ struct DenseP {
   int64_t off_w, off_b, pk_w = -1;   // pk_w: forward fragments (fused readout, training readout)
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
   int64_t pk_bf = -1;             // fused readout: split-bf16 A fragments (readout variants 2/3)
+  int64_t pk_h = -1;              // fused readout, layer 2: scaled split-fp16 fragments (readout variant 4)
   int64_t pk_bfn = -1;            // training forward: split-bf16 pieces, natural k (dense_bf)
   int64_t pk_bft = -1;            // training backward: split-bf16 pieces of W^T (dense_bf_t)
 };
@@ -237,11 +239,13 @@ struct ign_plan {
   float* d_packed = nullptr;
   bool params_set = false;
   bool fused_readout = false;
-  int readout_variant = 2;        // fused readout: 1 = f32 MFMA (readout3), 2 / 3 = split-bf16 with 6 / 9
+  int readout_variant = 4;        // fused readout: 4 = layer 2 on split-fp16 (3 products), 1 = f32 MFMA
+                                  // (readout3), 2 / 3 = split-bf16 with 6 / 9
                                   // piece products (readout_bf); IGN_READOUT_VARIANT
   int ro_width = 0;
-  int seq_variant = 4;            // ordered update: 4 / 5 = split-bf16 h.U with 6 / 9 piece products
-                                  // (H = 32, 64), 2 = f32 MFMA; IGN_SEQ_VARIANT
+  int seq_variant = 6;            // ordered update: 4 / 5 = split-bf16 h.U with 6 / 9 piece products,
+                                  // 6 / 7 = split-fp16 with 3 / 4 (inference; H = 32, 64), 2 = f32
+                                  // MFMA; IGN_SEQ_VARIANT
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels (placement only; off:
                                   // measured slower, profiles/r02/seq_experiments)
   int sum_variant = 7;            // sum update: 7 = split-bf16 GRU step where available (DIN = H = 32
@@ -267,6 +271,11 @@ struct ign_plan {
   std::shared_ptr<DevPool> pool;  // batch / training buffers (created with the stream, ensure_device)
   std::string describe;           // ign_plan_create_json: ign_plan_describe_json's document
 };
+
+// the ordered update of the training forward saves every step's state, which the split-fp16 kernels
+// (variants 6 / 7, inference only) do not: training runs the x6 split-bf16 form for them
+inline int train_seq_variant(const ign_plan* p) { return p->seq_variant >= 6 ? 4 : std::max(2, p->seq_variant); }
+
 
 struct ign_batch {
   ign_plan* plan = nullptr;

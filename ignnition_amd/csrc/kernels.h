@@ -29,6 +29,7 @@ struct SeqGruArgs {
   float* hs_save = nullptr;  // training: [n_steps + n_dst][H], order position p writes rows
                              // step_ptr[p] + p (state before) .. + len[p] (after each step)
   const void* Ubf = nullptr;  // variants 4/5: recurrent kernel as exact 3-piece bf16 A fragments
+  const void* Uh = nullptr;   // variants 6/7: scaled 2-piece fp16 A fragments + scale (pack_u_f16)
 };
 
 struct SumGruArgs {
@@ -94,6 +95,12 @@ hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStrea
 // recurrent kernel -> split-bf16 A fragments for seq variants 4/5 (H = 32 or 64); floats used: 9 H^2 / 2
 hipError_t launch_pack_u_bf16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_bf16_floats(int H) { return (H == 32 || H == 64) ? 9LL * H * H / 2 : 0; }
+// split-fp16 ordered update (kernels_bf.hip, inference only), passes 3 or 4
+hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStream_t st);
+// recurrent kernel -> scaled 2-piece fp16 A fragments for seq variants 6/7 (H = 32 or 64), then the
+// scale's exponent; floats used: 3 H^2 + 64
+hipError_t launch_pack_u_f16(const float* U, void* out, int H, hipStream_t st);
+inline int64_t pack_u_f16_floats(int H) { return (H == 32 || H == 64) ? 3LL * H * H + 64 : 0; }
 // pieces of a [K][3H] input kernel (K % 32 == 0) for the split-bf16 sum update
 hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream_t st);
 inline int64_t pack_w_bf16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 9LL * K * H / 2 : 0; }
@@ -125,6 +132,11 @@ hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hi
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from
 // launch_pack_dense_bf16 (W1 natural k order, W2 chained); floats used: 3 IN OUT / 2
 bool readout_bf_supported(int din, int n1, int n2, int act1, int act2);
+// readout variant 4: layer 1 on the x6 bf16 pieces (W1f as for launch_readout_bf), layer 2 on scaled
+// 2-piece fp16 pieces of W2 (pack_readout_h16: 256 x 256 floats + 64 of header)
+hipError_t launch_readout_h16(const Readout3Args& args, const void* W1f, const void* W2h, int din, hipStream_t st);
+hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
+                                   int n2, hipStream_t st);
 hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
                              hipStream_t st);
 hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, int chained, hipStream_t st);

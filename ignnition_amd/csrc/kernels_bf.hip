@@ -195,6 +195,206 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Variants 6 / 7 of the ordered update: seq_gru_bf's recurrence with h.U from scaled two-piece
+// fp16 operands (device_common.h split2h) on v_mfma_f32_16x16x32_f16: 3 (variant 6) or 4
+// (variant 7, adds lo*lo) products per gate tile instead of 6, and 2 pieces to split per state
+// value instead of 3.
+// Scales (exact powers of two, so every product is the fp32 product of the scaled values):
+// - U (pre-scaled as for pack_gru) by sigma = 2^(14 - floor(log2 max|U|)), once at pack time
+//   (pack_u_f16_kernel, stored after the fragments);
+// - the wave's state by S = 2^(15 - E), m = max(1, max |h| over the tile's 16 rows) < 2^E.  The
+//   GRU keeps |h| <= max(|h_0|, 1) along the sequence (h' = z h + (1 - z) tanh, a convex
+//   combination), so |S h| < 2^15 holds at every step and the fp16 pieces never overflow.
+// The kernel carries S h: with SS = S sigma and c = 1 / SS the gate arithmetic absorbs the
+// scales at no extra instruction:
+//   z  = 1 / (1 + 2^(c acc_z + x_z))
+//   rc = 1 / ((1 + 2^(c acc_r + x_r)) SS)            (= r / SS)
+//   n' = S - 2 S / (1 + 2^(x_n + rc acc_n))          (acc_n seeded with SS b_n: = S tanh(.))
+//   h' = n' + z (h' - n')
+template <int H, int PASSES>
+__global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
+  constexpr int NT = H / 16, KS = H / 32;
+  constexpr int NF = 6 * NT * KS;            // fragments: 2 pieces x 3 gates x NT tiles x KS k-steps
+  static_assert(H == 32 || H == 64, "split-fp16 ordered update: 32 or 64 units");
+  static_assert(PASSES == 3 || PASSES == 4, "3 or 4 piece products");
+  __shared__ float sbias[H];
+  __shared__ float sbn[4][H];                // per wave: the candidate's recurrent bias times SS
+  __shared__ h8 su[NF * 64];
+  for (int i = threadIdx.x; i < H; i += blockDim.x) sbias[i] = a.bias[3 * H + i];
+  {
+    const u4v* src = reinterpret_cast<const u4v*>(a.Uh);
+    u4v* dst = reinterpret_cast<u4v*>(su);
+    for (int e = threadIdx.x; e < NF * 64; e += blockDim.x) dst[e] = src[e];
+  }
+  // sigma's exponent (stored after the fragments by pack_u_f16_kernel)
+  const int es = __float_as_int(reinterpret_cast<const float*>(a.Uh)[(int64_t)NF * 64 * 4]);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const float* tab = a.table + 4 * g;
+  __syncthreads();
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int L = valid ? a.len[pos] : 0;
+    const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    int Lmax = L;
+    float m = 1.0f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(h[t][r]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      Lmax = max(Lmax, __shfl_xor(Lmax, o));
+      m = fmaxf(m, __shfl_xor(m, o));
+    }
+    // m = f 2^E, f in [0.5, 1): S = 2^(15 - E); SS = S sigma
+    const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(m)) >> 23) - 126;
+    const int eS = 15 - E;
+    const float S = __int_as_float((127 + eS) << 23);
+    const float S2n = -2.0f * S;
+    const float SS = __int_as_float((127 + eS + es) << 23);
+    const float c = __int_as_float((127 - eS - es) << 23);
+    // every lane writes (and later reads back) exactly its own bias slots: no cross-lane hand-off
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      h[t] *= S;
+      *reinterpret_cast<f4*>(&sbn[wave][16 * t + 4 * g]) = *reinterpret_cast<const f4*>(sbias + 16 * t + 4 * g) * SS;
+    }
+    auto load_x = [&](uint32_t code, f4 (&x)[3][NT]) {
+      const float* p = tab + (int64_t)code * (3 * H);
+#pragma unroll
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+    };
+    auto step = [&](int t, const f4 (&x)[3][NT]) __attribute__((always_inline)) {
+      // B fragments: the two fp16 pieces of the scaled state, k-step s = accumulator tiles 2s, 2s+1
+      h8 hf[2][KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        u4v w0, w1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e0 = 2 * q, e1 = 2 * q + 1;
+          uint32_t p0, p1;
+          split2h(h[2 * s + (e0 >> 2)][e0 & 3], h[2 * s + (e1 >> 2)][e1 & 3], p0, p1);
+          w0[q] = p0;
+          w1[q] = p1;
+        }
+        hf[0][s] = __builtin_bit_cast(h8, w0);
+        hf[1][s] = __builtin_bit_cast(h8, w1);
+      }
+      f4 acc[3][NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        acc[0][i] = f4{0, 0, 0, 0};
+        acc[1][i] = f4{0, 0, 0, 0};
+        acc[2][i] = *reinterpret_cast<const f4*>(&sbn[wave][16 * i + 4 * g]);
+      }
+      // the fragment reads are loop-invariant: an opaque lane offset keeps the compiler from
+      // hoisting them out of the step loop into registers (occupancy)
+      int lofs = lane;
+      asm volatile("" : "+v"(lofs));
+      // U lo x {lo (x4), hi}, then U hi x {lo, hi}: small products first
+#pragma unroll
+      for (int pu = 1; pu >= 0; --pu) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) {
+            h8 w[3];
+#pragma unroll
+            for (int G = 0; G < 3; ++G) w[G] = su[(((pu * 3 + G) * NT + i) * KS + s) * 64 + lofs];
+#pragma unroll
+            for (int ph = 1; ph >= 0; --ph) {
+              if (PASSES == 3 && pu + ph > 1) continue;
+#pragma unroll
+              for (int G = 0; G < 3; ++G) acc[G][i] = MFMA_H(w[G], hf[ph][s], acc[G][i]);
+            }
+          }
+        }
+      }
+      const bool act = t < L;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
+          const float z = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(acc[0][i][r], c, x[0][i][r])));
+          const float rc = rcpf_(fmaf(__builtin_amdgcn_exp2f(fmaf(acc[1][i][r], c, x[1][i][r])), SS, SS));
+          const float q = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(rc, acc[2][i][r], x[2][i][r])));
+          const float n = fmaf(q, S2n, S);
+          const float hn = n + z * (h[i][r] - n);
+          h[i][r] = act ? hn : h[i][r];
+        }
+      }
+    };
+    // the projected row of step t is loaded at the start of step t and consumed by the gates after
+    // the h.U MFMAs (a two-buffer one-step-ahead prefetch, loop unrolled by two, measured slower:
+    // 0.242 vs 0.214 ms per launch, 144 VGPRs -> 3 waves per SIMD)
+    uint32_t code = codes[0];
+    for (int t = 0; t < Lmax; ++t) {
+      f4 x[3][NT];
+      load_x(code, x);
+      code = codes[t + 1];
+      step(t, x);
+    }
+    if (valid) {
+      const float iS = __int_as_float((127 - eS) << 23);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t] * iS);
+    }
+  }  // tile loop
+}
+
+// U (pre-scaled as for pack_gru) -> sigma U as fp16 (hi, lo) A fragments of seq_gru_h16 (layout of
+// pack_u_bf16 with 2 pieces), then sigma's exponent as an int after them.  One block.
+__global__ __launch_bounds__(256) void pack_u_f16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out,
+                                                         int H) {
+  const int NT = H / 16, KS = H / 32, n = H * 3 * H;
+  __shared__ float red[256];
+  float m = 0.f;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const float sc = (e % (3 * H)) >= 2 * H ? IGN_2LOG2E : IGN_NLOG2E;
+    m = fmaxf(m, fabsf(sc * U[e]));
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  m = red[0];
+  // sigma = 2^(15 - E) with m = f 2^E, f in [0.5, 1): max |sigma U| < 2^15; clamped for tiny / zero U
+  int es = m > 0.f ? 15 - ((__float_as_int(m) >> 23) - 126) : 0;
+  es = min(100, max(-100, es));
+  const float sigma = __int_as_float((127 + es) << 23);
+  const int64_t total = 6LL * NT * KS * 64 * 8;
+  for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
+    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // ((piece * 3 + gate) * NT + tile) * KS + s
+    const int s = (int)(f % KS); f /= KS;
+    const int i = (int)(f % NT); f /= NT;
+    const int G = (int)(f % 3);
+    const int piece = (int)(f / 3);
+    const int k = 16 * (2 * s + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
+    const int col = G * H + 16 * i + (lane & 15);
+    const float sc = G == 2 ? IGN_2LOG2E : IGN_NLOG2E;
+    const float v = sigma * (sc * U[(int64_t)k * 3 * H + col]);
+    const _Float16 hi = (_Float16)v;
+    const _Float16 p = piece == 0 ? hi : (_Float16)(v - (float)hi);
+    out[e] = __builtin_bit_cast(uint16_t, p);
+  }
+  if (threadIdx.x == 0) reinterpret_cast<int*>(out)[total / 2] = es;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Variant 7 of the sum update (kernels.hip sum_gru_lds, DIN = H = 64): the same persistent,
 // in-degree-sorted tiles and message gather, with x.W and h.U on the bf16 matrix path,
 // fp32-exact (6 piece products).  At 64/64 the f32 form issues 384 f32 MFMAs per
@@ -830,6 +1030,253 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// Readout variant 4: readout_bf with layer 2 (256 x 256, 89 % of the MFMAs) on scaled two-piece
+// fp16 operands (device_common.h split2h, 3 products on v_mfma_f32_16x16x32_f16) instead of
+// x6 bf16.  Layer 1 stays x6 bf16.  Scales (powers of two, exact):
+// - W2 by sigma2 = 2^(15 - E(max |W2|)) at pack time (pack_readout_h16_kernel);
+// - the layer-2 input of row tile t by S_t, from an a-priori bound on the layer-1 activations:
+//   |W1^T x + b1| <= A mx_t + B (A = max_u sum_k |W1[k][u]|, B = max |b1|, mx_t = the tile's
+//   max |x|), and |act(z)| <= 1.0508 |z| + 1.7582 for linear / relu / selu / tanh / sigmoid,
+//   so |S_t act(z)| < 2^15 (no fp16 overflow) whatever the input scale.
+// S_t is applied where it is free: x is scaled before its (exact) bf16 split, the layer-1 bias
+// seeds the accumulator times S_t, and the activation is evaluated on the scaled value
+// (act_scaled).  Layer 2 accumulates S_t sigma2 (W2^T a + b2); its activation and the w3 dot
+// product run on that scale and the row's output is unscaled once.
+__global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                               const float* __restrict__ W2, uint16_t* __restrict__ out,
+                                                               int IN1, int N1, int N2) {
+  __shared__ float red[3][256];
+  float m2 = 0.f, a1 = 0.f, bb = 0.f;
+  for (int e = threadIdx.x; e < N1 * N2; e += blockDim.x) m2 = fmaxf(m2, fabsf(W2[e]));
+  for (int u = threadIdx.x; u < N1; u += blockDim.x) {
+    float l1 = 0.f;
+    for (int k = 0; k < IN1; ++k) l1 += fabsf(W1[(int64_t)k * N1 + u]);
+    a1 = fmaxf(a1, l1);
+    if (b1) bb = fmaxf(bb, fabsf(b1[u]));
+  }
+  red[0][threadIdx.x] = m2;
+  red[1][threadIdx.x] = a1;
+  red[2][threadIdx.x] = bb;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int q = 0; q < 3; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + o]);
+    __syncthreads();
+  }
+  m2 = red[0][0];
+  int es = m2 > 0.f ? 15 - ((__float_as_int(m2) >> 23) - 126) : 0;
+  es = min(100, max(-100, es));
+  const float sigma = __int_as_float((127 + es) << 23);
+  const int KS = N1 / 32;
+  const int64_t total = (int64_t)(N2 / 16) * KS * 2 * 512;
+  for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
+    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // (u * KS + s) * 2 + piece
+    const int piece = (int)(f & 1); f >>= 1;
+    const int s = (int)(f % KS);
+    const int u = (int)(f / KS);
+    const int k = 16 * (2 * s + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);   // chained k order
+    const float v = sigma * W2[(int64_t)k * N2 + 16 * u + (lane & 15)];
+    const _Float16 hi = (_Float16)v;
+    const _Float16 pc = piece == 0 ? hi : (_Float16)(v - (float)hi);
+    out[e] = __builtin_bit_cast(uint16_t, pc);
+  }
+  if (threadIdx.x == 0) {
+    int* hdr = reinterpret_cast<int*>(out + total);
+    hdr[0] = es;
+    hdr[1] = __float_as_int(red[1][0] * 1.001f);   // A, rounded up
+    hdr[2] = __float_as_int(red[2][0] * 1.001f);   // B
+  }
+}
+
+// S act(zs c) for zs = S z (S a power of two, c = 1 / S), at the cost of act(z)
+template <int ACT>
+__device__ __forceinline__ float act_scaled(float zs, float c, float cl, float laS, float S) {
+  if constexpr (ACT == IGN_K_ACT_RELU) return zs > 0.f ? zs : 0.f;
+  else if constexpr (ACT == IGN_K_ACT_SELU) {   // cl = c log2(e), laS = lambda alpha S
+    const float lam = 1.0507009873554805f;
+    const float e = __builtin_amdgcn_exp2f(fminf(zs, 0.f) * cl);
+    return zs > 0.f ? lam * zs : fmaf(laS, e, -laS);
+  } else if constexpr (ACT == IGN_K_ACT_LINEAR) return zs;
+  else return S * act_t<ACT>(zs * c);
+}
+
+template <int DIN, int ACT, int WAVES, int RT>
+__global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a, const bf8* __restrict__ W1f,
+                                                                  const h8* __restrict__ W2f) {
+  constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
+  constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
+  constexpr int NTH = 64 * WAVES;
+  constexpr int CHF = KS2 * 2 * 64;              // h8 per W2 chunk of one 16-unit tile (16 KB)
+  constexpr int NCH = U2;
+  constexpr int W1F = U1 * KS1 * 3 * 64;
+  static_assert(CHF % NTH == 0, "chunk layout: whole 1 KB pieces per wave");
+  constexpr float LA = 1.0507009873554805f * 1.6732632423543772f, LOG2E = 1.4426950408889634f;
+  __shared__ h8 sw2[2][CHF];
+  __shared__ bf8 sw1[W1F];
+  __shared__ f4 sbias[3 * 64];   // b1 | b2 | w3
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int j = lane & 15, g = lane >> 4;
+  const u4v* W2v = reinterpret_cast<const u4v*>(W2f);
+  {
+    const u4v* W1v = reinterpret_cast<const u4v*>(W1f);
+    for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
+  }
+  for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
+  for (int i = tid; i < 3 * 64; i += NTH) sbias[i] = ld4((i < 64 ? a.b1 : i < 128 ? a.b2 : a.w3) + 4 * (i & 63));
+  const int* hdr = reinterpret_cast<const int*>(W2f + (int64_t)NCH * CHF);
+  const int es2 = hdr[0];
+  const float A1 = __int_as_float(hdr[1]), B1 = __int_as_float(hdr[2]);
+  const int64_t n_groups = (a.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
+  for (int64_t grp = blockIdx.x; grp < n_groups; grp += (int64_t)gridDim.x) {
+  const int64_t r0 = (grp * WAVES + wave) * (16 * RT) + j;
+  // per row tile: the layer-1 input, its max |x|, and the scales derived from it
+  f4 xl[RT][KS1][2];
+  float mx[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int64_t r = r0 + 16 * t;
+    const bool ok = r < a.n_rows;
+    const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
+    mx[t] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      xl[t][s][0] = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+      xl[t][s][1] = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mx[t] = fmaxf(mx[t], fmaxf(fabsf(xl[t][s][0][q]), fabsf(xl[t][s][1][q])));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+    for (int t = 0; t < RT; ++t) mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], o));
+  float S[RT], cS[RT], SS[RT], cSS[RT];
+  bf8 xf[RT][KS1][3];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const float bnd = fmaf(fmaf(A1, mx[t], B1), 1.0508f, 1.7582f);
+    const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(bnd)) >> 23) - 126;   // bnd < 2^E
+    const int eS = 15 - E;
+    S[t] = __int_as_float((127 + eS) << 23);
+    cS[t] = __int_as_float((127 - eS) << 23);
+    SS[t] = __int_as_float((127 + eS + es2) << 23);
+    cSS[t] = __int_as_float((127 - eS - es2) << 23);
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const f4 lo = xl[t][s][0] * S[t], hi = xl[t][s][1] * S[t];
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      split_frag(v, xf[t][s]);
+    }
+  }
+  __syncthreads();
+  // layer 1 (x6 bf16) -> S_t act(z) in accumulator layout -> the layer-2 fp16 B fragments
+  h8 hf[RT][KS2][2];
+#pragma unroll
+  for (int s2 = 0; s2 < KS2; ++s2) {
+    float v[RT][8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int u = 2 * s2 + half;
+      f4 acc[RT];
+      const f4 bias = sbias[4 * u + g];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = bias * S[t];
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) split_mfma_rt<6, RT, KS1>(sw1 + ((u * KS1 + s) * 3) * 64 + lane, 64, xf, s, acc);
+#pragma unroll
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[t][4 * half + q] = act_scaled<ACT>(acc[t][q], cS[t], cS[t] * LOG2E, LA * S[t], S[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      u4v w0, w1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t p0, p1;
+        split2h(v[t][2 * q], v[t][2 * q + 1], p0, p1);
+        w0[q] = p0;
+        w1[q] = p1;
+      }
+      hf[t][s2][0] = __builtin_bit_cast(h8, w0);
+      hf[t][s2][1] = __builtin_bit_cast(h8, w1);
+    }
+  }
+  float y[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) y[t] = 0.f;
+#pragma unroll 1
+  for (int v = 0; v < NCH; ++v) {
+    const int cur = v & 1;
+    const f4 b = sbias[64 + 4 * v + g];
+    const int nv = (v + 1) % NCH;
+    // chunk v+1 by LDS-DMA into the other buffer (readout_bf_kernel: why asm, and M0)
+#pragma unroll
+    for (int k = 0; k < CHF / NTH; ++k) {
+      const int piece = wave + WAVES * k;
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(sw2[cur ^ 1] + piece * 64));
+      const u4v* src = W2v + (int64_t)nv * CHF + piece * 64 + lane;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int lofs = lane;
+    asm volatile("" : "+v"(lofs));
+    const h8* wbase = sw2[cur] + lofs;
+    f4 acc[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) acc[t] = b * SS[t];
+    h8 wn[2];
+#pragma unroll
+    for (int pu = 0; pu < 2; ++pu) wn[pu] = wbase[pu * 64];
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) {
+      h8 w[2];
+#pragma unroll
+      for (int pu = 0; pu < 2; ++pu) w[pu] = wn[pu];
+      if (s + 1 < KS2) {
+#pragma unroll
+        for (int pu = 0; pu < 2; ++pu) wn[pu] = wbase[((s + 1) * 2 + pu) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // W2 lo x a hi, W2 hi x {a lo, a hi}
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w[1], hf[t][s][0], acc[t]);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w[0], hf[t][s][1], acc[t]);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w[0], hf[t][s][0], acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const f4 w3 = sbias[128 + 4 * v + g];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        y[t] += w3[q] * act_scaled<ACT>(acc[t][q], cSS[t], cSS[t] * LOG2E, LA * SS[t], SS[t]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed (for every wave: barrier)
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    float yt = y[t];
+    yt += __shfl_xor(yt, 16);
+    yt += __shfl_xor(yt, 32);
+    const int64_t r = r0 + 16 * t;
+    if (g == 0 && r < a.n_rows) {
+      const float b3 = a.b3 ? a.b3[0] : 0.f;
+      a.y[r] = act_apply(fmaf(yt, cSS[t], b3), a.act3);
+    }
+  }
+  }  // row groups
+}
+
 __device__ __forceinline__ float act_grad_out(float a, int act) {   // act' through the output a
   switch (act) {
     case IGN_K_ACT_RELU: return a > 0.f ? 1.f : 0.f;
@@ -997,6 +1444,44 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
 }
 
 
+template <int DIN, int ACT>
+static void readout_h16_launch(const Readout3Args& args, const bf8* w1, const h8* w2, hipStream_t st) {
+  constexpr int WAVES = 8, RT = 2;
+  auto k = readout_h16_kernel<DIN, ACT, WAVES, RT>;
+  const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
+  hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w1, w2);
+}
+
+template <int DIN>
+static void readout_h16_din(const Readout3Args& args, const bf8* w1, const h8* w2, hipStream_t st) {
+  switch (args.act1) {
+    case IGN_K_ACT_SELU: readout_h16_launch<DIN, IGN_K_ACT_SELU>(args, w1, w2, st); break;
+    case IGN_K_ACT_RELU: readout_h16_launch<DIN, IGN_K_ACT_RELU>(args, w1, w2, st); break;
+    case IGN_K_ACT_TANH: readout_h16_launch<DIN, IGN_K_ACT_TANH>(args, w1, w2, st); break;
+    case IGN_K_ACT_SIGMOID: readout_h16_launch<DIN, IGN_K_ACT_SIGMOID>(args, w1, w2, st); break;
+    default: readout_h16_launch<DIN, IGN_K_ACT_LINEAR>(args, w1, w2, st); break;
+  }
+}
+
+hipError_t launch_readout_h16(const Readout3Args& args, const void* W1f, const void* W2h, int din, hipStream_t st) {
+  if (args.n_rows == 0) return hipSuccess;
+  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2h || !args.b1 || !args.b2)
+    return hipErrorInvalidValue;
+  const bf8* w1 = static_cast<const bf8*>(W1f);
+  const h8* w2 = static_cast<const h8*>(W2h);
+  if (din == 32) readout_h16_din<32>(args, w1, w2, st);
+  else readout_h16_din<64>(args, w1, w2, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
+                                   int n2, hipStream_t st) {
+  if (n1 != 256 || n2 != 256 || in1 % 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_readout_h16_kernel, dim3(1), dim3(256), 0, st, W1, b1, W2, static_cast<uint16_t*>(out), in1,
+                     n1, n2);
+  return hipGetLastError();
+}
+
 bool dense_bf_supported(int K, int M) {
   return (K == 32 || K == 64 || K == 128 || K == 256) && M % 128 == 0 && M > 0;
 }
@@ -1055,6 +1540,29 @@ hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, in
   if (IN % 32 || OUT % 16) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pack_dense_bf16_kernel, dim3(128), dim3(256), 0, st, W, static_cast<uint16_t*>(out), IN, OUT,
                      chained, 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  if (!args.Uh || args.hs_save || (h != 32 && h != 64) || (passes != 3 && passes != 4)) return hipErrorInvalidValue;
+  const int64_t work = grid_for(args.n_dst, 64);
+#define SEQ_H(HH, P)                                                                               \
+  {                                                                                                \
+    auto k = seq_gru_h16_kernel<HH, P>;                                                            \
+    hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);                \
+  }
+  if (h == 32 && passes == 3) SEQ_H(32, 3)
+  else if (h == 32) SEQ_H(32, 4)
+  else if (passes == 3) SEQ_H(64, 3)
+  else SEQ_H(64, 4)
+#undef SEQ_H
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_u_f16(const float* U, void* out, int H, hipStream_t st) {
+  if (H != 32 && H != 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H);
   return hipGetLastError();
 }
 

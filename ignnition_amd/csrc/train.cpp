@@ -535,7 +535,7 @@ int ign_forward_train_mp(ign_plan* p, ign_batch* b) {
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         a.hs_save = mt.hs[it];
         if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
-        HIP_TRY(launch_seq_gru(a, cp.H, std::max(2, p->seq_variant), st));
+        HIP_TRY(launch_seq_gru(a, cp.H, train_seq_variant(p), st));
       } else {
         SumGruArgs a{hin, hout, sb, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, p->d_packed + cp.pk_w,
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
@@ -796,7 +796,7 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
         a.scratch = t->bsum;
         // gate recompute on the forward's split-bf16 path when the forward ran seq_gru_bf x6
         // (bitwise the forward's gates); IGN_BWD_BF=0 keeps the f32 MFMA recompute
-        if (p->bwd_bf && H == 32 && cp.pk_ubf >= 0 && p->seq_variant == 4) a.Ubf = p->d_packed + cp.pk_ubf;
+        if (p->bwd_bf && H == 32 && cp.pk_ubf >= 0 && train_seq_variant(p) == 4) a.Ubf = p->d_packed + cp.pk_ubf;
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
       } else {
         HIP_TRY(launch_seq_gru_bwd(a, H, st));

@@ -290,7 +290,8 @@ def _scaled_err(got, exp):
 @pytest.mark.parametrize("hidden", [32, 64])
 def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
     """Ordered-update variants 4 / 5 and readout variants 2 / 3 form their contractions from
-    exact 3-piece bf16 splits (6 / 9 piece products, fp32 accumulation).  Their error vs the
+    exact 3-piece bf16 splits (6 / 9 piece products, fp32 accumulation); ordered-update variants
+    6 / 7 and readout variant 4's layer 2 from scaled 2-piece fp16 splits (3 / 4 piece products).  Their error vs the
     float64 oracle stays at the level of the native f32-MFMA kernels (seq 2, readout 1): within
     4x of it (or 1e-6), far inside the 1e-4 parity tolerance."""
     desc = model_examples.routenet(hidden=hidden, iterations=8)
@@ -301,7 +302,8 @@ def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
     prm = plan.init_params(5, bias_scale=0.2)
     ref = DenseOracle(desc, dims, prm).forward(graphs)
     errs = {}
-    for seq, ro in (("2", "1"), ("4", "1"), ("5", "1"), ("2", "2"), ("2", "3"), ("4", "2")):
+    for seq, ro in (("2", "1"), ("4", "1"), ("5", "1"), ("6", "1"), ("7", "1"), ("2", "2"), ("2", "3"), ("4", "2"),
+                    ("2", "4"), ("6", "4")):
         monkeypatch.setenv("IGN_SEQ_VARIANT", seq)
         monkeypatch.setenv("IGN_READOUT_VARIANT", ro)
         eng = Engine(plan, 0)
@@ -313,6 +315,45 @@ def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
         _close(out, ref)
         errs[seq + "/" + ro] = _scaled_err(out, ref)
     print("max scaled error vs float64 oracle (seq/readout variant):", errs)
+    for k, v in errs.items():
+        assert v <= max(4 * errs["2/1"], 1e-6), errs
+
+
+@pytest.mark.parametrize("hidden", [32, 64])
+@pytest.mark.parametrize("scale", [1e-3, 1.0, 3e4])
+def test_split_fp16_scaling(monkeypatch, hidden, scale):
+    """Ordered-update variants 6 / 7 scale the state by a power of two per 16-row tile (from the
+    tile's max |h|, which the GRU never exceeds along the sequence) and U by one at pack time;
+    readout variant 4 scales each row tile's layer-2 input from a bound on the layer-1
+    activations (max |x| of the tile, W1's column norms, b1) and W2 at pack time.  So the fp16
+    pieces neither overflow nor lose bits: path features of 1e-3, 1 and 3e4 (the path state
+    starts as [traffic | 0], the readout reads the path states) stay within the f32-MFMA
+    variants' error class vs the float64 oracle, and repeated runs are bitwise equal."""
+    desc = model_examples.routenet(hidden=hidden, iterations=8)
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", g) for g in range(2)])
+    for gr in graphs:
+        for f in mi.get_all_features():
+            gr[f.name] = np.asarray(gr[f.name], np.float32) * np.float32(scale)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(11, bias_scale=0.2)
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    errs = {}
+    for seq, ro in (("2", "1"), ("6", "1"), ("7", "1"), ("2", "4"), ("6", "4")):
+        monkeypatch.setenv("IGN_SEQ_VARIANT", seq)
+        monkeypatch.setenv("IGN_READOUT_VARIANT", ro)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        out = b.forward().reshape(-1)
+        again = b.forward().reshape(-1)
+        b.close()
+        eng.close()
+        assert np.array_equal(out, again)
+        _close(out, ref)
+        errs[seq + "/" + ro] = _scaled_err(out, ref)
+    print("scale %g H %d: max scaled error vs float64 oracle (seq/readout variant):" % (scale, hidden), errs)
     for k, v in errs.items():
         assert v <= max(4 * errs["2/1"], 1e-6), errs
 

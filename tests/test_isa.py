@@ -1,8 +1,8 @@
 """ISA checks of the readout kernel (CPU: hipcc cross-compiles gfx950 to assembly, no GPU).
 
-readout_bf_kernel issues its W2-chunk LDS-DMA as inline asm that loads M0, a register the compiler
+readout_bf_kernel and readout_h16_kernel issue their W2-chunk LDS-DMA as inline asm that loads M0, a register the compiler
 reserves (csrc/kernels_bf.hip): that is only sound while nothing else in the kernel uses M0.  The
-default DIN-32 instance must also stay free of register spills (its chunk loop runs at 254 VGPRs)."""
+DIN-32 selu instances must also stay free of register spills (their chunk loops run at 204-244 VGPRs)."""
 import os
 import re
 import subprocess
@@ -33,7 +33,7 @@ def _functions(asm, pattern):
 
 def test_readout_m0_only_feeds_the_lds_dma(asm):
     seen = 0
-    for name, body, _ in _functions(asm, "_Z17readout_bf_kernel"):
+    for name, body, _ in _functions(asm, "_Z1[78]readout_(?:bf|h16)_kernel"):
         lines = [l.strip() for l in body.splitlines() if l.startswith("\t") and not l.strip().startswith((";", "."))]
         for k, l in enumerate(lines):
             if "m0" not in l:
@@ -47,7 +47,7 @@ def test_readout_m0_only_feeds_the_lds_dma(asm):
 
 def test_default_readout_has_no_spills(asm):
     found = False
-    for name, body, meta in _functions(asm, r"_Z17readout_bf_kernelILi32ELi2ELi8ELi6ELi1ELb1ELi2ELb1E"):
+    for name, body, meta in _functions(asm, r"_Z1(?:7readout_bf_kernelILi32ELi2ELi8ELi6ELi1ELb1ELi2ELb1E|8readout_h16_kernelILi32ELi2ELi8ELi2E)"):
         found = True
         scratch = re.search(r"ScratchSize: (\d+)", meta)
         assert scratch and int(scratch.group(1)) == 0, name
