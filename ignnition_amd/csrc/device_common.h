@@ -37,12 +37,12 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 #define MFMA_H(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
 
-// (hi, lo) fp16 pieces of the pair (a, b), packed [a | b << 16] (v_cvt_pk_f16_f32, RNE)
-__device__ __forceinline__ void split2h(float a, float b, uint32_t& hi, uint32_t& lo) {
+// (hi, lo) fp16 pieces of the pair (a, b), each packed [a | b << 16] (v_cvt_pk_f16_f32, RNE)
+struct hpair { uint32_t hi, lo; };
+__device__ __forceinline__ hpair split2h(float a, float b) {
   const h2 p = __builtin_convertvector((f2){a, b}, h2);
   const h2 q = __builtin_convertvector((f2){a - (float)p[0], b - (float)p[1]}, h2);
-  hi = __builtin_bit_cast(uint32_t, p);
-  lo = __builtin_bit_cast(uint32_t, q);
+  return {__builtin_bit_cast(uint32_t, p), __builtin_bit_cast(uint32_t, q)};
 }
 
 __device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {

@@ -400,7 +400,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
         readout_bf_supported(p->dense[0].in, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act)) {
       dp.pk_bf = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
-      if (l == 1) { dp.pk_h = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64); }
+      if (l == 1) { dp.pk_h = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64); }
     }
     if (dense_bf_supported(dp.in, dp.out)) {
       dp.pk_bfn = pk;
@@ -1317,13 +1317,13 @@ int readout(ign_plan* p, ign_batch* b) {
     // products (readout_bf); f32 (readout3): out/16 x in/4 each of 16x16x4
     const double k1 = (double)(l1.out / 16) * (l1.in / 32) + (double)(l2.out / 16) * (l2.in / 32);
     const double k1f = (double)(l1.out / 16) * (l1.in / 4) + (double)(l2.out / 16) * (l2.in / 4);
-    // variant 4: layer 1 x6, layer 2 x3 (16x16x32 f16, the bf16 rate)
-    const double kh = 6.0 * (l1.out / 16) * (l1.in / 32) + 3.0 * (l2.out / 16) * (l2.in / 32);
+    // variant 4: both layers x3 (16x16x32 f16, the bf16 rate)
+    const double kh = 3.0 * k1;
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0),
              h16 ? tiles * kh * kMfmaBf16Flops : bf ? tiles * k1 * (p->readout_variant == 3 ? 9 : 6) * kMfmaBf16Flops : 0,
              bf ? 0 : tiles * k1f * kMfmaF32Flops);
     if (h16)
-      HIP_TRY(launch_readout_h16(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_h, l1.in, st));
+      HIP_TRY(launch_readout_h16(a, p->d_packed + l2.pk_h, l1.in, st));
     else if (bf)
       HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
                                 p->readout_variant == 3 ? 9 : 6, st));

@@ -132,9 +132,9 @@ hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hi
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from
 // launch_pack_dense_bf16 (W1 natural k order, W2 chained); floats used: 3 IN OUT / 2
 bool readout_bf_supported(int din, int n1, int n2, int act1, int act2);
-// readout variant 4: layer 1 on the x6 bf16 pieces (W1f as for launch_readout_bf), layer 2 on scaled
-// 2-piece fp16 pieces of W2 (pack_readout_h16: 256 x 256 floats + 64 of header)
-hipError_t launch_readout_h16(const Readout3Args& args, const void* W1f, const void* W2h, int din, hipStream_t st);
+// readout variant 4: both layers on scaled 2-piece fp16 pieces (pack_readout_h16: W2, header, W1,
+// header; floats 256 * 256 + 64 + IN1 * 256 + 64)
+hipError_t launch_readout_h16(const Readout3Args& args, const void* Wh, int din, hipStream_t st);
 hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
                                    int n2, hipStream_t st);
 hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,

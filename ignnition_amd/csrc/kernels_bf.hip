@@ -283,10 +283,9 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e0 = 2 * q, e1 = 2 * q + 1;
-          uint32_t p0, p1;
-          split2h(h[2 * s + (e0 >> 2)][e0 & 3], h[2 * s + (e1 >> 2)][e1 & 3], p0, p1);
-          w0[q] = p0;
-          w1[q] = p1;
+          const hpair p = split2h(h[2 * s + (e0 >> 2)][e0 & 3], h[2 * s + (e1 >> 2)][e1 & 3]);
+          w0[q] = p.hi;
+          w1[q] = p.lo;
         }
         hf[0][s] = __builtin_bit_cast(h8, w0);
         hf[1][s] = __builtin_bit_cast(h8, w1);
@@ -1031,18 +1030,21 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 
 
 // ---------------------------------------------------------------------------------------------
-// Readout variant 4: readout_bf with layer 2 (256 x 256, 89 % of the MFMAs) on scaled two-piece
-// fp16 operands (device_common.h split2h, 3 products on v_mfma_f32_16x16x32_f16) instead of
-// x6 bf16.  Layer 1 stays x6 bf16.  Scales (powers of two, exact):
-// - W2 by sigma2 = 2^(15 - E(max |W2|)) at pack time (pack_readout_h16_kernel);
+// Readout variant 4: readout_bf with both layers on scaled two-piece fp16 operands
+// (device_common.h split2h, 3 products on v_mfma_f32_16x16x32_f16) instead of x6 bf16.
+// Scales (powers of two, exact):
+// - W1 by sigma1, W2 by sigma2 = 2^(15 - E(max |W|)) at pack time (pack_readout_h16_kernel);
+// - the layer-1 input of row tile t by S1_t = 2^(15 - E(mx_t)), mx_t = the tile's max |x|;
 // - the layer-2 input of row tile t by S_t, from an a-priori bound on the layer-1 activations:
 //   |W1^T x + b1| <= A mx_t + B (A = max_u sum_k |W1[k][u]|, B = max |b1|, mx_t = the tile's
 //   max |x|), and |act(z)| <= 1.0508 |z| + 1.7582 for linear / relu / selu / tanh / sigmoid,
 //   so |S_t act(z)| < 2^15 (no fp16 overflow) whatever the input scale.
-// S_t is applied where it is free: x is scaled before its (exact) bf16 split, the layer-1 bias
-// seeds the accumulator times S_t, and the activation is evaluated on the scaled value
-// (act_scaled).  Layer 2 accumulates S_t sigma2 (W2^T a + b2); its activation and the w3 dot
+// The scales are applied where they are free: layer 1 accumulates S1_t sigma1 (W1^T x + b1) (the
+// bias seeds the accumulator times S1_t sigma1), and the activation maps that scale to S_t
+// (act_scaled); layer 2 accumulates S_t sigma2 (W2^T a + b2), its activation and the w3 dot
 // product run on that scale and the row's output is unscaled once.
+// Packed buffer: [W2 pieces (chained k) | 64-float header: e(sigma2), A, B | W1 pieces (natural
+// k) | 64-float header: e(sigma1)]; floats: N1 N2 + 64 + IN1 N1 + 64.
 __global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
                                                                const float* __restrict__ W2, uint16_t* __restrict__ out,
                                                                int IN1, int N1, int N2) {
@@ -1088,41 +1090,72 @@ __global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __re
     hdr[1] = __float_as_int(red[1][0] * 1.001f);   // A, rounded up
     hdr[2] = __float_as_int(red[2][0] * 1.001f);   // B
   }
+  __syncthreads();
+  // W1: natural k order (layer 1 reads its input rows from memory), scale sigma1
+  float m1 = 0.f;
+  for (int e = threadIdx.x; e < IN1 * N1; e += blockDim.x) m1 = fmaxf(m1, fabsf(W1[e]));
+  red[0][threadIdx.x] = m1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + o]);
+    __syncthreads();
+  }
+  m1 = red[0][0];
+  int es1 = m1 > 0.f ? 15 - ((__float_as_int(m1) >> 23) - 126) : 0;
+  es1 = min(60, max(-60, es1));
+  const float sigma1 = __int_as_float((127 + es1) << 23);
+  uint16_t* o1 = out + total + 128;   // after the 64-float header
+  const int KS1 = IN1 / 32;
+  const int64_t total1 = (int64_t)(N1 / 16) * KS1 * 2 * 512;
+  for (int64_t e = threadIdx.x; e < total1; e += blockDim.x) {
+    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // (u * KS1 + s) * 2 + piece
+    const int piece = (int)(f & 1); f >>= 1;
+    const int s = (int)(f % KS1);
+    const int u = (int)(f / KS1);
+    const int k = 32 * s + 8 * (lane >> 4) + jj;   // natural k order
+    const float v = sigma1 * W1[(int64_t)k * N1 + 16 * u + (lane & 15)];
+    const _Float16 hi = (_Float16)v;
+    const _Float16 pc = piece == 0 ? hi : (_Float16)(v - (float)hi);
+    o1[e] = __builtin_bit_cast(uint16_t, pc);
+  }
+  if (threadIdx.x == 0) reinterpret_cast<int*>(o1 + total1)[0] = es1;
 }
 
-// S act(zs c) for zs = S z (S a power of two, c = 1 / S), at the cost of act(z)
+// So act(zs c) for zs = z / c (c, So powers of two), at the cost of act(z) for selu:
+// k = So c (lambda So c for selu), cl = c log2(e), laS = lambda alpha So
 template <int ACT>
-__device__ __forceinline__ float act_scaled(float zs, float c, float cl, float laS, float S) {
-  if constexpr (ACT == IGN_K_ACT_RELU) return zs > 0.f ? zs : 0.f;
-  else if constexpr (ACT == IGN_K_ACT_SELU) {   // cl = c log2(e), laS = lambda alpha S
-    const float lam = 1.0507009873554805f;
+__device__ __forceinline__ float act_scaled(float zs, float c, float k, float cl, float laS, float So) {
+  if constexpr (ACT == IGN_K_ACT_RELU) return zs > 0.f ? zs * k : 0.f;
+  else if constexpr (ACT == IGN_K_ACT_SELU) {
     const float e = __builtin_amdgcn_exp2f(fminf(zs, 0.f) * cl);
-    return zs > 0.f ? lam * zs : fmaf(laS, e, -laS);
-  } else if constexpr (ACT == IGN_K_ACT_LINEAR) return zs;
-  else return S * act_t<ACT>(zs * c);
+    return zs > 0.f ? k * zs : fmaf(laS, e, -laS);
+  } else if constexpr (ACT == IGN_K_ACT_LINEAR) return zs * k;
+  else return So * act_t<ACT>(zs * c);
 }
 
 template <int DIN, int ACT, int WAVES, int RT>
-__global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a, const bf8* __restrict__ W1f,
-                                                                  const h8* __restrict__ W2f) {
+__global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a, const h8* __restrict__ W2f) {
   constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
   constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
   constexpr int NTH = 64 * WAVES;
   constexpr int CHF = KS2 * 2 * 64;              // h8 per W2 chunk of one 16-unit tile (16 KB)
   constexpr int NCH = U2;
-  constexpr int W1F = U1 * KS1 * 3 * 64;
+  constexpr int W1F = U1 * KS1 * 2 * 64;
   static_assert(CHF % NTH == 0, "chunk layout: whole 1 KB pieces per wave");
-  constexpr float LA = 1.0507009873554805f * 1.6732632423543772f, LOG2E = 1.4426950408889634f;
+  constexpr float LAM = 1.0507009873554805f, LA = LAM * 1.6732632423543772f, LOG2E = 1.4426950408889634f;
   __shared__ h8 sw2[2][CHF];
-  __shared__ bf8 sw1[W1F];
+  __shared__ h8 sw1[W1F];
   __shared__ f4 sbias[3 * 64];   // b1 | b2 | w3
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int j = lane & 15, g = lane >> 4;
   const u4v* W2v = reinterpret_cast<const u4v*>(W2f);
+  const h8* W1f = reinterpret_cast<const h8*>(reinterpret_cast<const float*>(W2f) + N1 * 256 + 64);
   {
     const u4v* W1v = reinterpret_cast<const u4v*>(W1f);
     for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
   }
+  const int es1 = reinterpret_cast<const int*>(W1f + W1F)[0];
   for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
   for (int i = tid; i < 3 * 64; i += NTH) sbias[i] = ld4((i < 64 ? a.b1 : i < 128 ? a.b2 : a.w3) + 4 * (i & 63));
   const int* hdr = reinterpret_cast<const int*>(W2f + (int64_t)NCH * CHF);
@@ -1152,26 +1185,34 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
   for (int o = 32; o >= 1; o >>= 1)
 #pragma unroll
     for (int t = 0; t < RT; ++t) mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], o));
-  float S[RT], cS[RT], SS[RT], cSS[RT];
-  bf8 xf[RT][KS1][3];
+  float S[RT], S1S[RT], c1[RT], SS[RT], cSS[RT];
+  h8 xf[RT][KS1][2];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const float bnd = fmaf(fmaf(A1, mx[t], B1), 1.0508f, 1.7582f);
     const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(bnd)) >> 23) - 126;   // bnd < 2^E
     const int eS = 15 - E;
     S[t] = __int_as_float((127 + eS) << 23);
-    cS[t] = __int_as_float((127 - eS) << 23);
     SS[t] = __int_as_float((127 + eS + es2) << 23);
     cSS[t] = __int_as_float((127 - eS - es2) << 23);
+    // layer-1 input scale: S1 = 2^(15 - E(mx)), |x S1| < 2^15
+    const int E1 = (__builtin_amdgcn_readfirstlane(__float_as_int(fmaxf(mx[t], 1e-18f))) >> 23) - 126;
+    const int eS1 = min(60, max(-60, 15 - E1));
+    const float S1 = __int_as_float((127 + eS1) << 23);
+    S1S[t] = __int_as_float((127 + eS1 + es1) << 23);
+    c1[t] = __int_as_float((127 - eS1 - es1) << 23);
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
-      const f4 lo = xl[t][s][0] * S[t], hi = xl[t][s][1] * S[t];
-      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      split_frag(v, xf[t][s]);
+      const f4 lo = xl[t][s][0] * S1, hi = xl[t][s][1] * S1;
+      const hpair p0 = split2h(lo[0], lo[1]), p1 = split2h(lo[2], lo[3]);
+      const hpair p2 = split2h(hi[0], hi[1]), p3 = split2h(hi[2], hi[3]);
+      const u4v w0 = {p0.hi, p1.hi, p2.hi, p3.hi}, w1 = {p0.lo, p1.lo, p2.lo, p3.lo};
+      xf[t][s][0] = __builtin_bit_cast(h8, w0);
+      xf[t][s][1] = __builtin_bit_cast(h8, w1);
     }
   }
   __syncthreads();
-  // layer 1 (x6 bf16) -> S_t act(z) in accumulator layout -> the layer-2 fp16 B fragments
+  // layer 1 (x3 fp16) -> S_t act(z) in accumulator layout -> the layer-2 fp16 B fragments
   h8 hf[RT][KS2][2];
 #pragma unroll
   for (int s2 = 0; s2 < KS2; ++s2) {
@@ -1182,24 +1223,34 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
       f4 acc[RT];
       const f4 bias = sbias[4 * u + g];
 #pragma unroll
-      for (int t = 0; t < RT; ++t) acc[t] = bias * S[t];
+      for (int t = 0; t < RT; ++t) acc[t] = bias * S1S[t];
 #pragma unroll
-      for (int s = 0; s < KS1; ++s) split_mfma_rt<6, RT, KS1>(sw1 + ((u * KS1 + s) * 3) * 64 + lane, 64, xf, s, acc);
+      for (int s = 0; s < KS1; ++s) {
+        const h8 w1 = sw1[((u * KS1 + s) * 2 + 1) * 64 + lane];
+        const h8 w0 = sw1[((u * KS1 + s) * 2 + 0) * 64 + lane];
 #pragma unroll
-      for (int t = 0; t < RT; ++t)
+        for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w1, xf[t][s][0], acc[t]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w0, xf[t][s][1], acc[t]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w0, xf[t][s][0], acc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const float k = (ACT == IGN_K_ACT_SELU ? LAM : 1.0f) * S[t] * c1[t];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          v[t][4 * half + q] = act_scaled<ACT>(acc[t][q], cS[t], cS[t] * LOG2E, LA * S[t], S[t]);
+          v[t][4 * half + q] = act_scaled<ACT>(acc[t][q], c1[t], k, c1[t] * LOG2E, LA * S[t], S[t]);
+      }
     }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       u4v w0, w1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint32_t p0, p1;
-        split2h(v[t][2 * q], v[t][2 * q + 1], p0, p1);
-        w0[q] = p0;
-        w1[q] = p1;
+        const hpair p = split2h(v[t][2 * q], v[t][2 * q + 1]);
+        w0[q] = p.hi;
+        w1[q] = p.lo;
       }
       hf[t][s2][0] = __builtin_bit_cast(h8, w0);
       hf[t][s2][1] = __builtin_bit_cast(h8, w1);
@@ -1259,7 +1310,8 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
     for (int t = 0; t < RT; ++t)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        y[t] += w3[q] * act_scaled<ACT>(acc[t][q], cSS[t], cSS[t] * LOG2E, LA * SS[t], SS[t]);
+        y[t] += w3[q] * act_scaled<ACT>(acc[t][q], cSS[t], ACT == IGN_K_ACT_SELU ? LAM : 1.0f, cSS[t] * LOG2E,
+                                        LA * SS[t], SS[t]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed (for every wave: barrier)
     __syncthreads();
   }
@@ -1445,32 +1497,31 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
 
 
 template <int DIN, int ACT>
-static void readout_h16_launch(const Readout3Args& args, const bf8* w1, const h8* w2, hipStream_t st) {
+static void readout_h16_launch(const Readout3Args& args, const h8* w, hipStream_t st) {
   constexpr int WAVES = 8, RT = 2;
   auto k = readout_h16_kernel<DIN, ACT, WAVES, RT>;
   const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
-  hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w1, w2);
+  hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w);
 }
 
 template <int DIN>
-static void readout_h16_din(const Readout3Args& args, const bf8* w1, const h8* w2, hipStream_t st) {
+static void readout_h16_din(const Readout3Args& args, const h8* w, hipStream_t st) {
   switch (args.act1) {
-    case IGN_K_ACT_SELU: readout_h16_launch<DIN, IGN_K_ACT_SELU>(args, w1, w2, st); break;
-    case IGN_K_ACT_RELU: readout_h16_launch<DIN, IGN_K_ACT_RELU>(args, w1, w2, st); break;
-    case IGN_K_ACT_TANH: readout_h16_launch<DIN, IGN_K_ACT_TANH>(args, w1, w2, st); break;
-    case IGN_K_ACT_SIGMOID: readout_h16_launch<DIN, IGN_K_ACT_SIGMOID>(args, w1, w2, st); break;
-    default: readout_h16_launch<DIN, IGN_K_ACT_LINEAR>(args, w1, w2, st); break;
+    case IGN_K_ACT_SELU: readout_h16_launch<DIN, IGN_K_ACT_SELU>(args, w, st); break;
+    case IGN_K_ACT_RELU: readout_h16_launch<DIN, IGN_K_ACT_RELU>(args, w, st); break;
+    case IGN_K_ACT_TANH: readout_h16_launch<DIN, IGN_K_ACT_TANH>(args, w, st); break;
+    case IGN_K_ACT_SIGMOID: readout_h16_launch<DIN, IGN_K_ACT_SIGMOID>(args, w, st); break;
+    default: readout_h16_launch<DIN, IGN_K_ACT_LINEAR>(args, w, st); break;
   }
 }
 
-hipError_t launch_readout_h16(const Readout3Args& args, const void* W1f, const void* W2h, int din, hipStream_t st) {
+hipError_t launch_readout_h16(const Readout3Args& args, const void* Wh, int din, hipStream_t st) {
   if (args.n_rows == 0) return hipSuccess;
-  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2h || !args.b1 || !args.b2)
+  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !Wh || !args.b1 || !args.b2)
     return hipErrorInvalidValue;
-  const bf8* w1 = static_cast<const bf8*>(W1f);
-  const h8* w2 = static_cast<const h8*>(W2h);
-  if (din == 32) readout_h16_din<32>(args, w1, w2, st);
-  else readout_h16_din<64>(args, w1, w2, st);
+  const h8* w = static_cast<const h8*>(Wh);
+  if (din == 32) readout_h16_din<32>(args, w, st);
+  else readout_h16_din<64>(args, w, st);
   return hipGetLastError();
 }
 
