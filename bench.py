@@ -397,7 +397,7 @@ def main():
                                    for k, v in warm.items() if v["launches"]}}
     seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "6"))
     ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "4"))
-    sum_v = int(os.environ.get("IGN_SUM_VARIANT", "7"))
+    sum_v = int(os.environ.get("IGN_SUM_VARIANT", "8"))
     BF = "split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
     H16 = ("split-fp16: power-of-two-scaled 2-piece fp16 operands (RNE, 2^-22 relative), %d products, "
            "fp32 accumulate")
@@ -405,8 +405,10 @@ def main():
     ro_c = {1: "f32 MFMA", 2: BF % 6, 3: BF % 9, 4: "layer 1 " + BF % 6 + "; layer 2 " + H16 % 3}
     contraction = {"ordered_update_hU": seq_c.get(seq_v, "f32 MFMA") if plan.hidden[0] in (32, 64) else "f32 MFMA",
                    "readout": ro_c.get(ro_v, BF % 6),
-                   # sum variant 7 (default): split-bf16 x.W / h.U for plain sums at DIN = H = 32 or 64
-                   "sum_update": BF % 6 if plan.hidden[0] in (32, 64) and sum_v == 7 else "f32 MFMA",
+                   # sum variants 8 (default) / 7: split-fp16 / split-bf16 x.W and h.U at DIN = H = 64,
+                   # split-bf16 at 32
+                   "sum_update": (H16 % 3 if plan.hidden[0] == 64 and sum_v == 8 else BF % 6)
+                   if plan.hidden[0] in (32, 64) and sum_v in (7, 8) else "f32 MFMA",
                    "projection": "f32 MFMA"}
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,

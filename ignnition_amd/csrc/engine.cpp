@@ -131,6 +131,7 @@ int ign::repack(ign_plan* p) {
                             p->stream));
     if (cp.pk_ubf >= 0) HIP_TRY(launch_pack_u_bf16(p->d_params + cp.off_rk, p->d_packed + cp.pk_ubf, cp.H, p->stream));
     if (cp.pk_uh >= 0) HIP_TRY(launch_pack_u_f16(p->d_params + cp.off_rk, p->d_packed + cp.pk_uh, cp.H, p->stream));
+    if (cp.pk_wh >= 0) HIP_TRY(launch_pack_w_f16(p->d_params + cp.off_k, p->d_packed + cp.pk_wh, cp.din, cp.H, p->stream));
     if (cp.pk_wbf >= 0)
       HIP_TRY(launch_pack_w_bf16(p->d_params + cp.off_k, p->d_packed + cp.pk_wbf, cp.din, cp.H, p->stream));
     if (cp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
@@ -200,7 +201,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   p->device = device;
   if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(7, std::max(2, atoi(v)));
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
-  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 ? 7 : 3;
+  if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 || atoi(v) == 8 ? atoi(v) : 3;
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
@@ -388,6 +389,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     cp.pk_b = pk; pk = align(pk + 4LL * cp.H);
     if (pack_u_bf16_floats(cp.H)) { cp.pk_ubf = pk; pk = align(pk + pack_u_bf16_floats(cp.H)); }
     if (pack_u_f16_floats(cp.H)) { cp.pk_uh = pk; pk = align(pk + pack_u_f16_floats(cp.H)); }
+    if (cp.din == 64 && cp.H == 64) { cp.pk_wh = pk; pk = align(pk + pack_w_f16_floats(cp.din, cp.H)); }
     if ((cp.din == 64 && cp.H == 64) || (cp.din == 32 && cp.H == 32)) { cp.pk_wbf = pk; pk = align(pk + pack_w_bf16_floats(cp.din, cp.H)); }
   }
   for (size_t l = 0; l < p->dense.size(); ++l) {
@@ -1235,22 +1237,29 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count,
                    p->xcd_remap};
       if (mp.aggr == IGN_AGGR_ATTENTION) a.msg_w = mb.d_msg_w;
+      int sv = std::min(p->sum_variant, 7);
       if (mp.aggr == IGN_AGGR_SUM && cp.pk_wbf >= 0 && cp.pk_ubf >= 0 && mp.din == cp.din && !mp.feature_concat) {
         a.Wbf = p->d_packed + cp.pk_wbf;
         a.Ubf = p->d_packed + cp.pk_ubf;
+        if (p->sum_variant == 8 && cp.pk_wh >= 0 && cp.pk_uh >= 0) {   // split-fp16 (DIN = H = 64)
+          a.Wbf = p->d_packed + cp.pk_wh;
+          a.Ubf = p->d_packed + cp.pk_uh;
+          sv = 8;
+        }
       }
       if (mp.aggr == IGN_AGGR_CONVOLUTION) {
         a.conv_kp = p->d_packed + p->pk_conv;
         a.conv_act = mp.act;
       }
       const double frac = mb.n_dst ? (double)count / mb.n_dst : 0.0;
-      // split-bf16 GRU step (sum_gru_g32 / sum_gru_bf: x6 of x.W and h.U per 16-row tile) or f32
-      const bool bf = p->sum_variant == 7 && a.Wbf && a.Ubf && mp.din == cp.H && (cp.H == 32 || cp.H == 64);
+      // split GRU step (sum_gru_g32 / sum_gru_bf: x6 of x.W and h.U per 16-row tile, sum_gru_h16:
+      // x3) or f32
+      const bool bf = sv >= 7 && a.Wbf && a.Ubf && mp.din == cp.H && (cp.H == 32 || cp.H == 64);
       const double tiles = (double)((count + 15) / 16);
       tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac,
-               bf ? tiles * 6 * 3 * (cp.H / 16) * (mp.din / 32 + cp.H / 32) * kMfmaBf16Flops : 0,
+               bf ? tiles * (sv == 8 ? 3 : 6) * 3 * (cp.H / 16) * (mp.din / 32 + cp.H / 32) * kMfmaBf16Flops : 0,
                bf ? 0 : sum_mfma_f32(count, mp.din, cp.H));
-      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
+      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, sv, st));
       tm.end();
     }
   }

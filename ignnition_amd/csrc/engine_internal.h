@@ -91,6 +91,7 @@ struct CellP {
   int64_t pk_wt = -1, pk_ut = -1; // backward: unscaled W^T / U^T fragments (pack_a)
   int64_t pk_wbf = -1;            // split-bf16 input-kernel fragments (sum variant 7, DIN = H = 64)
   int64_t pk_ubf = -1;            // split-bf16 recurrent-kernel fragments (seq variants 4/5)
+  int64_t pk_wh = -1;             // split-fp16 input-kernel fragments + scale (sum variant 8, DIN = H = 64)
   int64_t pk_uh = -1;             // split-fp16 recurrent-kernel fragments + scale (seq variants 6/7)
   bool used = false;
 };
@@ -248,8 +249,8 @@ struct ign_plan {
                                   // MFMA; IGN_SEQ_VARIANT
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels (placement only; off:
                                   // measured slower, profiles/r02/seq_experiments)
-  int sum_variant = 7;            // sum update: 7 = split-bf16 GRU step where available (DIN = H = 32
-                                  // or 64), 3 = f32 MFMA; IGN_SUM_VARIANT
+  int sum_variant = 8;            // sum update: 8 = split-fp16 GRU step at DIN = H = 64 and split-bf16
+                                  // at 32, 7 = split-bf16 at both, 3 = f32 MFMA; IGN_SUM_VARIANT
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
   bool tsgemm_bf = true;          // weight-gradient row contractions on tsgemm_bf (IGN_TSGEMM_BF=0: f32 MFMA)
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)

@@ -101,6 +101,11 @@ hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStre
 // scale's exponent; floats used: 3 H^2 + 64
 hipError_t launch_pack_u_f16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_f16_floats(int H) { return (H == 32 || H == 64) ? 3LL * H * H + 64 : 0; }
+// [K][3H] input kernel -> the same scaled fp16 layout (K % 32 == 0) for sum variant 8
+hipError_t launch_pack_w_f16(const float* W, void* out, int K, int H, hipStream_t st);
+inline int64_t pack_w_f16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 3LL * K * H + 64 : 0; }
+// sum variant 8: the split-fp16 sum update (DIN = H = 64; Wbf / Ubf carry pack_w_f16 / pack_u_f16)
+hipError_t launch_sum_gru_h16(const SumGruArgs& args, int din, int h, hipStream_t st);
 // pieces of a [K][3H] input kernel (K % 32 == 0) for the split-bf16 sum update
 hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream_t st);
 inline int64_t pack_w_bf16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 9LL * K * H / 2 : 0; }

@@ -1001,6 +1001,7 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
 #undef SUM_CASE
   if (din == 64 && h == 64) {
     if (mode != 0) return hipErrorInvalidValue;
+    if (variant == 8 && args.Wbf && args.Ubf) return launch_sum_gru_h16(args, din, h, st);
     if (variant == 7 && args.Wbf && args.Ubf) return launch_sum_gru_bf(args, din, h, st);
     constexpr int WV = 12;   // f32 MFMA, W / U in LDS, 4 rows in flight per lane
     auto kern = sum_gru_lds_kernel<64, 64, WV, 4>;

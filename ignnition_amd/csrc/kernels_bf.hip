@@ -355,8 +355,8 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
 // U (pre-scaled as for pack_gru) -> sigma U as fp16 (hi, lo) A fragments of seq_gru_h16 (layout of
 // pack_u_bf16 with 2 pieces), then sigma's exponent as an int after them.  One block.
 __global__ __launch_bounds__(256) void pack_u_f16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out,
-                                                         int H) {
-  const int NT = H / 16, KS = H / 32, n = H * 3 * H;
+                                                         int K, int H) {
+  const int NT = H / 16, KS = K / 32, n = K * 3 * H;
   __shared__ float red[256];
   float m = 0.f;
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
@@ -546,6 +546,187 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_bf_kernel(SumGruArgs a) {
         const float rr = sig2_(ar[r]);
         const float c = tanh2_(ax[r] + rr * ah[r]);
         hn[t][r] = c + z * (h[t][r] - c);
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Variant 8 of the sum update at DIN = H = 64: sum_gru_bf with x.W and h.U on scaled two-piece
+// fp16 operands (3 products, v_mfma_f32_16x16x32_f16; device_common.h split2h): 144 MFMAs per
+// 16-row tile instead of 288, and 2 pieces to split per value instead of 3.  W and U carry
+// pack-time powers of two (sigma_W, sigma_U); the tile's message sums x and states h are scaled so
+// that both products land on ONE accumulator scale K = S_x sigma_W = S_h sigma_U, the largest with
+// |S_x x| < 2^15 and |S_h h| < 2^15 (m = f 2^E, f in [0.5, 1) -> S <= 2^(15 - E)).  The biases seed
+// the accumulators times K and the gates take c = 1 / K.
+template <int DIN, int H, int WAVES, int GU>
+__global__ __launch_bounds__(64 * WAVES) void sum_gru_h16_kernel(SumGruArgs a) {
+  constexpr int NC = DIN / 16, NT = H / 16, KX = DIN / 32, KH = H / 32;
+  constexpr int WF = 6 * NT * KX * 64, UF = 6 * NT * KH * 64;   // h8 fragments (16 B)
+  __shared__ h8 sW[WF];
+  __shared__ h8 sU[UF];
+  __shared__ float sbias[4 * H];
+  {
+    const u4v* gW = static_cast<const u4v*>(a.Wbf);
+    const u4v* gU = static_cast<const u4v*>(a.Ubf);
+    u4v* dW = reinterpret_cast<u4v*>(sW);
+    u4v* dU = reinterpret_cast<u4v*>(sU);
+    for (int i = threadIdx.x; i < WF; i += 64 * WAVES) dW[i] = gW[i];
+    for (int i = threadIdx.x; i < UF; i += 64 * WAVES) dU[i] = gU[i];
+    for (int i = threadIdx.x; i < 4 * H; i += 64 * WAVES) sbias[i] = a.bias[i];
+  }
+  const int esW = reinterpret_cast<const int*>(a.Wbf)[WF * 4];   // after the fragments (pack_u_f16)
+  const int esU = reinterpret_cast<const int*>(a.Ubf)[UF * 4];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = xcd_block(a.xcd_remap) * WAVES + wave; tile < n_tiles; tile += (int64_t)gridDim.x * WAVES) {
+    const int64_t pos = tile * 16 + j;
+    const bool valid = pos < a.n_dst;
+    const int row = valid ? a.order[pos] : 0;
+    const int64_t m0 = valid ? a.msg_ptr[pos] : 0;
+    const int64_t m1 = valid ? a.msg_ptr[pos + 1] : 0;
+    f4 h[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    f4 x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = f4{0, 0, 0, 0};
+    // the same summation order as sum_gru_bf / sum_gru_lds (GU at a time, then pairs, then singles)
+    int64_t m = m0;
+    for (; m + GU <= m1; m += GU) {
+      f4 v[GU][NC];
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const float* p = src_row_bf(a.src, a.msg_src[m + u], DIN);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[u][c] = ld4(p + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] += v[u][c];
+    }
+    for (; m + 2 <= m1; m += 2) {
+      const float* p0 = src_row_bf(a.src, a.msg_src[m], DIN);
+      const float* p1 = src_row_bf(a.src, a.msg_src[m + 1], DIN);
+      f4 v0[NC], v1[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        v0[c] = ld4(p0 + 16 * c + 4 * g);
+        v1[c] = ld4(p1 + 16 * c + 4 * g);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] = (x[c] + v0[c]) + v1[c];
+    }
+    for (; m < m1; ++m) {
+      const float* p = src_row_bf(a.src, a.msg_src[m], DIN);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) x[c] += ld4(p + 16 * c + 4 * g);
+    }
+    if (a.x_save && valid) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) st4(a.x_save + (int64_t)row * DIN + 16 * c + 4 * g, x[c]);
+    }
+    // one accumulator scale K for both products (see above)
+    float mx = 1e-18f, mh = 1e-18f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fabsf(x[c][q]));
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mh = fmaxf(mh, fabsf(h[t][q]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mx = fmaxf(mx, __shfl_xor(mx, o));
+      mh = fmaxf(mh, __shfl_xor(mh, o));
+    }
+    const int Ex = (__builtin_amdgcn_readfirstlane(__float_as_int(mx)) >> 23) - 126;
+    const int Eh = (__builtin_amdgcn_readfirstlane(__float_as_int(mh)) >> 23) - 126;
+    const int eK = min(100, min(15 - Ex + esW, 15 - Eh + esU));
+    const float Sx = __int_as_float((127 + max(-120, eK - esW)) << 23);
+    const float Sh = __int_as_float((127 + max(-120, eK - esU)) << 23);
+    const float K = __int_as_float((127 + max(-120, eK)) << 23);
+    const float c = __int_as_float((127 - max(-120, eK)) << 23);
+    h8 xf[2][KX], hf[2][KH];
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      u4v w0, w1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e0 = 2 * q, e1 = 2 * q + 1;
+        const hpair p = split2h(x[2 * s + (e0 >> 2)][e0 & 3] * Sx, x[2 * s + (e1 >> 2)][e1 & 3] * Sx);
+        w0[q] = p.hi;
+        w1[q] = p.lo;
+      }
+      xf[0][s] = __builtin_bit_cast(h8, w0);
+      xf[1][s] = __builtin_bit_cast(h8, w1);
+    }
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      u4v w0, w1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e0 = 2 * q, e1 = 2 * q + 1;
+        const hpair p = split2h(h[2 * s + (e0 >> 2)][e0 & 3] * Sh, h[2 * s + (e1 >> 2)][e1 & 3] * Sh);
+        w0[q] = p.hi;
+        w1[q] = p.lo;
+      }
+      hf[0][s] = __builtin_bit_cast(h8, w0);
+      hf[1][s] = __builtin_bit_cast(h8, w1);
+    }
+    int lofs = lane;                    // opaque: keeps the fragment reads inside the tile loop
+    asm volatile("" : "+v"(lofs));
+    f4 hn[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int u0 = 16 * t + 4 * g;
+      f4 az = *reinterpret_cast<const f4*>(sbias + 0 * H + u0) * K;
+      f4 ar = *reinterpret_cast<const f4*>(sbias + 1 * H + u0) * K;
+      f4 ax = *reinterpret_cast<const f4*>(sbias + 2 * H + u0) * K;
+      f4 ah = *reinterpret_cast<const f4*>(sbias + 3 * H + u0) * K;
+      // piece products grouped by weight piece: W lo x {hi}, W hi x {lo, hi}
+#pragma unroll
+      for (int pu = 1; pu >= 0; --pu) {
+#pragma unroll
+        for (int s = 0; s < KX; ++s) {
+          const h8 wz = sW[(((pu * 3 + 0) * NT + t) * KX + s) * 64 + lofs];
+          const h8 wr = sW[(((pu * 3 + 1) * NT + t) * KX + s) * 64 + lofs];
+          const h8 wh = sW[(((pu * 3 + 2) * NT + t) * KX + s) * 64 + lofs];
+#pragma unroll
+          for (int ph = 1 - pu; ph >= 0; --ph) {
+            az = MFMA_H(wz, xf[ph][s], az);
+            ar = MFMA_H(wr, xf[ph][s], ar);
+            ax = MFMA_H(wh, xf[ph][s], ax);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < KH; ++s) {
+          const h8 wz = sU[(((pu * 3 + 0) * NT + t) * KH + s) * 64 + lofs];
+          const h8 wr = sU[(((pu * 3 + 1) * NT + t) * KH + s) * 64 + lofs];
+          const h8 wh = sU[(((pu * 3 + 2) * NT + t) * KH + s) * 64 + lofs];
+#pragma unroll
+          for (int ph = 1 - pu; ph >= 0; --ph) {
+            az = MFMA_H(wz, hf[ph][s], az);
+            ar = MFMA_H(wr, hf[ph][s], ar);
+            ah = MFMA_H(wh, hf[ph][s], ah);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[r] * c);
+        const float rr = sig2_(ar[r] * c);
+        const float cc = tanh2_(fmaf(rr, ah[r], ax[r]) * c);
+        hn[t][r] = cc + z * (h[t][r] - cc);
       }
     }
     if (valid) {
@@ -1613,7 +1794,13 @@ hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStre
 
 hipError_t launch_pack_u_f16(const float* U, void* out, int H, hipStream_t st) {
   if (H != 32 && H != 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H);
+  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_w_f16(const float* W, void* out, int K, int H, hipStream_t st) {
+  if ((H != 32 && H != 64) || K % 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(256), 0, st, W, static_cast<uint16_t*>(out), K, H);
   return hipGetLastError();
 }
 
@@ -1629,6 +1816,16 @@ hipError_t launch_pack_w_bf16(const float* W, void* out, int K, int H, hipStream
   return hipGetLastError();
 }
 
+
+hipError_t launch_sum_gru_h16(const SumGruArgs& args, int din, int h, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  if (din != 64 || h != 64 || !args.Wbf || !args.Ubf || args.msg_w || args.conv_kp) return hipErrorInvalidValue;
+  constexpr int WV = 12;
+  auto kern = sum_gru_h16_kernel<64, 64, WV, 4>;
+  const int64_t work = (args.n_dst + 16 * WV - 1) / (16 * WV);
+  hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, work, 64 * WV)), dim3(64 * WV), 0, st, args);
+  return hipGetLastError();
+}
 
 hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;

@@ -550,12 +550,12 @@ int ign_forward_train_mp(ign_plan* p, ign_batch* b) {
           a.sum_save = mt.ss[it];
         }
         // 64-wide plain sums on the forward's default split-bf16 kernel (x_save supported); else f32
-        if (p->sum_variant == 7 && mp.aggr == IGN_AGGR_SUM && cp.pk_wbf >= 0 && cp.pk_ubf >= 0 && mp.din == cp.din &&
+        if (p->sum_variant >= 7 && mp.aggr == IGN_AGGR_SUM && cp.pk_wbf >= 0 && cp.pk_ubf >= 0 && mp.din == cp.din &&
             !mp.feature_concat) {
           a.Wbf = p->d_packed + cp.pk_wbf;
           a.Ubf = p->d_packed + cp.pk_ubf;
         }
-        HIP_TRY(launch_sum_gru(a, mp.din, cp.H, cp.H == 64 ? (a.Wbf ? 7 : 3) : p->sum_variant, st));
+        HIP_TRY(launch_sum_gru(a, mp.din, cp.H, cp.H == 64 ? (a.Wbf ? 7 : 3) : std::min(p->sum_variant, 7), st));
       }
       t->cur[mp.dst] = rec.v_in + 1;
       t->recs.push_back(rec);

@@ -360,8 +360,9 @@ def test_split_fp16_scaling(monkeypatch, hidden, scale):
 
 @pytest.mark.parametrize("model", ["synthetic64", "routenet32"])
 def test_split_bf16_sum_update_is_fp32_accurate(monkeypatch, model):
-    """Sum-update variant 7 (x.W and h.U from exact 3-piece bf16 splits, 6 piece products: the
-    default at DIN = H = 64, sum_gru_bf, and at 32, sum_gru_g32 with its code-prefetched gather)
+    """Sum-update variant 7 (x.W and h.U from exact 3-piece bf16 splits, 6 piece products:
+    sum_gru_bf at DIN = H = 64, and at 32, sum_gru_g32 with its code-prefetched gather) and
+    variant 8 (sum_gru_h16 at 64: scaled 2-piece fp16, 3 products; variant 7's kernel at 32)
     vs the f32-MFMA variant 3, on the synthetic graph's model and on RouteNet's path -> link
     update: both inside the parity tolerance vs the float64 oracle, the split form within 4x of
     the f32 error (or 1e-6); repeated runs are bitwise equal."""
@@ -373,7 +374,7 @@ def test_split_bf16_sum_update_is_fp32_accurate(monkeypatch, model):
     prm = plan.init_params(7, bias_scale=0.2)
     ref = DenseOracle(desc, dims, prm).forward(graphs)
     errs, outs = {}, {}
-    for v in ("3", "7"):
+    for v in ("3", "7", "8"):
         monkeypatch.setenv("IGN_SUM_VARIANT", v)
         eng = Engine(plan, 0)
         eng.set_params(prm)
@@ -387,6 +388,9 @@ def test_split_bf16_sum_update_is_fp32_accurate(monkeypatch, model):
     print("max scaled error vs float64 oracle (sum variant):", errs)
     assert not np.array_equal(outs["3"], outs["7"])   # the variant switch took effect
     assert errs["7"] <= max(4 * errs["3"], 1e-6), errs
+    assert errs["8"] <= max(4 * errs["3"], 1e-6), errs
+    if model == "synthetic64":
+        assert not np.array_equal(outs["7"], outs["8"])
 
 
 @pytest.mark.parametrize("window", ["0", "1", None])
