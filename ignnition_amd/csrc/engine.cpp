@@ -199,6 +199,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (d->num_entities <= 0 || d->num_entities > 8) return fail(IGN_ERR_INVALID, "1..8 entities supported");
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
+  if (const char* v = getenv("IGN_FUSE_PROJ")) p->fuse_proj = atoi(v) != 0;
   if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(7, std::max(2, atoi(v)));
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 || atoi(v) == 8 ? atoi(v) : 3;
@@ -1145,6 +1146,34 @@ static double sum_mfma_f32(int64_t n, int din, int H) {
   return (double)((n + 15) / 16) * 3 * (H / 16) * ((din + H) / 4) * kMfmaF32Flops;
 }
 
+// The ordered MP whose input projection sum MP mi can produce in its epilogue (sum_gru_g32), or -1:
+// the next MP (cyclically, within this forward) that touches mi's destination entity reads it as
+// its only source, with the projection sum_gru_g32 forms (32 -> 3 x 32, no message network, no
+// feature concat), and every row of the entity is one of mi's destinations (no halo rows).
+static int fused_proj_target(const ign_plan* p, const ign_batch* b, int mi) {
+  const MPP& mp = p->mps[mi];
+  const int e = mp.dst, n = (int)p->mps.size();
+  if (mp.sorted || mp.aggr != IGN_AGGR_SUM || mp.feature_concat || mp.din != 32 || p->cells[mp.cell].H != 32 ||
+      b->halo[e] > 0)
+    return -1;
+  for (const MsgNN& nn : mp.nn)
+    if (!nn.layers.empty()) return -1;
+  for (int k = 1; k <= n; ++k) {
+    const int m2 = (mi + k) % n;
+    if (m2 <= mi && b->fuse_last_iter) return -1;   // the next reader runs in no later iteration
+    const MPP& q = p->mps[m2];
+    bool reads = false;
+    for (const auto& sd : q.src) reads = reads || sd.entity == e;
+    if (!reads && q.dst != e) continue;
+    const CellP& qc = p->cells[q.cell];
+    if (m2 == mi || !reads || !q.sorted || q.src.size() != 1 || q.feature_concat || !q.nn[0].layers.empty() ||
+        q.din != 32 || qc.H != 32 || qc.pk_wbf < 0)
+      return -1;
+    return m2;
+  }
+  return -1;
+}
+
 int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   int rc = check_pb(p, b);
   if (rc) return rc;
@@ -1175,7 +1204,9 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   if (mp.sorted) {
     if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split is for sum MPs only");
     const int W3 = 3 * cp.H;
-    for (size_t s = 0; s < mp.src.size(); ++s) {
+    const bool projected = b->fuse_ok && b->proj_ready[mi];   // by the previous sum update's epilogue
+    if (projected) b->proj_ready[mi] = 0;
+    for (size_t s = 0; s < mp.src.size() && !projected; ++s) {
       const int64_t rs = mb.src_rows[s];
       const int sdin_t = mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : mp.din;
       tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3), 0,
@@ -1251,6 +1282,18 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
         a.conv_kp = p->d_packed + p->pk_conv;
         a.conv_act = mp.act;
       }
+      // the next ordered MP's input projection in the epilogue (sum_gru_g32 only)
+      int target = -1;
+      if (b->fuse_ok && part == IGN_PART_ALL && sv == 7 && a.Wbf && a.Ubf && mp.aggr == IGN_AGGR_SUM &&
+          count == mb.n_dst && mb.n_dst == b->rows[dst])
+        target = fused_proj_target(p, b, mi);
+      if (target >= 0) {
+        const CellP& tc = p->cells[p->mps[target].cell];
+        a.proj_out = b->mp[target].d_table + b->mp[target].src_off[0] * 3 * tc.H;
+        a.proj_W = p->d_packed + tc.pk_wbf;
+        a.proj_b = p->d_packed + tc.pk_b;
+        a.proj_bias_row = b->mp[target].d_table + b->mp[target].zero_row * 3 * tc.H;
+      }
       const double frac = mb.n_dst ? (double)count / mb.n_dst : 0.0;
       // split GRU step (sum_gru_g32 / sum_gru_bf: x6 of x.W and h.U per 16-row tile, sum_gru_h16:
       // x3) or f32
@@ -1261,6 +1304,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                bf ? 0 : sum_mfma_f32(count, mp.din, cp.H));
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, sv, st));
       tm.end();
+      if (target >= 0) b->proj_ready[target] = 1;
     }
   }
   if (part != IGN_PART_INTERIOR) b->cur[dst] ^= 1;   // GM:602: the destination state is overwritten
@@ -1368,10 +1412,15 @@ int copy_out(ign_plan* p, ign_batch* b, float* pred_out) {
 int forward_body(ign_plan* p, ign_batch* b) {
   int rc = ign_forward_begin(p, b);
   if (rc) return rc;
-  for (int it = 0; it < p->T; ++it)                     // GM:406
-    for (int mi = 0; mi < (int)p->mps.size(); ++mi)     // GM:410-414 (stages flattened in order)
-      if ((rc = ign_forward_mp(p, b, mi, IGN_PART_ALL))) return rc;
-  return readout(p, b);
+  b->proj_ready.assign(p->mps.size(), 0);
+  b->fuse_ok = p->fuse_proj;
+  for (int it = 0; it < p->T && !rc; ++it) {            // GM:406
+    b->fuse_last_iter = it + 1 == p->T;
+    for (int mi = 0; mi < (int)p->mps.size() && !rc; ++mi)   // GM:410-414 (stages flattened in order)
+      rc = ign_forward_mp(p, b, mi, IGN_PART_ALL);
+  }
+  b->fuse_ok = false;
+  return rc ? rc : readout(p, b);
 }
 
 // Capture the whole forward (init, T x MPs, readout; HIP event records included when timing is

@@ -249,6 +249,7 @@ struct ign_plan {
                                   // MFMA; IGN_SEQ_VARIANT
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels (placement only; off:
                                   // measured slower, profiles/r02/seq_experiments)
+  bool fuse_proj = true;          // sum_gru_g32 projects for the next ordered MP (IGN_FUSE_PROJ=0: off)
   int sum_variant = 8;            // sum update: 8 = split-fp16 GRU step at DIN = H = 64 and split-bf16
                                   // at 32, 7 = split-bf16 at both, 3 = f32 MFMA; IGN_SUM_VARIANT
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
@@ -288,6 +289,10 @@ struct ign_batch {
   std::vector<float*> d_state[2];               // per entity ping-pong
   std::vector<int> cur;
   std::vector<MPB> mp;
+  // forward_body only: a sum update may project its new states for the next ordered MP that reads
+  // them (fused_proj_target); proj_ready[m'] tells m' that its table is already filled
+  bool fuse_ok = false, fuse_last_iter = false;
+  std::vector<char> proj_ready;
   float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
   std::vector<float*> d_ro_tmp;                 // generic readout intermediates
   std::vector<RoBatchOp> ro;                    // readout ops

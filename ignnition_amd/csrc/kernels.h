@@ -51,6 +51,13 @@ struct SumGruArgs {
   float* sum_save = nullptr;       // training, convolution: [rows][DIN] message sums before K
   const void* Wbf = nullptr;       // split-bf16 pieces of W / U (pack_w_bf16 / pack_u_bf16): variant 7
   const void* Ubf = nullptr;
+  // sum_gru_g32 only: also project the new states for the next ordered MP that reads them
+  // (table row r = h_new[r] . W' + b', as project_kernel; split-bf16 x6): its projected table,
+  // its input kernel's pack_w_bf16 pieces and its combined pre-scaled biases
+  float* proj_out = nullptr;
+  const void* proj_W = nullptr;
+  const float* proj_b = nullptr;
+  float* proj_bias_row = nullptr;  // the table's hole row: receives proj_b alone (as project_kernel)
 };
 
 // Attention weights (AUX:287-343): per (graph, position) group of dense cells, the axis-0 softmax

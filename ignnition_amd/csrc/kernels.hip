@@ -986,6 +986,7 @@ hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, h
   // or 64); otherwise the f32-MFMA kernels
   if (din == 32 && h == 32 && mode == 0 && variant == 7 && args.Wbf && args.Ubf)
     return launch_sum_gru_g32(args, 6, st);   // 6 rows in flight: 0.100 ms vs 0.105 (8), 0.108 (4)
+  if (args.proj_out) return hipErrorInvalidValue;   // the fused projection exists in sum_gru_g32 only
 #define SUM_CASE(D, HH)                                                                    \
   if (din == D && h == HH) {                                                               \
     if (mode == 1) hipLaunchKernelGGL((sum_gru_kernel<D, HH, 1>), grid, dim3(256), 0, st, args); \

@@ -857,6 +857,28 @@ __global__ __launch_bounds__(256) void sum_gru_g32_kernel(SumGruArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, hn[t]);
   }
+  if (a.proj_out) {
+    // the next ordered MP's input projection of the new states (project_kernel's rows, formed on
+    // the split-bf16 path): hn is already in the chained B layout; W' pieces come from L2
+    if (a.proj_bias_row && blockIdx.x == 0)
+      for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) a.proj_bias_row[i] = a.proj_b[i];
+    bf8 pf[3][1];
+    split_frags<1>(hn, pf);
+    const bf8* pw = static_cast<const bf8*>(a.proj_W);
+#pragma unroll
+    for (int G = 0; G < 3; ++G)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        f4 acc = ld4(a.proj_b + G * H + 16 * i + 4 * g);
+#pragma unroll
+        for (int pu = 2; pu >= 0; --pu) {
+          const bf8 w = pw[((pu * 3 + G) * NT + i) * 64 + lane];
+#pragma unroll
+          for (int ph = 2 - pu; ph >= 0; --ph) acc = MFMA_BF(w, pf[ph][0], acc);
+        }
+        if (valid) st4(a.proj_out + (int64_t)row * 3 * H + G * H + 16 * i + 4 * g, acc);
+      }
+  }
 }
 
 hipError_t launch_sum_gru_g32(const SumGruArgs& args, int gu, hipStream_t st) {

@@ -358,6 +358,39 @@ def test_split_fp16_scaling(monkeypatch, hidden, scale):
         assert v <= max(4 * errs["2/1"], 1e-6), errs
 
 
+@pytest.mark.parametrize("order", ["routenet", "sum_first"])
+def test_fused_projection_matches_oracle(monkeypatch, order):
+    """The 32-wide sum update projects its new states for the next ordered MP that reads them
+    (sum_gru_g32's epilogue, IGN_FUSE_PROJ, default on): in RouteNet the link states of
+    iteration t feed iteration t+1's path update; with the stages swapped the sum update runs
+    first and the ordered update reads its result in the same iteration (the epilogue then also
+    writes the table's hole row).  Fused and unfused forwards both match the float64 oracle, are
+    deterministic, and differ (the switch took effect: the projection runs on split-bf16 instead
+    of f32 MFMA)."""
+    desc = model_examples.routenet(hidden=32, iterations=4)
+    if order == "sum_first":
+        desc["message_passing"]["stages"] = desc["message_passing"]["stages"][::-1]
+    _, dims, _ = workloads.model("routenet")
+    mi = Model_information(copy.deepcopy(desc), dims)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", g) for g in range(3)])
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(13, bias_scale=0.2)
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("IGN_FUSE_PROJ", v)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        out = b.forward().reshape(-1)
+        np.testing.assert_array_equal(out, b.forward().reshape(-1))
+        b.close()
+        eng.close()
+        _close(out, ref)
+        outs[v] = out
+    assert not np.array_equal(outs["0"], outs["1"])
+
+
 @pytest.mark.parametrize("model", ["synthetic64", "routenet32"])
 def test_split_bf16_sum_update_is_fp32_accurate(monkeypatch, model):
     """Sum-update variant 7 (x.W and h.U from exact 3-piece bf16 splits, 6 piece products:
