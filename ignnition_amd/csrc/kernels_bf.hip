@@ -1248,12 +1248,16 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 // product run on that scale and the row's output is unscaled once.
 // Packed buffer: [W2 pieces (chained k) | 64-float header: e(sigma2), A, B | W1 pieces (natural
 // k) | 64-float header: e(sigma1)]; floats: N1 N2 + 64 + IN1 N1 + 64.
+// Scales of the packed buffer (one block): headers after the W2 and W1 pieces.  The pieces
+// themselves are written by pack_readout_h16_frag_kernel over a full grid (the repack after every
+// optimizer step must stay cheap).
 __global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
                                                                const float* __restrict__ W2, uint16_t* __restrict__ out,
                                                                int IN1, int N1, int N2) {
-  __shared__ float red[3][256];
-  float m2 = 0.f, a1 = 0.f, bb = 0.f;
+  __shared__ float red[4][256];
+  float m2 = 0.f, a1 = 0.f, bb = 0.f, m1 = 0.f;
   for (int e = threadIdx.x; e < N1 * N2; e += blockDim.x) m2 = fmaxf(m2, fabsf(W2[e]));
+  for (int e = threadIdx.x; e < IN1 * N1; e += blockDim.x) m1 = fmaxf(m1, fabsf(W1[e]));
   for (int u = threadIdx.x; u < N1; u += blockDim.x) {
     float l1 = 0.f;
     for (int k = 0; k < IN1; ++k) l1 += fabsf(W1[(int64_t)k * N1 + u]);
@@ -1263,66 +1267,54 @@ __global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __re
   red[0][threadIdx.x] = m2;
   red[1][threadIdx.x] = a1;
   red[2][threadIdx.x] = bb;
+  red[3][threadIdx.x] = m1;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o)
-      for (int q = 0; q < 3; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + o]);
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + o]);
     __syncthreads();
-  }
-  m2 = red[0][0];
-  int es = m2 > 0.f ? 15 - ((__float_as_int(m2) >> 23) - 126) : 0;
-  es = min(100, max(-100, es));
-  const float sigma = __int_as_float((127 + es) << 23);
-  const int KS = N1 / 32;
-  const int64_t total = (int64_t)(N2 / 16) * KS * 2 * 512;
-  for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
-    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
-    int64_t f = e >> 9;                       // (u * KS + s) * 2 + piece
-    const int piece = (int)(f & 1); f >>= 1;
-    const int s = (int)(f % KS);
-    const int u = (int)(f / KS);
-    const int k = 16 * (2 * s + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);   // chained k order
-    const float v = sigma * W2[(int64_t)k * N2 + 16 * u + (lane & 15)];
-    const _Float16 hi = (_Float16)v;
-    const _Float16 pc = piece == 0 ? hi : (_Float16)(v - (float)hi);
-    out[e] = __builtin_bit_cast(uint16_t, pc);
   }
   if (threadIdx.x == 0) {
-    int* hdr = reinterpret_cast<int*>(out + total);
-    hdr[0] = es;
+    m2 = red[0][0];
+    m1 = red[3][0];
+    const int es2 = m2 > 0.f ? min(100, max(-100, 15 - ((__float_as_int(m2) >> 23) - 126))) : 0;
+    const int es1 = m1 > 0.f ? min(60, max(-60, 15 - ((__float_as_int(m1) >> 23) - 126))) : 0;
+    const int64_t total2 = (int64_t)N1 * N2 * 2;   // halves of the W2 pieces
+    int* hdr = reinterpret_cast<int*>(out + total2);
+    hdr[0] = es2;
     hdr[1] = __float_as_int(red[1][0] * 1.001f);   // A, rounded up
     hdr[2] = __float_as_int(red[2][0] * 1.001f);   // B
+    reinterpret_cast<int*>(out + total2 + 128 + (int64_t)IN1 * N1 * 2)[0] = es1;
   }
-  __syncthreads();
-  // W1: natural k order (layer 1 reads its input rows from memory), scale sigma1
-  float m1 = 0.f;
-  for (int e = threadIdx.x; e < IN1 * N1; e += blockDim.x) m1 = fmaxf(m1, fabsf(W1[e]));
-  red[0][threadIdx.x] = m1;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + o]);
-    __syncthreads();
-  }
-  m1 = red[0][0];
-  int es1 = m1 > 0.f ? 15 - ((__float_as_int(m1) >> 23) - 126) : 0;
-  es1 = min(60, max(-60, es1));
-  const float sigma1 = __int_as_float((127 + es1) << 23);
-  uint16_t* o1 = out + total + 128;   // after the 64-float header
-  const int KS1 = IN1 / 32;
-  const int64_t total1 = (int64_t)(N1 / 16) * KS1 * 2 * 512;
-  for (int64_t e = threadIdx.x; e < total1; e += blockDim.x) {
-    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
-    int64_t f = e >> 9;                       // (u * KS1 + s) * 2 + piece
+}
+
+// W2 pieces (chained k order, as readout_bf's layer 2) and W1 pieces (natural k order: layer 1
+// reads its input rows from memory), each scaled by its header's power of two
+__global__ __launch_bounds__(256) void pack_readout_h16_frag_kernel(const float* __restrict__ W1,
+                                                                    const float* __restrict__ W2,
+                                                                    uint16_t* __restrict__ out, int IN1, int N1,
+                                                                    int N2) {
+  const int64_t total2 = (int64_t)N1 * N2 * 2, total1 = (int64_t)IN1 * N1 * 2;
+  uint16_t* o1 = out + total2 + 128;
+  const float sigma2 = __int_as_float((127 + reinterpret_cast<const int*>(out + total2)[0]) << 23);
+  const float sigma1 = __int_as_float((127 + reinterpret_cast<const int*>(o1 + total1)[0]) << 23);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total2 + total1;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const bool l2 = e < total2;
+    const int64_t ee = l2 ? e : e - total2;
+    const int jj = (int)(ee & 7), lane = (int)((ee >> 3) & 63);
+    int64_t f = ee >> 9;                       // (u * KS + s) * 2 + piece
     const int piece = (int)(f & 1); f >>= 1;
-    const int s = (int)(f % KS1);
-    const int u = (int)(f / KS1);
-    const int k = 32 * s + 8 * (lane >> 4) + jj;   // natural k order
-    const float v = sigma1 * W1[(int64_t)k * N1 + 16 * u + (lane & 15)];
+    const int KS = (l2 ? N1 : IN1) / 32;
+    const int s = (int)(f % KS);
+    const int u = (int)(f / KS);
+    const int k = l2 ? 16 * (2 * s + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3) : 32 * s + 8 * (lane >> 4) + jj;
+    const float v = l2 ? sigma2 * W2[(int64_t)k * N2 + 16 * u + (lane & 15)]
+                       : sigma1 * W1[(int64_t)k * N1 + 16 * u + (lane & 15)];
     const _Float16 hi = (_Float16)v;
     const _Float16 pc = piece == 0 ? hi : (_Float16)(v - (float)hi);
-    o1[e] = __builtin_bit_cast(uint16_t, pc);
+    (l2 ? out : o1)[ee] = __builtin_bit_cast(uint16_t, pc);
   }
-  if (threadIdx.x == 0) reinterpret_cast<int*>(o1 + total1)[0] = es1;
 }
 
 // So act(zs c) for zs = z / c (c, So powers of two), at the cost of act(z) for selu:
@@ -1732,6 +1724,8 @@ hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float
                                    int n2, hipStream_t st) {
   if (n1 != 256 || n2 != 256 || in1 % 32) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pack_readout_h16_kernel, dim3(1), dim3(256), 0, st, W1, b1, W2, static_cast<uint16_t*>(out), in1,
+                     n1, n2);
+  hipLaunchKernelGGL(pack_readout_h16_frag_kernel, dim3(128), dim3(256), 0, st, W1, W2, static_cast<uint16_t*>(out), in1,
                      n1, n2);
   return hipGetLastError();
 }
