@@ -354,10 +354,10 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
 
 // U (pre-scaled as for pack_gru) -> sigma U as fp16 (hi, lo) A fragments of seq_gru_h16 (layout of
 // pack_u_bf16 with 2 pieces), then sigma's exponent as an int after them.  One block.
-__global__ __launch_bounds__(256) void pack_u_f16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out,
+__global__ __launch_bounds__(1024) void pack_u_f16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out,
                                                          int K, int H) {
   const int NT = H / 16, KS = K / 32, n = K * 3 * H;
-  __shared__ float red[256];
+  __shared__ float red[1024];
   float m = 0.f;
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
     const float sc = (e % (3 * H)) >= 2 * H ? IGN_2LOG2E : IGN_NLOG2E;
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void pack_u_f16_kernel(const float* __restrict
   }
   red[threadIdx.x] = m;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
     __syncthreads();
   }
@@ -1251,10 +1251,10 @@ __global__ __launch_bounds__(64 * WAVES) void readout_bf_kernel(Readout3Args a, 
 // Scales of the packed buffer (one block): headers after the W2 and W1 pieces.  The pieces
 // themselves are written by pack_readout_h16_frag_kernel over a full grid (the repack after every
 // optimizer step must stay cheap).
-__global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
+__global__ __launch_bounds__(1024) void pack_readout_h16_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
                                                                const float* __restrict__ W2, uint16_t* __restrict__ out,
                                                                int IN1, int N1, int N2) {
-  __shared__ float red[4][256];
+  __shared__ float red[4][1024];
   float m2 = 0.f, a1 = 0.f, bb = 0.f, m1 = 0.f;
   for (int e = threadIdx.x; e < N1 * N2; e += blockDim.x) m2 = fmaxf(m2, fabsf(W2[e]));
   for (int e = threadIdx.x; e < IN1 * N1; e += blockDim.x) m1 = fmaxf(m1, fabsf(W1[e]));
@@ -1269,7 +1269,7 @@ __global__ __launch_bounds__(256) void pack_readout_h16_kernel(const float* __re
   red[2][threadIdx.x] = bb;
   red[3][threadIdx.x] = m1;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o)
       for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + o]);
     __syncthreads();
@@ -1723,7 +1723,7 @@ hipError_t launch_readout_h16(const Readout3Args& args, const void* Wh, int din,
 hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
                                    int n2, hipStream_t st) {
   if (n1 != 256 || n2 != 256 || in1 % 32) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_readout_h16_kernel, dim3(1), dim3(256), 0, st, W1, b1, W2, static_cast<uint16_t*>(out), in1,
+  hipLaunchKernelGGL(pack_readout_h16_kernel, dim3(1), dim3(1024), 0, st, W1, b1, W2, static_cast<uint16_t*>(out), in1,
                      n1, n2);
   hipLaunchKernelGGL(pack_readout_h16_frag_kernel, dim3(128), dim3(256), 0, st, W1, W2, static_cast<uint16_t*>(out), in1,
                      n1, n2);
@@ -1810,13 +1810,13 @@ hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStre
 
 hipError_t launch_pack_u_f16(const float* U, void* out, int H, hipStream_t st) {
   if (H != 32 && H != 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(256), 0, st, U, static_cast<uint16_t*>(out), H, H);
+  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(1024), 0, st, U, static_cast<uint16_t*>(out), H, H);
   return hipGetLastError();
 }
 
 hipError_t launch_pack_w_f16(const float* W, void* out, int K, int H, hipStream_t st) {
   if ((H != 32 && H != 64) || K % 32) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(256), 0, st, W, static_cast<uint16_t*>(out), K, H);
+  hipLaunchKernelGGL(pack_u_f16_kernel, dim3(1), dim3(1024), 0, st, W, static_cast<uint16_t*>(out), K, H);
   return hipGetLastError();
 }
 
