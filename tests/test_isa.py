@@ -1,4 +1,4 @@
-"""ISA checks of the readout kernel (CPU: hipcc cross-compiles gfx950 to assembly, no GPU).
+"""ISA checks of the readout and ordered-update kernels (CPU: hipcc cross-compiles gfx950 to assembly, no GPU).
 
 readout_bf_kernel and readout_h16_kernel issue their W2-chunk LDS-DMA as inline asm that loads M0, a register the compiler
 reserves (csrc/kernels_bf.hip): that is only sound while nothing else in the kernel uses M0.  The
@@ -50,5 +50,19 @@ def test_default_readout_has_no_spills(asm):
     for name, body, meta in _functions(asm, r"_Z1(?:7readout_bf_kernelILi32ELi2ELi8ELi6ELi1ELb1ELi2ELb1E|8readout_h16_kernelILi32ELi2ELi8ELi2E)"):
         found = True
         scratch = re.search(r"ScratchSize: (\d+)", meta)
+        assert scratch and int(scratch.group(1)) == 0, name
+    assert found
+
+
+def test_default_ordered_update_keeps_four_waves(asm):
+    """seq_gru_h16<32, 3> (the default ordered update) at 4 waves per SIMD: at most 128 VGPRs and
+    no scratch; 5-6 waves (fewer registers) and 3 waves (a register prefetch) both measured slower
+    (DESIGN.md §3b')."""
+    found = False
+    for name, body, meta in _functions(asm, r"_Z18seq_gru_h16_kernelILi32ELi3E"):
+        found = True
+        vgpr = re.search(r"NumVgprs: (\d+)", meta)
+        scratch = re.search(r"ScratchSize: (\d+)", meta)
+        assert vgpr and int(vgpr.group(1)) <= 128, (name, vgpr and vgpr.group(1))
         assert scratch and int(scratch.group(1)) == 0, name
     assert found
