@@ -172,6 +172,10 @@ int ign::repack(ign_plan* p) {
       HIP_TRY(launch_pack_dense_bf16(p->d_params + dp.off_w, p->d_packed + dp.pk_bfn, dp.in, dp.out, 0, p->stream));
     if (dp.pk_bft >= 0)
       HIP_TRY(launch_pack_dense_bf16_t(p->d_params + dp.off_w, p->d_packed + dp.pk_bft, dp.in, dp.out, p->stream));
+    if (dp.pk_hn >= 0)
+      HIP_TRY(launch_pack_dense_f16(p->d_params + dp.off_w, p->d_packed + dp.pk_hn, dp.in, dp.out, 0, p->stream));
+    if (dp.pk_ht >= 0)
+      HIP_TRY(launch_pack_dense_f16(p->d_params + dp.off_w, p->d_packed + dp.pk_ht, dp.out, dp.in, 1, p->stream));
   }
   for (auto& dp : p->dense)
     if (dp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + dp.off_w, dp.in, dp.out, p->d_packed + dp.pk_wt, p->stream));
@@ -206,6 +210,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
+  if (const char* v = getenv("IGN_TRAIN_DENSE_H16")) p->train_dense_h16 = atoi(v) != 0;
   if (const char* v = getenv("IGN_TSGEMM_BF")) p->tsgemm_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(4, std::max(1, atoi(v)));
@@ -408,10 +413,14 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     if (dense_bf_supported(dp.in, dp.out)) {
       dp.pk_bfn = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
+      dp.pk_hn = pk;
+      pk = align(pk + (int64_t)dp.in * dp.out + 64);
     }
     if (dense_bf_supported(dp.out, dp.in)) {
       dp.pk_bft = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
+      dp.pk_ht = pk;
+      pk = align(pk + (int64_t)dp.in * dp.out + 64);
     }
   }
   // backward fragments (training): W^T / U^T per cell, W^T per Dense layer where the MFMA

@@ -105,6 +105,7 @@ struct DenseP {
   int64_t pk_h = -1;              // fused readout, layer 2: scaled split-fp16 fragments (readout variant 4)
   int64_t pk_bfn = -1;            // training forward: split-bf16 pieces, natural k (dense_bf)
   int64_t pk_bft = -1;            // training backward: split-bf16 pieces of W^T (dense_bf_t)
+  int64_t pk_hn = -1, pk_ht = -1;  // training: scaled split-fp16 pieces of W / W^T (dense_h16)
 };
 
 struct MsgNN {                    // message-creation network of one MP source (GM:440-475)
@@ -253,6 +254,7 @@ struct ign_plan {
   int sum_variant = 8;            // sum update: 8 = split-fp16 GRU step at DIN = H = 64 and split-bf16
                                   // at 32, 7 = split-bf16 at both, 3 = f32 MFMA; IGN_SUM_VARIANT
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
+  bool train_dense_h16 = true;    // ... on the split-fp16 form of dense_bf (IGN_TRAIN_DENSE_H16=0: split-bf16)
   bool tsgemm_bf = true;          // weight-gradient row contractions on tsgemm_bf (IGN_TSGEMM_BF=0: f32 MFMA)
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)

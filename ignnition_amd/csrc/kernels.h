@@ -162,6 +162,14 @@ hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const
 hipError_t launch_dense_bf_t(const float* dz, int64_t n, int K, const void* Wtbf, int M, float* out, int accumulate,
                              int act, const float* aprev, hipStream_t st);
 hipError_t launch_pack_dense_bf16_t(const float* W, void* out, int IN, int OUT, hipStream_t st);
+// the same two row GEMMs on scaled split-fp16 (x3; DESIGN.md §3b'): W pieces from
+// launch_pack_dense_f16 (IN x OUT natural k, trans = 1 for W^T: IN = OUT_orig, OUT = IN_orig);
+// floats used: IN * OUT + 64
+hipError_t launch_dense_h16(const float* x, int64_t n, int K, int x_stride, const void* Wh, const float* bias, int M,
+                            int act, float* y, hipStream_t st);
+hipError_t launch_dense_h16_t(const float* dz, int64_t n, int K, const void* Wth, int M, float* out, int accumulate,
+                              int act, const float* aprev, hipStream_t st);
+hipError_t launch_pack_dense_f16(const float* W, void* out, int IN, int OUT, int trans, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
                                 int out, int act, float* y, hipStream_t st);
 hipError_t launch_concat_cols(float* dst, int64_t n, int dst_stride, int col0, const float* src, int width,

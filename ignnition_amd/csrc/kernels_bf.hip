@@ -1545,33 +1545,65 @@ __device__ __forceinline__ float act_grad_out(float a, int act) {   // act' thro
 // registers (K / 32 x 3 fragments per tile) and writes act(acc) as 16 B per lane.
 // BWD: the backward row GEMM instead, y[r] (+)= (x[r] . W^T) * act'(aprev[r]) with W^T packed
 // (row_gemm_t's contract; bias unused, ACT = the activation whose derivative is applied).
-template <int KS, int G, int ACT, bool BWD = false>
+template <int KS, int G, int ACT, bool BWD = false, int NP = 3>
 __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__ x, int64_t n, int x_stride,
-                                                       const bf8* __restrict__ Wf, const float* __restrict__ bias,
+                                                       const void* __restrict__ Wf, const float* __restrict__ bias,
                                                        int M, float* __restrict__ y, const float* __restrict__ aprev,
                                                        int accumulate) {
   constexpr int WAVES = 8, RT = 2, NTH = 64 * WAVES;
-  constexpr int CHF = G * KS * 3 * 64;   // bf8 per stage
+  // NP = 3: split-bf16 x6; NP = 2: scaled split-fp16 x3 (W pieces carry sigma = 2^es after the
+  // fragments, each 16-row tile of x its own S = 2^(15 - E(max |x|)); DESIGN.md §3b')
+  constexpr int CHF = G * KS * NP * 64;   // 16-B fragments per stage
   constexpr int PER = (CHF + NTH - 1) / NTH;
-  __shared__ bf8 sw[2][CHF];
+  __shared__ u4v sw[2][CHF];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int j = lane & 15, g = lane >> 4;
   const u4v* Wv = reinterpret_cast<const u4v*>(Wf);
   const int NV = M / (16 * G);
-  for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw[0])[i] = Wv[i];
+  for (int i = tid; i < CHF; i += NTH) sw[0][i] = Wv[i];
   const int64_t r0 = ((int64_t)blockIdx.x * WAVES + wave) * (16 * RT) + j;
   bf8 xf[RT][KS][3];
+  h8 xh[RT][KS][2];
+  float cS[RT], KSig[RT];   // NP = 2: 1 / (S sigma) and S sigma per row tile
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const int64_t r = r0 + 16 * t;
     const bool ok = r < n;
     const float* xr = x + (ok ? r : 0) * (int64_t)x_stride;
+    if constexpr (NP == 3) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
-      const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
-      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      split_frag(v, xf[t][s]);
+      for (int s = 0; s < KS; ++s) {
+        const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+        const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+        const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        split_frag(v, xf[t][s]);
+      }
+    } else {
+      f4 xv[KS][2];
+      float mx = 1e-18f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        xv[s][0] = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+        xv[s][1] = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fmaxf(fabsf(xv[s][0][q]), fabsf(xv[s][1][q])));
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      const int es = reinterpret_cast<const int*>(Wv + (int64_t)(M / 16) * KS * 2 * 64)[0];
+      const int eS = min(60, max(-60, 15 - ((__builtin_amdgcn_readfirstlane(__float_as_int(mx)) >> 23) - 126)));
+      const float S = __int_as_float((127 + eS) << 23);
+      KSig[t] = __int_as_float((127 + eS + es) << 23);
+      cS[t] = __int_as_float((127 - eS - es) << 23);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const f4 lo = xv[s][0] * S, hi = xv[s][1] * S;
+        const hpair p0 = split2h(lo[0], lo[1]), p1 = split2h(lo[2], lo[3]);
+        const hpair p2 = split2h(hi[0], hi[1]), p3 = split2h(hi[2], hi[3]);
+        const u4v w0 = {p0.hi, p1.hi, p2.hi, p3.hi}, w1 = {p0.lo, p1.lo, p2.lo, p3.lo};
+        xh[t][s][0] = __builtin_bit_cast(h8, w0);
+        xh[t][s][1] = __builtin_bit_cast(h8, w1);
+      }
     }
   }
   __syncthreads();
@@ -1596,9 +1628,26 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
       const f4 b = bias ? ld4(bias + 16 * u + 4 * g) : f4{0, 0, 0, 0};
       f4 acc[RT];
 #pragma unroll
-      for (int t = 0; t < RT; ++t) acc[t] = b;
+      for (int t = 0; t < RT; ++t) acc[t] = NP == 3 ? b : b * KSig[t];
+      if constexpr (NP == 3) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) split_mfma_rt<6, RT, KS>(sw[cur] + (c * KS + s) * 3 * 64 + lofs, 64, xf, s, acc);
+        for (int s = 0; s < KS; ++s)
+          split_mfma_rt<6, RT, KS>(reinterpret_cast<const bf8*>(sw[cur]) + (c * KS + s) * 3 * 64 + lofs, 64, xf, s, acc);
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const h8* wb = reinterpret_cast<const h8*>(sw[cur]) + (c * KS + s) * 2 * 64 + lofs;
+          const h8 w0 = wb[0], w1 = wb[64];
+#pragma unroll
+          for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w1, xh[t][s][0], acc[t]);
+#pragma unroll
+          for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w0, xh[t][s][1], acc[t]);
+#pragma unroll
+          for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w0, xh[t][s][0], acc[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] *= cS[t];
+      }
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         const int64_t r = r0 + 16 * t;
@@ -1621,7 +1670,7 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
         const int i = tid + NTH * q;
-        if (CHF % NTH == 0 || i < CHF) reinterpret_cast<u4v*>(sw[cur ^ 1])[i] = stage[q];
+        if (CHF % NTH == 0 || i < CHF) sw[cur ^ 1][i] = stage[q];
       }
     }
     __syncthreads();
@@ -1734,11 +1783,11 @@ bool dense_bf_supported(int K, int M) {
   return (K == 32 || K == 64 || K == 128 || K == 256) && M % 128 == 0 && M > 0;
 }
 
-template <int KS, int G, bool BWD>
-static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const bf8* W, const float* bias, int M, int act,
+template <int KS, int G, bool BWD, int NP>
+static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const void* W, const float* bias, int M, int act,
                               float* y, const float* aprev, int accumulate, hipStream_t st) {
   const dim3 grid((unsigned)((n + 255) / 256)), block(512);
-#define DBF(A) hipLaunchKernelGGL((dense_bf_kernel<KS, G, A, BWD>), grid, block, 0, st, x, n, x_stride, W, bias, M, y, aprev, accumulate)
+#define DBF(A) hipLaunchKernelGGL((dense_bf_kernel<KS, G, A, BWD, NP>), grid, block, 0, st, x, n, x_stride, W, bias, M, y, aprev, accumulate)
   switch (act) {
     case IGN_K_ACT_SELU: DBF(IGN_K_ACT_SELU); break;
     case IGN_K_ACT_RELU: DBF(IGN_K_ACT_RELU); break;
@@ -1750,15 +1799,15 @@ static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const bf8
   return hipGetLastError();
 }
 
-template <bool BWD>
-static hipError_t dense_bf_any(const float* x, int64_t n, int K, int x_stride, const bf8* W, const float* bias, int M,
+template <bool BWD, int NP = 3>
+static hipError_t dense_bf_any(const float* x, int64_t n, int K, int x_stride, const void* W, const float* bias, int M,
                                int act, float* y, const float* aprev, int accumulate, hipStream_t st) {
-  // stages of <= 24 KB: G 16-unit tiles of K x 16 x 3 pieces (M % 128 == 0: G divides M / 16)
+  // stages of <= 24 KB: G 16-unit tiles of K x 16 x NP pieces (M % 128 == 0: G divides M / 16)
   switch (K) {
-    case 32: return dense_bf_ks<1, 8, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-    case 64: return dense_bf_ks<2, 4, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-    case 128: return dense_bf_ks<4, 2, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-    default: return dense_bf_ks<8, 1, BWD>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    case 64: return dense_bf_ks<2, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    case 128: return dense_bf_ks<4, 2, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    default: return dense_bf_ks<8, 1, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
   }
 }
 
@@ -1766,14 +1815,77 @@ hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const
                            int act, float* y, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (!dense_bf_supported(K, M) || x_stride % 4 || !Wbf) return hipErrorInvalidValue;
-  return dense_bf_any<false>(x, n, K, x_stride, static_cast<const bf8*>(Wbf), bias, M, act, y, nullptr, 0, st);
+  return dense_bf_any<false>(x, n, K, x_stride, Wbf, bias, M, act, y, nullptr, 0, st);
+}
+
+hipError_t launch_dense_h16(const float* x, int64_t n, int K, int x_stride, const void* Wh, const float* bias, int M,
+                            int act, float* y, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!dense_bf_supported(K, M) || x_stride % 4 || !Wh) return hipErrorInvalidValue;
+  return dense_bf_any<false, 2>(x, n, K, x_stride, Wh, bias, M, act, y, nullptr, 0, st);
+}
+
+hipError_t launch_dense_h16_t(const float* dz, int64_t n, int K, const void* Wth, int M, float* out, int accumulate,
+                              int act, const float* aprev, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!dense_bf_supported(K, M) || !Wth) return hipErrorInvalidValue;
+  return dense_bf_any<true, 2>(dz, n, K, K, Wth, nullptr, M, act < 0 ? IGN_K_ACT_LINEAR : act, out,
+                               act < 0 ? nullptr : aprev, accumulate, st);
+}
+
+// Scaled fp16 pieces of a Dense kernel for dense_bf_kernel<.., NP = 2> (natural k; trans: of W^T),
+// layout (u * KS + s) * 2 + piece, then sigma's exponent: one block for the scale, a grid for the pieces
+__global__ __launch_bounds__(1024) void dense_f16_scale_kernel(const float* __restrict__ W, int64_t nel,
+                                                               int* __restrict__ hdr) {
+  __shared__ float red[1024];
+  float m = 0.f;
+  for (int64_t e = threadIdx.x; e < nel; e += blockDim.x) m = fmaxf(m, fabsf(W[e]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    hdr[0] = red[0] > 0.f ? min(60, max(-60, 15 - ((__float_as_int(red[0]) >> 23) - 126))) : 0;
+}
+
+__global__ void pack_dense_f16_kernel(const float* __restrict__ W, uint16_t* __restrict__ out, int IN, int OUT,
+                                      int trans) {
+  const int KS = IN / 32;
+  const int64_t total = (int64_t)(OUT / 16) * KS * 2 * 512;
+  const float sigma = __int_as_float((127 + reinterpret_cast<const int*>(out + total)[0]) << 23);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;                       // (u * KS + s) * 2 + piece
+    const int piece = (int)(f & 1); f >>= 1;
+    const int s = (int)(f % KS);
+    const int u = (int)(f / KS);
+    const int k = 32 * s + 8 * (lane >> 4) + jj;
+    const int nn = 16 * u + (lane & 15);
+    const float v = sigma * (trans ? W[(int64_t)nn * IN + k] : W[(int64_t)k * OUT + nn]);
+    const _Float16 hi = (_Float16)v;
+    const _Float16 pc = piece == 0 ? hi : (_Float16)(v - (float)hi);
+    out[e] = __builtin_bit_cast(uint16_t, pc);
+  }
+}
+
+hipError_t launch_pack_dense_f16(const float* W, void* out, int IN, int OUT, int trans, hipStream_t st) {
+  // trans: pieces of W^T for launch_dense_h16_t (W is [OUT][IN] as seen by the contraction)
+  if (IN % 32 || OUT % 16) return hipErrorInvalidValue;
+  uint16_t* o = static_cast<uint16_t*>(out);
+  const int64_t total = (int64_t)(OUT / 16) * (IN / 32) * 2 * 512;
+  hipLaunchKernelGGL(dense_f16_scale_kernel, dim3(1), dim3(1024), 0, st, W, (int64_t)IN * OUT,
+                     reinterpret_cast<int*>(o + total));
+  hipLaunchKernelGGL(pack_dense_f16_kernel, dim3(128), dim3(256), 0, st, W, o, IN, OUT, trans);
+  return hipGetLastError();
 }
 
 hipError_t launch_dense_bf_t(const float* dz, int64_t n, int K, const void* Wtbf, int M, float* out, int accumulate,
                              int act, const float* aprev, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (!dense_bf_supported(K, M) || !Wtbf) return hipErrorInvalidValue;
-  return dense_bf_any<true>(dz, n, K, K, static_cast<const bf8*>(Wtbf), nullptr, M, act < 0 ? IGN_K_ACT_LINEAR : act,
+  return dense_bf_any<true>(dz, n, K, K, Wtbf, nullptr, M, act < 0 ? IGN_K_ACT_LINEAR : act,
                             out, act < 0 ? nullptr : aprev, accumulate, st);
 }
 

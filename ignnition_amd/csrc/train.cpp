@@ -595,7 +595,10 @@ int ign_forward_train_end(ign_plan* p, ign_batch* b, float* pred_out) {
   for (size_t l = 0; l < p->dense.size(); ++l) {
     const DenseP& d = p->dense[l];
     float* o = l + 1 == p->dense.size() ? b->d_pred : t->act[l];
-    if (p->train_dense_bf && d.pk_bfn >= 0 && in_stride % 4 == 0)   // split-bf16, fp32-exact operands
+    if (p->train_dense_bf && p->train_dense_h16 && d.pk_hn >= 0 && in_stride % 4 == 0)   // split-fp16 (x3)
+      HIP_TRY(launch_dense_h16(in, P, d.in, in_stride, p->d_packed + d.pk_hn, d.use_bias ? p->d_params + d.off_b : nullptr,
+                               d.out, d.act, o, st));
+    else if (p->train_dense_bf && d.pk_bfn >= 0 && in_stride % 4 == 0)   // split-bf16, fp32-exact operands
       HIP_TRY(launch_dense_bf(in, P, d.in, in_stride, p->d_packed + d.pk_bfn, d.use_bias ? p->d_params + d.off_b : nullptr,
                               d.out, d.act, o, st));
     else
@@ -664,7 +667,9 @@ int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* gra
       out = grad_of(p->ro_in[0]);
       acc = 1;
     }
-    if (p->train_dense_bf && d.pk_bft >= 0)   // split-bf16, fp32-exact operands
+    if (p->train_dense_bf && p->train_dense_h16 && d.pk_ht >= 0)   // split-fp16 (x3)
+      HIP_TRY(launch_dense_h16_t(t->dz[zi], P, d.out, p->d_packed + d.pk_ht, d.in, out, acc, act, aprev, st));
+    else if (p->train_dense_bf && d.pk_bft >= 0)   // split-bf16, fp32-exact operands
       HIP_TRY(launch_dense_bf_t(t->dz[zi], P, d.out, p->d_packed + d.pk_bft, d.in, out, acc, act, aprev, st));
     else if (d.pk_wt >= 0)
       HIP_TRY(launch_row_gemm_t(t->dz[zi], P, d.out, p->d_packed + d.pk_wt, d.in, out, acc, act, aprev, st));

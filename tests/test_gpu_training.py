@@ -245,11 +245,13 @@ def test_fused_backward_is_deterministic_and_matches_unfused(monkeypatch):
     assert np.linalg.norm(g1.astype(np.float64) - g3) <= 1e-5 * np.linalg.norm(g3)
 
 
-@pytest.mark.parametrize("switch", ["IGN_TSGEMM_BF", "IGN_BWD_BF", "IGN_TRAIN_DENSE_BF"])
+@pytest.mark.parametrize("switch", ["IGN_TSGEMM_BF", "IGN_BWD_BF", "IGN_TRAIN_DENSE_BF", "IGN_TRAIN_DENSE_H16"])
 def test_split_bf16_backward_matches_f32(monkeypatch, switch):
     """The split-bf16 weight-gradient contractions (tsgemm_bf) and the split-bf16 gate recompute of
-    the ordered backward (the forward's x6 path) against their f32-MFMA forms: bitwise
-    deterministic, and equal to fp32 reassociation (relative L2 <= 1e-5) on 24 synth50 graphs."""
+    the ordered backward (the forward's x6 path) against their f32-MFMA forms, and the training
+    Dense layers' split-fp16 row GEMMs (IGN_TRAIN_DENSE_H16, forward and backward) against their
+    split-bf16 form: bitwise deterministic, and equal to fp32 reassociation (relative L2 <= 1e-5)
+    on 24 synth50 graphs."""
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "synth50", 24)
     prm = MPPlan.from_model_info(mi).init_params(13, bias_scale=0.1)
     monkeypatch.setenv(switch, "1")
