@@ -59,7 +59,35 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: every rank builds its shard's host inputs and runs the barrier / max-over-ranks "
+                         "timing / edge-sum reduction around K empty steps (gloo); rank 0 prints the line with "
+                         "value null.  Checks the N-rank plumbing on a CPU-only host")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """``bench.py --gpus N`` started as one process (WORLD_SIZE unset): run N ranks of this same
+    command under torch.distributed.run, one per GPU of this node, as a CHILD process -- this
+    process has not touched the GPU and does not exec -- and return its exit code.  Rank 0's
+    JSON line reaches our stdout unchanged (the child inherits it)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host driver (RCCL)
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=env)
 
 
 def load_traffic(kernel_kind, workload):
@@ -181,12 +209,20 @@ def cpu_baseline_cxx(plan, mi, prm, graphs, budget_s, what="synth50 graphs"):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:   # the driver's `bench.py --gpus N`: start the N ranks ourselves
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%s but --gpus %d; launch with --nproc-per-node equal to --gpus"
+                 % (os.environ["WORLD_SIZE"], args.gpus))
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     # IGN_DIST_BACKEND=gloo + IGN_BENCH_DEVICE=0 rehearse the N>1 path on a one-GPU box
-    backend = os.environ.get("IGN_DIST_BACKEND", "nccl")
+    backend = "gloo" if args.dry_run else os.environ.get("IGN_DIST_BACKEND", "nccl")
     device = int(os.environ.get("IGN_BENCH_DEVICE", local))
     if world > 1:
         import torch
@@ -222,6 +258,8 @@ def main():
                                                                      first_id=ids[0])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(seed=0, bias_scale=0.05)
+    if args.dry_run:
+        return dry_run(args, dist, rank, world, mi, graphs, synthetic)
     cpu = cpu_cxx = None
     if world == 1 and not args.no_cpu and not args.train:
         # before anything touches the GPU: the baseline's worker processes are forked
@@ -435,6 +473,35 @@ def main():
         "cpu_baseline_cxx": cpu_cxx,
     }
     print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def dry_run(args, dist, rank, world, mi, graphs, synthetic):
+    """--dry-run: the rank plumbing of a real run without a GPU (the shard of each rank, the
+    barrier + MAX-over-ranks time, the SUM of edges), so a CPU host can check that `--gpus N`
+    yields one line from N ranks."""
+    from ignnition_amd import workloads
+    if synthetic:
+        edges = workloads.edges_per_forward(mi, graphs) // world   # the rank's in-edge share
+    else:
+        edges = workloads.edges_per_forward(mi, graphs)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dt, total = workloads.reduce_step_stats(dist, dt, edges)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+                          "scaling": "strong" if synthetic else "weak", "vs_baseline": None, "dtype": "fp32",
+                          "data": "dry run (no GPU)",
+                          "config": {"workload": "%s_%s_x%d" % (args.model, args.topology, args.graphs),
+                                     "edges_per_step_total": total, "dry_run": True}}))
     if dist is not None:
         dist.destroy_process_group()
 

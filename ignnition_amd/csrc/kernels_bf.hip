@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 // scales at no extra instruction:
 //   z  = 1 / (1 + 2^(c acc_z + x_z))
 //   rc = 1 / ((1 + 2^(c acc_r + x_r)) SS)            (= r / SS)
-//   n' = S - 2 S / (1 + 2^(x_n + rc acc_n))          (acc_n seeded with SS b_n: = S tanh(.))
+//   n' = S tanh2_(x_n + rc acc_n)                     (acc_n seeded with SS b_n)
 //   h' = n' + z (h' - n')
 template <int H, int PASSES>
 __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
@@ -258,7 +258,6 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
     const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(m)) >> 23) - 126;
     const int eS = 15 - E;
     const float S = __int_as_float((127 + eS) << 23);
-    const float S2n = -2.0f * S;
     const float SS = __int_as_float((127 + eS + es) << 23);
     const float c = __int_as_float((127 - eS - es) << 23);
     // every lane writes (and later reads back) exactly its own bias slots: no cross-lane hand-off
@@ -327,8 +326,7 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
         for (int r = 0; r < 4; ++r) {   // x rows carry the input-side biases (project_kernel)
           const float z = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(acc[0][i][r], c, x[0][i][r])));
           const float rc = rcpf_(fmaf(__builtin_amdgcn_exp2f(fmaf(acc[1][i][r], c, x[1][i][r])), SS, SS));
-          const float q = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(rc, acc[2][i][r], x[2][i][r])));
-          const float n = fmaf(q, S2n, S);
+          const float n = S * tanh2_(fmaf(rc, acc[2][i][r], x[2][i][r]));
           const float hn = n + z * (h[i][r] - n);
           h[i][r] = act ? hn : h[i][r];
         }

@@ -147,17 +147,28 @@ def debug(model_description, out_dir: str = "../debug_model/"):
 WARM_START_VARS = ["kernel.*", "recurrent_kernel.*", "bias.*"]   # FO:127-129
 
 
-def warm_start(defaults: dict, checkpoint: dict, patterns=WARM_START_VARS) -> dict:
+def warm_start(defaults: dict, checkpoint: dict, patterns=WARM_START_VARS, match: str = "component") -> dict:
     """tf.estimator.WarmStartSettings(vars_to_warm_start=["kernel.*", "recurrent_kernel.*",
     "bias.*"]) (FO:126-131) over the model's freshly initialised ``defaults``: a tensor is taken
-    from the checkpoint when its variable name (the last component of the Keras-like name, e.g.
-    ``kernel1`` of ``attention/kernel1``) matches one of the regexes; every other tensor keeps
-    its initial value.  A checkpoint tensor of another shape raises, as TF's warm start does; a
-    checkpoint that lacks a matching tensor leaves it initialised."""
+    from the checkpoint when its name matches one of the regexes; every other tensor keeps its
+    initial value.  A checkpoint tensor of another shape raises, as TF's warm start does; a
+    checkpoint that lacks a matching tensor leaves it initialised.
+
+    ``match`` says which name the regexes see ("warm start"):
+    * ``"component"`` (default): the variable's own name, the last component of the Keras-like
+      name (``kernel1`` of ``attention/kernel1``) -- the evident intent of the reference's list;
+    * ``"full"``: TF's literal rule.  WarmStartSettings resolves each string through
+      ``get_collection(TRAINABLE_VARIABLES, scope=regex)``, i.e. ``re.match`` anchored at the start
+      of the FULL variable name.  Every variable of the reference's model is nested under a layer
+      scope (``path_update/...``), so under this rule the reference's three patterns select
+      nothing and warm start restores no tensor."""
     import re
+    if match not in ("component", "full"):
+        raise ValueError("warm start: match must be 'component' or 'full', not %r" % (match,))
     out = dict(defaults)
     for name, init in defaults.items():
-        if name not in checkpoint or not any(re.match(p, name.split("/")[-1]) for p in patterns):
+        key = name if match == "full" else name.split("/")[-1]
+        if name not in checkpoint or not any(re.match(p, key) for p in patterns):
             continue
         v = np.asarray(checkpoint[name], np.float32)
         if v.shape != np.shape(init):
@@ -210,7 +221,8 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
         os.makedirs(model_dir, exist_ok=True)
     trainer = Trainer(model, device=device, dist=dist)
     if paths.get("warm_start_path", None):
-        trainer.set_params(warm_start(trainer.params(), load_params(paths["warm_start_path"])))
+        trainer.set_params(warm_start(trainer.params(), load_params(paths["warm_start_path"]),
+                                      match=opts.get("warm_start_match", "component")))
     native = str_to_bool(opts.get("native_reader", "True"))   # C++ reader
     make_input = gm.input_fn_native if native else gm.input_fn
     # data parallel: one shuffle seed for every rank (rank 0's), each rank reads its slice of
@@ -230,10 +242,10 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
                                 rank=rank, world=world)
         prepared = trainer.prefetch(source.ids(), depth=depth, workers=workers, load=source.load)
     else:
-        import random
-        random.seed(seed)   # the generator's random.shuffle (GEN) draws the same order on every rank
+        # the training stream shuffles with its own random.Random(seed): the same order on every
+        # rank, whatever the eval generator (rank 0, main thread) draws from the global random
         prepared = trainer.prefetch(gm.input_fn(paths["train_dataset"], shuffle=shuffle_train, batch_size=batch_size,
-                                                rank=rank, world=world), depth=depth)
+                                                rank=rank, world=world, seed=seed), depth=depth)
 
     def eval_batches():
         it = make_input(paths["eval_dataset"], shuffle=str_to_bool(opts.get("shuffle_eval_samples", "False")),

@@ -83,10 +83,12 @@ def _global_batches(stream, batch_size: int, rank: int, world: int):
         yield mine
 
 
-def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, rank=0, world=1):
+def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, rank=0, world=1, seed=None):
     """GM:102-198: generator -> normalization -> repeat -> batches of ``batch_size`` graphs.
     ``rank`` / ``world``: data-parallel slice of every global batch (``_global_batches``); the
-    ranks must draw the same stream (seed ``random`` identically when ``shuffle``)."""
+    ranks must draw the same stream: pass the same ``seed`` on every rank, which gives the stream
+    its own ``random.Random`` (reshuffled every epoch from it, untouched by any other draw of the
+    process).  ``seed=None`` shuffles with the global ``random``, as the reference does."""
     mi = model_info
     feature_list = mi.get_all_features()
     adjacency_info = mi.get_adjecency_info()
@@ -96,11 +98,14 @@ def input_fn(data_dir, shuffle=False, training=True, batch_size=1, repeat=True, 
     unique_additional_input = [a for a in additional_input if a not in [f.name for f in feature_list]]
     feature_names = [f.name for f in feature_list]
 
+    import random
+    rng = random.Random(seed) if seed is not None else None
+
     def stream():
         while True:
             n = 0
             for item in generator(data_dir, feature_names, output_name, adjacency_info, interleave_list,
-                                  unique_additional_input, training, shuffle):
+                                  unique_additional_input, training, shuffle, rng):
                 n += 1
                 if training:
                     xs, ys = item

@@ -139,8 +139,10 @@ def sample_to_data(sample: dict, feature_names, output_name, adj_names, interlea
 
 
 def generator(dir, feature_names, output_name, adj_names, interleave_names, additional_input,
-              training, shuffle=False):
-    """GEN:53-230.  Accepts str or bytes arguments (the reference receives bytes from tf.data)."""
+              training, shuffle=False, rng=None):
+    """GEN:53-230.  Accepts str or bytes arguments (the reference receives bytes from tf.data).
+    ``rng``: a ``random.Random`` for the shuffle (default: the process-global ``random``, as GEN);
+    a data-parallel input stream passes its own so that no other thread or rank's draws move it."""
     dir = _s(dir)
     feature_names = [_s(x) for x in feature_names]
     output_name = _s(output_name)
@@ -150,7 +152,7 @@ def generator(dir, feature_names, output_name, adj_names, interleave_names, addi
     # glob order is filesystem order in the reference; sorted here so runs are reproducible.
     samples = sorted(glob.glob(str(dir) + "/*.tar.gz"))
     if shuffle:
-        random.shuffle(samples)
+        (rng or random).shuffle(samples)
     for sample_file in samples:
         try:
             with tarfile.open(sample_file, "r:gz") as tar:

@@ -279,15 +279,16 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
   const int64_t R = g.n[p->readout_inputs[0]];
   int width = 0;
   for (int i = 0; i < p->num_readout_inputs; ++i) width += p->entities[p->readout_inputs[i]].hidden_dim;
-  std::vector<T> a(width), b2;
-  for (int64_t r = 0; r < R; ++r) {
+  // one row of the readout; rows are independent, so one large graph splits them over the
+  // threads in static chunks (the serial loop was most of the 25k-node graph's CPU time)
+  auto readout_row = [&](int64_t r, std::vector<T>& a, std::vector<T>& b2) {
     int col = 0;
     for (int i = 0; i < p->num_readout_inputs; ++i) {
       const int e = p->readout_inputs[i], H = p->entities[e].hidden_dim;
       std::copy(S[e].begin() + r * H, S[e].begin() + (r + 1) * H, a.begin() + col);
       col += H;
     }
-    std::vector<T> cur = a;
+    std::vector<T>& cur = a;
     for (const auto& L : m.dense) {
       b2.assign(L.out, T(0));
       for (int j0 = 0; j0 < L.out; j0 += 64) {   // 64 output columns at a time (register-resident)
@@ -313,6 +314,23 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
       cur.swap(b2);
     }
     for (size_t j = 0; j < cur.size(); ++j) out[r * (int64_t)cur.size() + j] = (float)cur[j];
+  };
+  if (par) {
+#pragma omp parallel
+    {
+      std::vector<T> a(width), b2;
+#pragma omp for schedule(static)
+      for (int64_t r = 0; r < R; ++r) {
+        a.resize(width);
+        readout_row(r, a, b2);
+      }
+    }
+  } else {
+    std::vector<T> a(width), b2;
+    for (int64_t r = 0; r < R; ++r) {
+      a.resize(width);
+      readout_row(r, a, b2);
+    }
   }
   return IGN_OK;
 }

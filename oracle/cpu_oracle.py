@@ -17,46 +17,59 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "cpu_forward.cpp")
 LIB = os.path.join(HERE, "_build", "libign_oracle.so")
+# the same source without -ffast-math: every float32 operation IEEE round-to-nearest (FMA
+# contraction allowed, as in TF's Eigen kernels on an AVX2/FMA host), libm expf / tanhf, no
+# reassociation -- the plain-float32 yardstick of the full-batch precision test
+LIB_IEEE = os.path.join(HERE, "_build", "libign_oracle_ieee.so")
+
+_FLAGS = {
+    # -ffast-math: vectorised expf / tanhf (libmvec) in the gates; the timed CPU line, checked
+    # against the float64 dense oracle at the parity tolerance (tests/test_cpu_oracle.py)
+    LIB: ["-O3", "-march=x86-64-v3", "-ffast-math"],
+    LIB_IEEE: ["-O3", "-march=x86-64-v3", "-fno-fast-math", "-fno-unsafe-math-optimizations"],
+}
 
 
 def build(force: bool = False) -> str:
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
-        return LIB
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    # -ffast-math: vectorised expf / tanhf (libmvec) in the gates; a float32 restatement checked
-    # against the float64 dense oracle at the parity tolerance (tests/test_cpu_oracle.py)
-    cmd = ["g++", "-O3", "-march=x86-64-v3", "-ffast-math", "-fopenmp", "-std=c++17", "-shared", "-fPIC",
-           "-I", os.path.join(REPO, "include"), SRC, "-o", LIB]
-    subprocess.check_call(cmd)
+    for lib, flags in _FLAGS.items():
+        if not force and os.path.exists(lib) and os.path.getmtime(lib) >= os.path.getmtime(SRC):
+            continue
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        cmd = ["g++", *flags, "-fopenmp", "-std=c++17", "-shared", "-fPIC",
+               "-I", os.path.join(REPO, "include"), SRC, "-o", lib]
+        subprocess.check_call(cmd)
     return LIB
 
 
-_lib = None
+_libs = {}
 
 
-def _load():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
-            raise ImportError("oracle/_build/libign_oracle.so not built: python -m oracle.cpu_oracle")
-        lib = C.CDLL(LIB)
+def _load(ieee: bool = False):
+    path = LIB_IEEE if ieee else LIB
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise ImportError("%s not built: python -m oracle.cpu_oracle" % os.path.relpath(path, REPO))
+        lib = C.CDLL(path)
         lib.ign_oracle_forward.restype = C.c_int
         lib.ign_oracle_forward.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.c_void_p,
                                            C.c_int32, C.c_int32]
         lib.ign_oracle_last_error.restype = C.c_char_p
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
 class OracleError(RuntimeError):
     pass
 
 
-def cpu_forward(plan, graphs, params: dict, threads: int = 0, float64: bool = False) -> np.ndarray:
+def cpu_forward(plan, graphs, params: dict, threads: int = 0, float64: bool = False,
+                ieee: bool = False) -> np.ndarray:
     """float64=False: float32 arithmetic (TF's on the CPU; bench.py's line); True: float64 (the
-    checker: float32 runs of this model differ from float64 by up to ~2e-4 on outliers)."""
+    checker: float32 runs of this model differ from float64 by up to ~2e-4 on outliers).
+    ieee=True: the float32 arithmetic of the build without -ffast-math (libm expf / tanhf, no
+    reassociation), the yardstick the engine's full-batch error is held to."""
     from ignnition_amd.engine import batch_desc
-    lib = _load()
+    lib = _load(ieee and not float64)
     pd, pkeep = plan.to_desc()
     bd, bkeep, (G, E, num, cnt, _) = batch_desc(plan, graphs)
     specs = plan.param_specs()

@@ -189,3 +189,45 @@ def test_edge_cut_carries_edge_parameters():
     assert sorted(ids.tolist()) == list(range(E))   # every edge exactly once
     for k in kept:
         assert np.all(np.diff(k) > 0)                # original order within a partition
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=repo)
+    lines = []
+    for ln in r.stdout.splitlines():
+        ln = ln.strip()
+        if ln.startswith("{"):
+            lines.append(json.loads(ln))
+    return r, lines
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """The driver runs `python bench.py --gpus N` without a launcher: bench.py must start N ranks
+    itself (torch.distributed.run as a child process) and print exactly one line, from rank 0,
+    with n_gpus N and the edges of every rank's shard summed."""
+    r, lines = _bench(["--gpus", "2", "--dry-run", "--topology", "nsfnet", "--graphs", "2", "--steps", "3",
+                       "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["scaling"] == "weak"
+    _, _, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 4)
+    assert line["config"]["edges_per_step_total"] == workloads.edges_per_forward(mi, graphs)
+
+
+def test_bench_single_rank_dry_run_and_world_mismatch():
+    r, lines = _bench(["--dry-run", "--topology", "nsfnet", "--graphs", "2", "--steps", "2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 1
+    # launched by torchrun with a world that differs from --gpus: refuse instead of mislabeling
+    r, lines = _bench(["--gpus", "4", "--dry-run", "--topology", "nsfnet", "--graphs", "2"],
+                      {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and not lines
+    assert "WORLD_SIZE" in r.stderr

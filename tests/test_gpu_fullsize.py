@@ -13,9 +13,13 @@ configs[4] — the synthetic 1M-node / 10M-edge graph, H=64, T=8
 
 configs[2] — RouteNet on 512 synth50-size graphs batched into one CSR (the default bench):
   * deterministic; three graphs of the batch equal the same graph run alone (GM:712-724: the
-    reference runs the model per graph); two graphs against the float64 oracle; and every
-    prediction of the batch against the float64 C++ restatement, within the error of plain float32
-    arithmetic of the same model (its float32 mode), max and 99.99th percentile.
+    reference runs the model per graph); two graphs against the float64 oracle.
+
+Full-batch precision (configs[1]-[3] at 512 graphs: RouteNet synth50, Q-size synth50, RouteNet
+GEANT2): every prediction of the engine's default contractions against the float64 C++
+restatement, held to plain IEEE float32 arithmetic of the same model (the restatement built
+without -ffast-math: libm expf / tanhf) -- DESIGN §4 has the table, including the split-bf16 x6
+and f32-MFMA variants this test also records.
 
 Tolerance: |engine - oracle| <= 1e-4 * max(1, |oracle|).
 """
@@ -156,19 +160,49 @@ def test_routenet_512_synth50_batch():
     for gi in (7, 400):
         err = _scaled_err(o1[off[gi]:off[gi + 1]], ora.forward([graphs[gi]]))
         assert err <= TOL, (gi, err)
-    # every prediction: against the float64 restatement, with plain float32 arithmetic of the same
-    # model (the restatement's float32 mode) as the yardstick -- over 1.25M predictions a few
-    # outliers of any float32 evaluation of this model exceed 1e-4 (8 iterations of sequence GRUs
-    # amplify rounding); the engine must stay within the float32 yardstick's error
-    ref = cpu_oracle.cpu_forward(plan, graphs, prm, 0, float64=True)
-    e_eng = _scaled(o1, ref)
-    e_f32 = _scaled(cpu_oracle.cpu_forward(plan, graphs, prm, 0), ref)
-    print("512 x synth50, vs float64: engine max %.3g p99.99 %.3g mean %.3g | float32 yardstick max %.3g p99.99 %.3g"
-          % (e_eng.max(), np.quantile(e_eng, 0.9999), e_eng.mean(), e_f32.max(), np.quantile(e_f32, 0.9999)))
-    # measured (round 2): engine max 2.3e-4, p99.99 5.8e-5, mean 7.8e-7; float32 yardstick max
-    # 1.9e-4, p99.99 3.0e-5 -- the same tail, within 2x; the 1e-4 per-prediction bound holds for
-    # the spot-checked graphs above and at the 99.99th percentile
-    assert e_eng.max() <= max(TOL, 2.0 * e_f32.max())
-    assert np.quantile(e_eng, 0.9999) <= min(TOL, 3.0 * np.quantile(e_f32, 0.9999))
-    assert e_eng.mean() <= 1e-5
     eng.close()
+
+
+IEEE_VARIANTS = {"default": {}, "bf16x6": {"IGN_SEQ_VARIANT": "4", "IGN_READOUT_VARIANT": "2", "IGN_SUM_VARIANT": "7"},
+                 "f32mfma": {"IGN_SEQ_VARIANT": "2", "IGN_READOUT_VARIANT": "1", "IGN_SUM_VARIANT": "3"}}
+
+
+def _tails(e):
+    return {"max": float(e.max()), "p9999": float(np.quantile(e, 0.9999)), "mean": float(e.mean())}
+
+
+@pytest.mark.parametrize("model,topology", [("routenet", "synth50"), ("qsize", "synth50"), ("routenet", "geant2")])
+def test_full_batch_precision_vs_ieee_float32(monkeypatch, model, topology):
+    """512 graphs: the default's 99.99th percentile and mean within 1.25x of IEEE float32's, its
+    maximum within 1.5x.  Why not 1.25x for the maximum: the worst of 1.25 M predictions after
+    8 GRU iterations is one chaotic outlier, and float32 evaluations of EQUAL accuracy move it by
+    ~1.3x (libm tanhf vs a 1.2-ulp polynomial: 1.74e-4 vs 1.97e-4 on RouteNet synth50;
+    tools/probes/gate_precision_emulation.py), while the 99.99th percentile moves by < 10 %.
+    Measured round 3 (max / p99.99 vs IEEE): RouteNet synth50 1.25x / 1.22x, Q-size 1.11x / 1.19x,
+    GEANT2 1.10x / 0.75x.  The round-2 kernels' exp-form tanh gave 1.84x / 2.42x on RouteNet."""
+    if device_count() == 0:
+        pytest.fail("no GPU visible")
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(model, topology, 512)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(1, bias_scale=0.05)
+    ref = cpu_oracle.cpu_forward(plan, graphs, prm, 0, float64=True)
+    res = {"ieee_f32": _tails(_scaled(cpu_oracle.cpu_forward(plan, graphs, prm, 0, ieee=True), ref))}
+    for name, env in IEEE_VARIANTS.items():
+        for k in ("IGN_SEQ_VARIANT", "IGN_READOUT_VARIANT", "IGN_SUM_VARIANT"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        out = b.forward().reshape(-1)
+        b.close()
+        eng.close()
+        assert np.all(np.isfinite(out))
+        res[name] = _tails(_scaled(out, ref))
+    print("%s_%s_x512 vs float64:" % (model, topology),
+          "; ".join("%s max %.3g p99.99 %.3g mean %.3g" % (k, v["max"], v["p9999"], v["mean"]) for k, v in res.items()))
+    d, y = res["default"], res["ieee_f32"]
+    assert d["p9999"] <= 1.25 * y["p9999"], res
+    assert d["mean"] <= 1.25 * y["mean"], res
+    assert d["max"] <= 1.5 * y["max"], res

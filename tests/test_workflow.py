@@ -200,3 +200,38 @@ def test_set_params_checks_names_and_shapes():
     with pytest.raises(ValueError, match="shape"):
         eng.set_params(bad)
     eng.close()
+
+
+def test_warm_start_full_name_rule_is_tfs_anchored_match():
+    """match="full": TF's get_collection(scope=regex) rule, re.match on the full variable name;
+    the reference's patterns then select only top-level names (none in its models)."""
+    init = {"path_update/kernel": np.zeros((2, 3), np.float32), "kernel_top": np.zeros(2, np.float32),
+            "bias": np.zeros(1, np.float32)}
+    ckpt = {k: np.ones_like(v) for k, v in init.items()}
+    full = fo.warm_start(init, ckpt, match="full")
+    assert np.all(full["kernel_top"] == 1) and np.all(full["bias"] == 1)
+    assert np.all(full["path_update/kernel"] == 0)
+    comp = fo.warm_start(init, ckpt)
+    assert all(np.all(v == 1) for v in comp.values())
+    with pytest.raises(ValueError, match="match"):
+        fo.warm_start(init, ckpt, match="prefix")
+
+
+def test_python_input_stream_has_its_own_rng(example_dir):
+    """Data-parallel input_fn streams shuffle with random.Random(seed): draws from the global
+    random between them (rank 0's eval generator) do not move one rank's order, so the two ranks'
+    batches stay the halves of the one-rank stream's global batches."""
+    import random
+    mi = fo.create_model()
+    gm.set_model_info(mi)
+    path = fo.CONFIG["PATHS"]["train_dataset"]
+    whole = gm.input_fn(path, shuffle=True, batch_size=2, seed=5)
+    ranks = [gm.input_fn(path, shuffle=True, batch_size=1, seed=5, rank=r, world=2) for r in range(2)]
+    lab = lambda ys: [float(np.asarray(y).reshape(-1)[0]) for y in ys]
+    for _ in range(6):
+        g = lab(next(whole)[1])
+        random.random()                       # another thread's draw on the global generator
+        r0 = lab(next(ranks[0])[1])
+        random.shuffle(list(range(10)))
+        r1 = lab(next(ranks[1])[1])
+        assert r0 + r1 == g

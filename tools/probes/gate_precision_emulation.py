@@ -1,0 +1,120 @@
+"""Where the engine's full-batch error tail comes from: the float32 restatement
+(oracle/cpu_forward.cpp, IEEE build) with the GRU gates rewritten the way the gfx950 kernels
+evaluate them, on the 512 x synth50 RouteNet batch, against the float64 restatement.
+
+Variants (compile-time macros added to a temporary copy of the source):
+  ieee        libm tanhf / expf (the yardstick)
+  expt        tanh(x) = 1 - 2 / (1 + 2^(2 log2(e) x))   (the round-2 kernels' candidate)
+  poly55      |x| < 0.55: odd polynomial (device_common.h tanh_tc_), else the exp form (round 3)
+  sighw0      poly55 + sigmoid as 1 / (1 + 2^(-log2(e) x)) on the pre-scaled argument
+  sighw1/2    sighw0 with exp2 and the reciprocal perturbed by uniform +-0.5 / +-1 ulp
+              (a model of v_exp_f32 / v_rcp_f32, documented as 1 ulp)
+Round-3 result: max / p99.99 / mean scaled error
+  ieee 1.74e-4 / 2.18e-5 / 3.80e-7, expt 4.54e-4 / 2.88e-5 / 4.30e-7, poly55 1.97e-4 / 2.11e-5,
+  sighw0 2.22e-4 / 2.03e-5, sighw1 2.17e-4 / 2.07e-5, sighw2 3.93e-4 / 2.91e-5:
+the exp-form tanh was the dominant term; the maximum over 1.25 M predictions moves by ~1.3x
+between formulations of equal accuracy (ieee / poly55 / sighw0), the 99.99th percentile does not.
+
+    python tools/probes/gate_precision_emulation.py [variants...]      (CPU only, ~1 min)
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+
+FLAGS = {"ieee": [], "expt": ["-DEXPT"], "poly55": ["-DPOLY55"], "sighw0": ["-DPOLY55", "-DSIGHW", "-DPERT=0"],
+         "sighw1": ["-DPOLY55", "-DSIGHW", "-DPERT=1"], "sighw2": ["-DPOLY55", "-DSIGHW", "-DPERT=2"]}
+
+PRELUDE = r'''namespace {
+template <typename T> inline T TANHX(T x) {
+#if defined(POLY55)
+  if (sizeof(T) == 4) {
+    const float xf = (float)x;
+    if (fabsf(xf) < 0.55f) {
+      const float u = xf * xf;
+      float p = -0.0062725638953669005f;
+      p = p * u + 0.021070224531615167f; p = p * u - 0.0538518588145328f;
+      p = p * u + 0.13332580319582182f; p = p * u - 0.3333331730407817f;
+      return T(xf + (xf * u) * p);
+    }
+    return T(1.0f - 2.0f * (1.0f / (1.0f + exp2f(xf * 2.8853900817779268f))));
+  }
+#elif defined(EXPT)
+  if (sizeof(T) == 4) return T(1.0f - 2.0f * (1.0f / (1.0f + exp2f((float)x * 2.8853900817779268f))));
+#endif
+  return std::tanh(x);
+}
+#ifndef PERT
+#define PERT 0
+#endif
+inline float pert(float v, uint32_t seed) {
+  if (!std::isfinite(v) || v == 0.0f) return v;
+  uint32_t h = seed * 2654435761u; h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+  const float u = ((h & 0xffff) / 65535.0f) * 2.0f - 1.0f;
+  const float ulp = nextafterf(fabsf(v), INFINITY) - fabsf(v);
+  return v + u * ulp * 0.5f * PERT;
+}
+template <typename T> inline T SIGX(T x) {
+#if defined(SIGHW)
+  if (sizeof(T) == 4) {
+    const float y = (float)x * -1.4426950408889634f;
+    const uint32_t s0 = __builtin_bit_cast(uint32_t, y);
+    const float e = pert(exp2f(y), s0);
+    return T(pert(1.0f / (1.0f + e), s0 ^ 0x9e3779b9u));
+  }
+#endif
+  return T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), x))));
+}
+'''
+
+
+def build(tmp):
+    src = open(os.path.join(REPO, "oracle", "cpu_forward.cpp")).read()
+    src = src.replace('#include "../include/ignmp.h"', '#include "%s"' % os.path.join(REPO, "include", "ignmp.h"))
+    sig = ("for (int j = 0; j < 2 * H; ++j) mx[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), "
+           "mx[j] + mh[j]))));")
+    tnh = "for (int j = 0; j < H; ++j) mh[j] = std::tanh(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);"
+    assert src.count(sig) == 2 and src.count(tnh) == 2, "oracle/cpu_forward.cpp gate lines changed"
+    src = src.replace(sig, "for (int j = 0; j < 2 * H; ++j) mx[j] = SIGX(mx[j] + mh[j]);")
+    src = src.replace(tnh, "for (int j = 0; j < H; ++j) mh[j] = TANHX(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);")
+    src = src.replace("namespace {", PRELUDE, 1)
+    path = os.path.join(tmp, "cpu_forward_emu.cpp")
+    open(path, "w").write(src)
+    return path
+
+
+def main(variants):
+    from ignnition_amd import workloads
+    from ignnition_amd.engine import MPPlan
+    from oracle import cpu_oracle
+    cpu_oracle.build()
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "synth50", 512)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(1, bias_scale=0.05)
+    ref = cpu_oracle.cpu_forward(plan, graphs, prm, 0, float64=True).astype(np.float64)
+    with tempfile.TemporaryDirectory() as tmp:
+        src = build(tmp)
+        for v in variants:
+            lib = os.path.join(tmp, "lib_%s.so" % v)
+            subprocess.check_call(["g++", "-O3", "-march=x86-64-v3", "-fopenmp", "-std=c++17", "-shared", "-fPIC",
+                                   *FLAGS[v], src, "-o", lib])
+            h = C.CDLL(lib)
+            h.ign_oracle_forward.restype = C.c_int
+            h.ign_oracle_forward.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.c_void_p,
+                                             C.c_int32, C.c_int32]
+            h.ign_oracle_last_error.restype = C.c_char_p
+            cpu_oracle._libs[cpu_oracle.LIB_IEEE] = h
+            out = cpu_oracle.cpu_forward(plan, graphs, prm, 0, ieee=True).astype(np.float64)
+            cpu_oracle._libs.pop(cpu_oracle.LIB_IEEE)
+            e = np.abs(out - ref) / np.maximum(1.0, np.abs(ref))
+            print("%-7s max %.3g p99.99 %.3g mean %.3g" % (v, e.max(), np.quantile(e, 0.9999), e.mean()), flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(FLAGS))
