@@ -440,7 +440,7 @@ def main():
     H16 = ("split-fp16: power-of-two-scaled 2-piece fp16 operands (RNE, 2^-22 relative), %d products, "
            "fp32 accumulate")
     seq_c = {2: "f32 MFMA", 4: BF % 6, 5: BF % 9, 6: H16 % 3, 7: H16 % 4}
-    ro_c = {1: "f32 MFMA", 2: BF % 6, 3: BF % 9, 4: "layer 1 " + BF % 6 + "; layer 2 " + H16 % 3}
+    ro_c = {1: "f32 MFMA", 2: BF % 6, 3: BF % 9, 4: "both layers " + H16 % 3}
     contraction = {"ordered_update_hU": seq_c.get(seq_v, "f32 MFMA") if plan.hidden[0] in (32, 64) else "f32 MFMA",
                    "readout": ro_c.get(ro_v, BF % 6),
                    # sum variants 8 (default) / 7: split-fp16 / split-bf16 x.W and h.U at DIN = H = 64,

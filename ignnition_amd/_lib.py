@@ -92,7 +92,7 @@ ACT = {None: 0, "None": 0, "linear": 0, "relu": 1, "selu": 2, "sigmoid": 3, "tan
 # every symbol declared in include/ignmp.h
 SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_create", "ign_plan_destroy",
            "ign_plan_num_params", "ign_plan_num_param_tensors", "ign_plan_param_tensor", "ign_plan_set_params",
-           "ign_plan_set_timing", "ign_plan_set_stream", "ign_batch_create", "ign_batch_destroy", "ign_batch_info",
+           "ign_plan_set_timing", "ign_plan_set_stream", "ign_plan_trim_cache", "ign_batch_create", "ign_batch_destroy", "ign_batch_info",
            "ign_forward", "ign_synchronize", "ign_batch_predictions", "ign_batch_state", "ign_stats",
            "ign_forward_begin", "ign_forward_mp", "ign_forward_end", "ign_batch_mp_split", "ign_batch_bind_state",
            "ign_batch_state_slot", "ign_gather_rows", "ign_plan_set_timing_kinds",
@@ -132,6 +132,7 @@ def _load():
         "ign_plan_set_params": (C.c_int, [VP, VP, i32]),
         "ign_plan_set_timing": (C.c_int, [VP, i32]),
         "ign_plan_set_stream": (C.c_int, [VP, VP]),
+        "ign_plan_trim_cache": (C.c_int, [VP]),
         "ign_batch_create": (C.c_int, [VP, P(BatchDesc), P(VP)]),
         "ign_batch_destroy": (None, [VP]),
         "ign_batch_info": (C.c_int, [VP, P(BatchInfo)]),
@@ -174,7 +175,10 @@ def _load():
         "ign_backward_end": (C.c_int, [VP, VP]),
         "ign_batch_train_buffers": (C.c_int, [VP, i32, P(VP), P(VP)]),
     }
+    ab = "IGN_LIB_PATH" in os.environ   # an A/B build of an older tree may lack newer entry points
     for name, (res, args) in sig.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -23,6 +23,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // the MACs per cycle, so even 6-9 piece products cost less than one f32 pass.
 typedef short bf8 __attribute__((ext_vector_type(8)));      // 8 bf16: A/B fragment of 16x16x32
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef int32_t i4v __attribute__((ext_vector_type(4)));
 #define MFMA_BF(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 // ---- split-fp16 contraction (scaled two-piece fp16 operands, 3 products) --------------------------
@@ -37,12 +38,19 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 #define MFMA_H(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
 
-// (hi, lo) fp16 pieces of the pair (a, b), each packed [a | b << 16] (v_cvt_pk_f16_f32, RNE)
+// (hi, lo) fp16 pieces of the pair (a, b), each packed [a | b << 16] (v_cvt_pk_f16_f32, RNE).
+// lo = fp16(a - hi): a - hi is exact in fp32 (hi is a's nearest fp16), so one mixed-precision fma
+// per value, v_fma_mix{lo,hi}_f16 (a * 1 - hi, rounded once to fp16), gives the same bits as
+// converting hi back to fp32, subtracting and converting again: 3 instructions per pair, not 5.
 struct hpair { uint32_t hi, lo; };
 __device__ __forceinline__ hpair split2h(float a, float b) {
   const h2 p = __builtin_convertvector((f2){a, b}, h2);
-  const h2 q = __builtin_convertvector((f2){a - (float)p[0], b - (float)p[1]}, h2);
-  return {__builtin_bit_cast(uint32_t, p), __builtin_bit_cast(uint32_t, q)};
+  const uint32_t hi = __builtin_bit_cast(uint32_t, p);
+  uint32_t lo;   // mixlo leaves bits 31:16 alone and mixhi overwrites them: no initial value
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lo) : "v"(a), "v"(b), "v"(hi));
+  return {hi, lo};
 }
 
 __device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {

@@ -11,11 +11,11 @@
 // IGN_POOL=0 bypasses the cache (hipMalloc / hipFree per block).  IGN_POOL_POISON=1 fills every
 // scratch block it hands out with NaN (0xFF bytes): the parity tests under it show that no kernel
 // reads batch scratch it has not written (tests/test_gpu_parity.py).  IGN_POOL_CACHE_GB caps the
-// idle bytes kept (default 64).
+// idle bytes kept (default 16; ign_plan_trim_cache releases them all).
 //
 // The host side has the same problem: the batch builders' index tables are ~10^8 bytes of host
 // memory per batch.  hvec (engine_internal.h) draws blocks >= 1 MiB from a process-wide cache
-// (IGN_HOST_CACHE_GB idle bytes kept, default 16) whose blocks keep their pages and are pinned,
+// (IGN_HOST_CACHE_GB idle bytes kept, default 4) whose blocks keep their pages and are pinned,
 // so the uploads from them are direct DMA.
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
@@ -102,9 +102,11 @@ std::shared_ptr<DevPool> pool_create(int device) {
   pool->device = device;
   pool->enabled = env_int("IGN_POOL", 1) != 0;
   pool->poison = env_int("IGN_POOL_POISON", 0) != 0;
-  pool->cap = (size_t)std::max(0, env_int("IGN_POOL_CACHE_GB", 64)) << 30;
+  pool->cap = (size_t)std::max(0, env_int("IGN_POOL_CACHE_GB", 16)) << 30;
   return pool;
 }
+
+bool pool_enabled(const DevPool* pool) { return pool && pool->enabled; }
 
 hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch) {
   *out = nullptr;
@@ -186,7 +188,7 @@ struct HostCache {
   std::unordered_map<void*, bool> pinned;      // every live or idle block -> registered for DMA
   size_t idle_bytes = 0;
   size_t cap = 0;
-  HostCache() { cap = (size_t)std::max(0, env_int("IGN_HOST_CACHE_GB", 16)) << 30; }
+  HostCache() { cap = (size_t)std::max(0, env_int("IGN_HOST_CACHE_GB", 4)) << 30; }
   void unmap(void* p, size_t cls) {
     auto it = pinned.find(p);
     if (it != pinned.end()) {
@@ -248,6 +250,26 @@ void host_block_free(void* p, size_t bytes) {
       it->second.pop_back();
       c.idle_bytes -= it->first;
     }
+}
+
+void pool_trim_idle(DevPool* pool) {
+  if (!pool) return;
+  std::lock_guard<std::mutex> g(pool->mu);
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(pool->device);
+  pool->trim(0, true);
+  hipSetDevice(prev);
+}
+
+void host_cache_trim() {
+  HostCache& c = host_cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  for (auto& kv : c.idle) {
+    for (void* p : kv.second) c.unmap(p, kv.first);
+    c.idle_bytes -= kv.first * kv.second.size();
+    kv.second.clear();
+  }
 }
 
 void pool_stats(DevPool* pool, int64_t* live_bytes, int64_t* idle_bytes) {

@@ -79,8 +79,14 @@ int ensure_device(ign_plan* p) {
   return IGN_OK;
 }
 
+// one non-blocking upload stream per host thread and device (a stream belongs to the device that
+// was current when it was created; a thread may build batches for plans on several devices)
 hipStream_t upload_stream() {
-  thread_local hipStream_t s = nullptr;
+  thread_local std::vector<hipStream_t> streams;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if ((int)streams.size() <= dev) streams.resize(dev + 1, nullptr);
+  hipStream_t& s = streams[dev];
   if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
   return s;
 }
@@ -833,6 +839,18 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
             multi_rows[fill[multi_of[slot_of[k]]]++] = (uint32_t)table_row(mcode[k]);
       }
       for (int64_t i = 0; i < ND; i += 16) mb.wave_steps += len[i];   // sorted: a tile's first row is its longest
+      {   // the ordered update's tile headers: one 16-B load per position, no dependent code load
+        const int64_t NDp = (ND + 15) / 16 * 16;
+        hvec<int32_t> hdr((size_t)(4 * NDp));
+        for (int64_t i = 0; i < NDp; ++i) {
+          const bool v = i < ND;
+          hdr[4 * i] = v ? order[i] : 0;
+          hdr[4 * i + 1] = v ? len[i] : 0;
+          hdr[4 * i + 2] = v ? step_ptr[i] : (int32_t)steps;
+          hdr[4 * i + 3] = (int32_t)scode[v ? step_ptr[i] : steps];
+        }
+        if ((rc = dev_upload(b.get(), &mb.d_seq_hdr, hdr))) return rc;
+      }
       if (mb.zero_row + 1 + mb.n_multi >= (int64_t)UINT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
       mb.n_steps = steps;
       mb.n_msgs = n_msgs;
@@ -1034,12 +1052,23 @@ void ign_batch_destroy(ign_batch* b) {
   if (!b) return;
   if (b->plan) {
     hipSetDevice(b->plan->device);
-    if (b->plan->stream) hipStreamSynchronize(b->plan->stream);
+    // With the block cache every released block carries an event recorded on the plan stream
+    // (pool_release), so the host need not wait here and the next step can be queued behind this
+    // one.  Without it (IGN_POOL=0) pool_release waits itself; a captured graph is destroyed only
+    // once its launches have finished.
+    if (b->plan->stream && (b->graph || !pool_enabled(b->pool.get()))) hipStreamSynchronize(b->plan->stream);
   }
   if (b->graph) hipGraphExecDestroy(b->graph);
   if (b->train) train_state_destroy(b->train);
   if (b->pool) pool_release(b->pool.get(), b->allocs, b->plan ? b->plan->stream : nullptr);
   delete b;
+}
+
+int ign_plan_trim_cache(ign_plan* p) {
+  if (!p) return fail(IGN_ERR_INVALID, "null argument");
+  if (p->pool) pool_trim_idle(p->pool.get());
+  host_cache_trim();
+  return IGN_OK;
 }
 
 int ign_batch_info(const ign_batch* b, ign_batch_info_t* o) {
@@ -1236,6 +1265,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                  p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
     if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
     if (cp.pk_uh >= 0) a.Uh = p->d_packed + cp.pk_uh;
+    a.hdr = mb.d_seq_hdr;
     {   // MFMAs per wave step: split-fp16 / split-bf16 (variants 6, 7 / 4, 5; H = 32 / 64) passes x
         // 3 gates x H/16 x H/32 on the 16x16x32 pipe; f32 (seq_gru2) 3 gates x H/16 x H/4
       const int v = p->seq_variant;

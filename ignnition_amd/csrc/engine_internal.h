@@ -30,6 +30,9 @@ std::shared_ptr<DevPool> pool_create(int device);
 hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch);
 void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t after);
 void pool_stats(DevPool* pool, int64_t* live_bytes, int64_t* idle_bytes);
+bool pool_enabled(const DevPool* pool);
+void pool_trim_idle(DevPool* pool);   // every idle block, waiting for its fence
+void host_cache_trim();               // every idle host block
 
 // devpool.cpp: process-wide cache of large host blocks (>= kHostBlockMin bytes) for the batch
 // builders' index tables.  A batch touches ~10^8 bytes of fresh host memory; straight from malloc
@@ -140,6 +143,7 @@ struct MPB {
   int32_t* d_msg_ptr = nullptr;
   uint32_t* d_msg_src = nullptr;
   uint32_t* d_step_code = nullptr;
+  int32_t* d_seq_hdr = nullptr;   // sorted MPs: per order position {order, len, step_ptr, first code} (SeqGruArgs::hdr)
   float* d_table = nullptr;       // sorted MPs: [sources' rows | zero row | multi rows][3H]
   std::vector<int64_t> src_off;   // first table row of each source
   std::vector<int64_t> src_rows;

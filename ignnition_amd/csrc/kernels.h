@@ -30,6 +30,9 @@ struct SeqGruArgs {
                              // step_ptr[p] + p (state before) .. + len[p] (after each step)
   const void* Ubf = nullptr;  // variants 4/5: recurrent kernel as exact 3-piece bf16 A fragments
   const void* Uh = nullptr;   // variants 6/7: scaled 2-piece fp16 A fragments + scale (pack_u_f16)
+  // variants 6/7: [ceil(n_dst / 16) * 16][4] per order position {order, len, step_ptr,
+  // step_code[step_ptr]}; the padding positions are {0, 0, n_steps, zero row}
+  const int32_t* hdr = nullptr;
 };
 
 struct SumGruArgs {

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include "kernels.h"
 
 #include "device_common.h"
@@ -234,25 +235,49 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   const float* tab = a.table + 4 * g;
   __syncthreads();
   const int64_t n_tiles = (a.n_dst + 15) / 16;
-  for (int64_t tile = xcd_block(a.xcd_remap) * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+  const int64_t tile_stride = (int64_t)gridDim.x * 4;
+  // Tile prologue, one memory round trip: the 16-B position headers (row, final_len, first step,
+  // first step's code; padded to whole tiles with empty positions) of the wave's next tile are
+  // loaded while the current tile runs, so a tile starts by issuing its state rows and first
+  // projected rows together.  No branch guards a load.
+  int64_t tile = xcd_block(a.xcd_remap) * 4 + wave;
+  i4v hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile, n_tiles - 1) * 16 + j));
+  for (; tile < n_tiles; tile += tile_stride) {
     const int64_t pos = tile * 16 + j;
     const bool valid = pos < a.n_dst;
-    const int row = valid ? a.order[pos] : 0;
-    const int L = valid ? a.len[pos] : 0;
-    const uint32_t* codes = a.step_code + (valid ? a.step_ptr[pos] : 0);
+    const int row = hd[0];
+    const int L = hd[1];
+    const uint32_t* codes = a.step_code + hd[2];
     f4 h[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) h[t] = valid ? ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-    int Lmax = L;
+    for (int t = 0; t < NT; ++t) {
+      const f4 v = ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g);
+      h[t] = valid ? v : f4{0, 0, 0, 0};
+    }
+    // the first step's projected rows (and the second step's code) are in flight with the state
+    f4 x[3][NT];
+    {
+      const float* p = tab + (int64_t)(uint32_t)hd[3] * (3 * H);
+#pragma unroll
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
+    }
+    uint32_t code = codes[1];
+    hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile + tile_stride, n_tiles - 1) * 16 + j));
+    // positions are sorted by final_len, descending: lane 0 (position tile * 16) is the longest
+    const int Lmax = __builtin_amdgcn_readfirstlane(L);
     float m = 1.0f;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(h[t][r]));
+    // m = max(1, max |h|) over the tile: after the first iteration every |h| <= 1 (a GRU output
+    // is a convex combination of h and tanh), so a ballot settles it; the cross-lane reduction
+    // runs only for a tile that holds a larger state
+    if (__ballot(m > 1.0f) != 0) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      Lmax = max(Lmax, __shfl_xor(Lmax, o));
-      m = fmaxf(m, __shfl_xor(m, o));
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     }
     // m = f 2^E, f in [0.5, 1): S = 2^(15 - E); SS = S sigma
     const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(m)) >> 23) - 126;
@@ -273,7 +298,9 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
 #pragma unroll
         for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
     };
-    auto step = [&](int t, const f4 (&x)[3][NT]) __attribute__((always_inline)) {
+    // MASKED: some row of the tile ends before step t (t >= the tile's shortest final_len);
+    // the steps before that update every row without a select
+    auto step = [&](int t, const f4 (&x)[3][NT], auto masked) __attribute__((always_inline)) {
       // B fragments: the two fp16 pieces of the scaled state, k-step s = accumulator tiles 2s, 2s+1
       h8 hf[2][KS];
 #pragma unroll
@@ -328,19 +355,23 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
           const float rc = rcpf_(fmaf(__builtin_amdgcn_exp2f(fmaf(acc[1][i][r], c, x[1][i][r])), SS, SS));
           const float n = S * tanh2_(fmaf(rc, acc[2][i][r], x[2][i][r]));
           const float hn = n + z * (h[i][r] - n);
-          h[i][r] = act ? hn : h[i][r];
+          if constexpr (decltype(masked)::value) h[i][r] = act ? hn : h[i][r];
+          else h[i][r] = hn;
         }
       }
     };
     // the projected row of step t is loaded at the start of step t and consumed by the gates after
     // the h.U MFMAs (a two-buffer one-step-ahead prefetch, loop unrolled by two, measured slower:
     // 0.242 vs 0.214 ms per launch, 144 VGPRs -> 3 waves per SIMD)
-    uint32_t code = codes[0];
-    for (int t = 0; t < Lmax; ++t) {
-      f4 x[3][NT];
+    // every tile has Lmax >= 1 (a destination without messages is rejected at batch build);
+    // Lmin: final_len of the tile's last valid position (sorted descending), 0 with padding lanes
+    const int Lmin = __builtin_amdgcn_readlane(L, (int)min<int64_t>(15, a.n_dst - 1 - tile * 16));
+    for (int t = 0;;) {
+      if (t < Lmin) step(t, x, std::false_type{});
+      else step(t, x, std::true_type{});
+      if (++t >= Lmax) break;
       load_x(code, x);
       code = codes[t + 1];
-      step(t, x);
     }
     if (valid) {
       const float iS = __int_as_float((127 - eS) << 23);
@@ -1321,8 +1352,10 @@ template <int ACT>
 __device__ __forceinline__ float act_scaled(float zs, float c, float k, float cl, float laS, float So) {
   if constexpr (ACT == IGN_K_ACT_RELU) return zs > 0.f ? zs * k : 0.f;
   else if constexpr (ACT == IGN_K_ACT_SELU) {
+    // zs > 0: e = 1, so the negative arm is laS - laS = 0 and k max(zs, 0) + 0 = k zs; zs <= 0:
+    // k max(zs, 0) = 0.  The same bits as the select, without the compare and the select
     const float e = __builtin_amdgcn_exp2f(fminf(zs, 0.f) * cl);
-    return zs > 0.f ? k * zs : fmaf(laS, e, -laS);
+    return fmaf(k, fmaxf(zs, 0.f), fmaf(laS, e, -laS));
   } else if constexpr (ACT == IGN_K_ACT_LINEAR) return zs * k;
   else return So * act_t<ACT>(zs * c);
 }
@@ -1903,7 +1936,8 @@ hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, in
 
 hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (!args.Uh || args.hs_save || (h != 32 && h != 64) || (passes != 3 && passes != 4)) return hipErrorInvalidValue;
+  if (!args.Uh || !args.hdr || args.hs_save || (h != 32 && h != 64) || (passes != 3 && passes != 4))
+    return hipErrorInvalidValue;
   const int64_t work = grid_for(args.n_dst, 64);
 #define SEQ_H(HH, P)                                                                               \
   {                                                                                                \

@@ -96,15 +96,23 @@ class NativeDataset:
             dt, ptr, total, lens = C.c_int32(), C.c_void_p(), C.c_int64(), C.POINTER(C.c_int64)()
             check(lib.ign_dataset_batch_get(owner.handle, key.encode(), C.byref(dt), C.byref(ptr), C.byref(total),
                                             C.byref(lens)))
-            ctype = C.c_float if dt.value == 0 else C.c_int64
-            vals = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(max(total.value, 1),))[:total.value]
+            ctype, np_t = (C.c_float, np.float32) if dt.value == 0 else (C.c_int64, np.int64)
+            n = total.value
+            if n == 0 or not ptr.value:
+                vals = np.zeros(0, np_t)
+            else:
+                # a ctypes view of the gather's buffer that holds the owner: every array made from
+                # it (its numpy base chain ends here) keeps the ign_dataset_batch alive
+                buf = (ctype * n).from_address(ptr.value)
+                buf._owner = owner
+                vals = np.frombuffer(buf, dtype=np_t, count=n)
             glen = np.ctypeslib.as_array(lens, shape=(max(G, 1),))[:G].copy()
             return vals, glen
 
         arrays = {k: get(k) for k in keys}
         labels = get("__label__") if self.training else None
         bg = BatchedGraphs(arrays, G)
-        bg._owner = owner          # the arrays view the gather's buffers
+        bg._owner = owner          # (the arrays themselves also hold it)
         return bg, (None if labels is None else (labels[0].copy(), labels[1]))
 
     def close(self):

@@ -420,6 +420,11 @@ class Engine:
     def synchronize(self):
         check(lib.ign_synchronize(self.handle))
 
+    def trim_cache(self):
+        """Release the idle cached device blocks of this plan and the idle pinned host blocks
+        (ign_plan_trim_cache), e.g. when torch or RCCL run short of memory."""
+        check(lib.ign_plan_trim_cache(self.handle))
+
     def set_stream(self, hip_stream: int):
         """Run on an external HIP stream (e.g. ``torch.cuda.current_stream().cuda_stream``)."""
         check(lib.ign_plan_set_stream(self.handle, C.c_void_p(hip_stream)))

@@ -241,6 +241,11 @@ int  ign_plan_set_timing(ign_plan* plan, int32_t enabled);   /* also resets the 
  * default all.  Each event pair costs a few microseconds of queue time. */
 int  ign_plan_set_timing_kinds(ign_plan* plan, uint32_t kinds);
 int  ign_plan_set_stream(ign_plan* plan, void* hip_stream);
+/* Give the plan's idle cached device blocks (kept for the next batches, IGN_POOL_CACHE_GB) and the
+ * process's idle pinned host blocks (IGN_HOST_CACHE_GB) back to the runtime, waiting for the
+ * in-flight work that still reads them: call when another allocator (torch, RCCL) runs short.
+ * No reference counterpart (TF owns its allocator). */
+int  ign_plan_trim_cache(ign_plan* plan);
 
 int  ign_batch_create(ign_plan* plan, const ign_batch_desc* desc, ign_batch** out);
 void ign_batch_destroy(ign_batch* batch);

@@ -173,3 +173,27 @@ def test_prefetcher_keeps_job_order_and_raises_in_place():
     with pytest.raises(ValueError, match="bad batch"):
         next(pf)
     pf.close()
+
+
+def test_batch_arrays_keep_their_buffers_alive(tmp_path):
+    """NativeDataset.batch returns zero-copy views of the gather's buffers; an array taken out of
+    the BatchedGraphs must stay valid after the BatchedGraphs is dropped."""
+    import gc
+    from examples.make_example import make
+    from ignnition_amd import framework_operations as fo
+    from ignnition_amd.dataset import NativeDataset, plan_keys
+    from ignnition_amd.engine import MPPlan
+    d = make("routenet", str(tmp_path / "rn"), "nsfnet", 3)
+    fo.load_config(d + "/train_options.ini")
+    mi = fo.create_model()
+    ds = NativeDataset.for_model(fo.CONFIG["PATHS"]["train_dataset"], mi, training=True)
+    keys = plan_keys(MPPlan.from_model_info(mi))
+    bg, _ = ds.batch([0, 1, 2], keys)
+    key = next(k for k in keys if k.startswith("src_"))
+    arr = bg.arrays[key][0]
+    ref = arr.copy()
+    del bg
+    gc.collect()
+    for _ in range(3):   # reuse the freed memory if it were freed
+        ds.batch([2, 1, 0], keys)
+    np.testing.assert_array_equal(arr, ref)

@@ -294,3 +294,11 @@ def test_pooled_buffers_reused_and_poisoned(monkeypatch, kind):
         else:
             assert np.isfinite(pred).all() and np.isfinite(g.cpu().numpy()).all()
         b.close()
+    # ign_plan_trim_cache hands every idle block back (batch destroy no longer waits on the
+    # stream: the fences do); a batch built afterwards runs on fresh blocks, same bits
+    eng.trim_cache()
+    _, b, pred, loss, _, g = _engine_grads(desc, dims, graphs, labels, prm, eng=eng)
+    np.testing.assert_array_equal(pred, p0)
+    np.testing.assert_array_equal(g.cpu().numpy(), g0)
+    b.close()
+    eng.trim_cache()
