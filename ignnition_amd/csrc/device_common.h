@@ -118,11 +118,30 @@ __device__ __forceinline__ float act_t(float x) {
   if constexpr (ACT == IGN_K_ACT_RELU) return x > 0.f ? x : 0.f;
   else if constexpr (ACT == IGN_K_ACT_SELU) {   // branch-free: exp of min(x, 0), then select
     const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
-    const float e = __expf(fminf(x, 0.f));
+    const float e = __expf(__builtin_amdgcn_fmed3f(x, -3.0e38f, 0.f));   // min(x, 0), no canonicalise
     return x > 0.f ? lam * x : la * (e - 1.0f);
   } else if constexpr (ACT == IGN_K_ACT_SIGMOID) return sigmoidf_(x);
   else if constexpr (ACT == IGN_K_ACT_TANH) return tanhf_(x);
   else return x;
+}
+
+// max over the wave of a value >= 0 in every lane, in every lane: DPP row shifts (lane 15 of each
+// row of 16 ends with the row's max), two row broadcasts (lane 63 ends with the wave's), readlane.
+// No LDS round trip, unlike a __shfl_xor butterfly.
+// (The comparisons run on the bit patterns: non-negative floats order as unsigned integers, and an
+// integer max needs no canonicalising v_max_f32 x, x, x first.)
+__device__ __forceinline__ float wave_max_nonneg(float x) {
+  uint32_t v = __float_as_uint(x);
+#define IGN_DPP_MAX(ctrl, rmask) \
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, rmask, 0xf, true))
+  IGN_DPP_MAX(0x111, 0xf);   // row_shr:1
+  IGN_DPP_MAX(0x112, 0xf);   // row_shr:2
+  IGN_DPP_MAX(0x114, 0xf);   // row_shr:4
+  IGN_DPP_MAX(0x118, 0xf);   // row_shr:8
+  IGN_DPP_MAX(0x142, 0xa);   // row_bcast:15 into rows 1 and 3
+  IGN_DPP_MAX(0x143, 0xc);   // row_bcast:31 into rows 2 and 3
+#undef IGN_DPP_MAX
+  return __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)v, 63));
 }
 
 // XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (b, b+8, ...

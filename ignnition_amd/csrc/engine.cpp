@@ -142,6 +142,7 @@ int ign::repack(ign_plan* p) {
       HIP_TRY(launch_pack_w_bf16(p->d_params + cp.off_k, p->d_packed + cp.pk_wbf, cp.din, cp.H, p->stream));
     if (cp.pk_wt >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_k, cp.din, 3 * cp.H, p->d_packed + cp.pk_wt, p->stream));
     if (cp.pk_ut >= 0) HIP_TRY(launch_pack_a(p->d_params + cp.off_rk, cp.H, 3 * cp.H, p->d_packed + cp.pk_ut, p->stream));
+    if (cp.pk_uth >= 0) HIP_TRY(launch_pack_ut_f16(p->d_params + cp.off_rk, p->d_packed + cp.pk_uth, cp.H, p->stream));
   }
   for (auto& mp : p->mps)
     if (mp.feature_concat) {
@@ -219,6 +220,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_TRAIN_DENSE_H16")) p->train_dense_h16 = atoi(v) != 0;
   if (const char* v = getenv("IGN_TSGEMM_BF")) p->tsgemm_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
+  if (const char* v = getenv("IGN_TRAIN_SEQ_H16")) p->train_seq_h16 = atoi(v) != 0;
   if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(4, std::max(1, atoi(v)));
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
@@ -434,6 +436,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   for (auto& cp : p->cells) {
     if (!cp.used || !bwd_shape_supported(cp.H, cp.H)) continue;   // U^T: the recurrent backward
     cp.pk_ut = pk; pk = align(pk + 3LL * cp.H * cp.H);
+    if (pack_ut_f16_floats(cp.H)) { cp.pk_uth = pk; pk = align(pk + pack_ut_f16_floats(cp.H)); }
     if (!bwd_shape_supported(cp.din, cp.H)) continue;            // W^T (an axis-2 concat cell goes generic)
     cp.pk_wt = pk; pk = align(pk + 3LL * cp.din * cp.H);
   }

@@ -96,6 +96,7 @@ struct CellP {
   int64_t pk_ubf = -1;            // split-bf16 recurrent-kernel fragments (seq variants 4/5)
   int64_t pk_wh = -1;             // split-fp16 input-kernel fragments + scale (sum variant 8, DIN = H = 64)
   int64_t pk_uh = -1;             // split-fp16 recurrent-kernel fragments + scale (seq variants 6/7)
+  int64_t pk_uth = -1;            // backward: split-fp16 U fragments for dh = du . U^T (H = 32)
   bool used = false;
 };
 
@@ -261,6 +262,7 @@ struct ign_plan {
   bool train_dense_h16 = true;    // ... on the split-fp16 form of dense_bf (IGN_TRAIN_DENSE_H16=0: split-bf16)
   bool tsgemm_bf = true;          // weight-gradient row contractions on tsgemm_bf (IGN_TSGEMM_BF=0: f32 MFMA)
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
+  bool train_seq_h16 = true;      // training forward's ordered update on split-fp16 (IGN_TRAIN_SEQ_H16=0: bf16)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
                                   // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
@@ -282,7 +284,13 @@ struct ign_plan {
 
 // the ordered update of the training forward saves every step's state, which the split-fp16 kernels
 // (variants 6 / 7, inference only) do not: training runs the x6 split-bf16 form for them
-inline int train_seq_variant(const ign_plan* p) { return p->seq_variant >= 6 ? 4 : std::max(2, p->seq_variant); }
+// the training forward's ordered update: split-fp16 x3 with state saving (seq_gru_h16<SAVE>) where
+// the backward can recompute its gates bitwise (fused seq_gru_bwd, H = 32; IGN_TRAIN_SEQ_H16=0: the
+// split-bf16 x6 form), else split-bf16 x6 / f32
+inline int train_seq_variant(const ign_plan* p, int H) {
+  if (p->seq_variant == 6 && H == 32 && p->train_seq_h16 && p->bwd_bf && p->bwd_fuse) return 6;
+  return p->seq_variant >= 6 ? 4 : std::max(2, p->seq_variant);
+}
 
 
 struct ign_batch {

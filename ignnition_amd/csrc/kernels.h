@@ -111,6 +111,10 @@ hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStre
 // scale's exponent; floats used: 3 H^2 + 64
 hipError_t launch_pack_u_f16(const float* U, void* out, int H, hipStream_t st);
 inline int64_t pack_u_f16_floats(int H) { return (H == 32 || H == 64) ? 3LL * H * H + 64 : 0; }
+// U (unscaled, [H][3H]) as the A operand of dh = du . U^T in the ordered backward (rows: the H state
+// units, k: the 3H gate units in the chained order), scaled fp16 pieces + scale exponent; H = 32
+hipError_t launch_pack_ut_f16(const float* U, void* out, int H, hipStream_t st);
+inline int64_t pack_ut_f16_floats(int H) { return H == 32 ? 3LL * H * H + 64 : 0; }
 // [K][3H] input kernel -> the same scaled fp16 layout (K % 32 == 0) for sum variant 8
 hipError_t launch_pack_w_f16(const float* W, void* out, int K, int H, hipStream_t st);
 inline int64_t pack_w_f16_floats(int K, int H) { return ((H == 32 || H == 64) && K % 32 == 0) ? 3LL * K * H + 64 : 0; }

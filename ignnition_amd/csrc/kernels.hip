@@ -944,10 +944,10 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) 
 
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  // 6 / 7: split-fp16 h.U with 3 / 4 piece products (inference; training's state-saving forward
-  // runs the x6 bf16 form); 4 / 5: split-bf16 h.U with 6 / 9 piece products (kernels_bf.hip;
-  // H = 32, 64); 2: f32 MFMA
-  if ((variant == 6 || variant == 7) && (h == 32 || h == 64) && args.Uh && !args.hs_save)
+  // 6 / 7: split-fp16 h.U with 3 / 4 piece products (the state-saving training forward: 6 only);
+  // 4 / 5: split-bf16 h.U with 6 / 9 piece products (kernels_bf.hip; H = 32, 64); 2: f32 MFMA
+  if ((variant == 6 || variant == 7) && (h == 32 || h == 64) && args.Uh && args.hdr &&
+      (!args.hs_save || variant == 6))
     return launch_seq_gru_h16(args, h, variant == 6 ? 3 : 4, st);
   if (variant >= 6) variant = 4;
   if ((variant == 4 || variant == 5) && (h == 32 || h == 64))

@@ -212,7 +212,10 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 //   rc = 1 / ((1 + 2^(c acc_r + x_r)) SS)            (= r / SS)
 //   n' = S tanh2_(x_n + rc acc_n)                     (acc_n seeded with SS b_n)
 //   h' = n' + z (h' - n')
-template <int H, int PASSES>
+// SAVE (training forward, PASSES 3): also writes every state of the sequence to hs_save as
+// seq_gru_bf<SAVE> does (the state before, then the state after each step, unscaled), for the
+// backward's bitwise gate recompute (train_kernels.hip seq_gru_bwd_kernel<H, true, 2>).
+template <int H, int PASSES, bool SAVE = false>
 __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   constexpr int NT = H / 16, KS = H / 32;
   constexpr int NF = 6 * NT * KS;            // fragments: 2 pieces x 3 gates x NT tiles x KS k-steps
@@ -242,12 +245,17 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   // projected rows together.  No branch guards a load.
   int64_t tile = xcd_block(a.xcd_remap) * 4 + wave;
   i4v hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile, n_tiles - 1) * 16 + j));
+  // the previous tile's new states, stored once this tile's loads are issued (vmcnt: see SAVE)
+  f4 hout[NT];
+  int out_row = -1;
   for (; tile < n_tiles; tile += tile_stride) {
     const int64_t pos = tile * 16 + j;
     const bool valid = pos < a.n_dst;
     const int row = hd[0];
     const int L = hd[1];
     const uint32_t* codes = a.step_code + hd[2];
+    float* hsv = nullptr;
+    if constexpr (SAVE) hsv = a.hs_save + ((int64_t)hd[2] + pos) * H + 4 * g;
     f4 h[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -264,6 +272,18 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
         for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
     }
     uint32_t code = codes[1];
+    // every store is issued after the loads it would otherwise hold up (gfx9's vmcnt counts
+    // stores too, in issue order: a load issued after a store is waited for only with it)
+    if (out_row >= 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)out_row * H + 16 * t + 4 * g, hout[t]);
+    }
+    if constexpr (SAVE) {
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) st4(hsv + 16 * t, h[t]);
+      }
+    }
     hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile + tile_stride, n_tiles - 1) * 16 + j));
     // positions are sorted by final_len, descending: lane 0 (position tile * 16) is the longest
     const int Lmax = __builtin_amdgcn_readfirstlane(L);
@@ -285,6 +305,7 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
     const float S = __int_as_float((127 + eS) << 23);
     const float SS = __int_as_float((127 + eS + es) << 23);
     const float c = __int_as_float((127 - eS - es) << 23);
+    const float iS = __int_as_float((127 - eS) << 23);
     // every lane writes (and later reads back) exactly its own bias slots: no cross-lane hand-off
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -360,25 +381,40 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
         }
       }
     };
+    auto save = [&](int t) __attribute__((always_inline)) {   // the state after step t
+      if constexpr (SAVE) {
+        if (valid && t < L) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) st4(hsv + (int64_t)(t + 1) * H + 16 * i, h[i] * iS);
+        }
+      }
+    };
     // the projected row of step t is loaded at the start of step t and consumed by the gates after
     // the h.U MFMAs (a two-buffer one-step-ahead prefetch, loop unrolled by two, measured slower:
     // 0.242 vs 0.214 ms per launch, 144 VGPRs -> 3 waves per SIMD)
     // every tile has Lmax >= 1 (a destination without messages is rejected at batch build);
-    // Lmin: final_len of the tile's last valid position (sorted descending), 0 with padding lanes
+    // Lmin: final_len of the tile's last valid position (sorted descending); padding lanes of
+    // the last tile run the unmasked steps too, harmlessly (their rows are never stored)
     const int Lmin = __builtin_amdgcn_readlane(L, (int)min<int64_t>(15, a.n_dst - 1 - tile * 16));
     for (int t = 0;;) {
       if (t < Lmin) step(t, x, std::false_type{});
       else step(t, x, std::true_type{});
-      if (++t >= Lmax) break;
+      if (++t >= Lmax) {
+        save(t - 1);
+        break;
+      }
       load_x(code, x);
       code = codes[t + 1];
+      save(t - 1);
     }
-    if (valid) {
-      const float iS = __int_as_float((127 - eS) << 23);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t] * iS);
-    }
+    for (int t = 0; t < NT; ++t) hout[t] = h[t] * iS;
+    out_row = valid ? row : -1;
   }  // tile loop
+  if (out_row >= 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)out_row * H + 16 * t + 4 * g, hout[t]);
+  }
 }
 
 // U (pre-scaled as for pack_gru) -> sigma U as fp16 (hi, lo) A fragments of seq_gru_h16 (layout of
@@ -673,11 +709,8 @@ __global__ __launch_bounds__(64 * WAVES) void sum_gru_h16_kernel(SumGruArgs a) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int q = 0; q < 4; ++q) mh = fmaxf(mh, fabsf(h[t][q]));
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      mx = fmaxf(mx, __shfl_xor(mx, o));
-      mh = fmaxf(mh, __shfl_xor(mh, o));
-    }
+    mx = wave_max_nonneg(mx);
+    mh = wave_max_nonneg(mh);
     const int Ex = (__builtin_amdgcn_readfirstlane(__float_as_int(mx)) >> 23) - 126;
     const int Eh = (__builtin_amdgcn_readfirstlane(__float_as_int(mh)) >> 23) - 126;
     const int eK = min(100, min(15 - Ex + esW, 15 - Eh + esU));
@@ -1354,8 +1387,10 @@ __device__ __forceinline__ float act_scaled(float zs, float c, float k, float cl
   else if constexpr (ACT == IGN_K_ACT_SELU) {
     // zs > 0: e = 1, so the negative arm is laS - laS = 0 and k max(zs, 0) + 0 = k zs; zs <= 0:
     // k max(zs, 0) = 0.  The same bits as the select, without the compare and the select
-    const float e = __builtin_amdgcn_exp2f(fminf(zs, 0.f) * cl);
-    return fmaf(k, fmaxf(zs, 0.f), fmaf(laS, e, -laS));
+    // min / max as v_med3_f32 clamps: fminf / fmaxf would first canonicalise the MFMA result
+    // (an extra v_max_f32 x, x, x each, IEEE mode); the clamp bounds are never reached
+    const float e = __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(zs, -3.0e38f, 0.f) * cl);
+    return fmaf(k, __builtin_amdgcn_fmed3f(zs, 0.f, 3.0e38f), fmaf(laS, e, -laS));
   } else if constexpr (ACT == IGN_K_ACT_LINEAR) return zs * k;
   else return So * act_t<ACT>(zs * c);
 }
@@ -1408,9 +1443,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
     }
   }
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-    for (int t = 0; t < RT; ++t) mx[t] = fmaxf(mx[t], __shfl_xor(mx[t], o));
+  for (int t = 0; t < RT; ++t) mx[t] = wave_max_nonneg(mx[t]);
   float S[RT], S1S[RT], c1[RT], SS[RT], cSS[RT];
   h8 xf[RT][KS1][2];
 #pragma unroll
@@ -1619,8 +1652,7 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
 #pragma unroll
         for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fmaxf(fabsf(xv[s][0][q]), fabsf(xv[s][1][q])));
       }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      mx = wave_max_nonneg(mx);
       const int es = reinterpret_cast<const int*>(Wv + (int64_t)(M / 16) * KS * 2 * 64)[0];
       const int eS = min(60, max(-60, 15 - ((__builtin_amdgcn_readfirstlane(__float_as_int(mx)) >> 23) - 126)));
       const float S = __int_as_float((127 + eS) << 23);
@@ -1936,19 +1968,66 @@ hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, in
 
 hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (!args.Uh || !args.hdr || args.hs_save || (h != 32 && h != 64) || (passes != 3 && passes != 4))
+  if (!args.Uh || !args.hdr || (h != 32 && h != 64) || (passes != 3 && passes != 4) ||
+      (args.hs_save && passes != 3))
     return hipErrorInvalidValue;
   const int64_t work = grid_for(args.n_dst, 64);
-#define SEQ_H(HH, P)                                                                               \
+#define SEQ_H(HH, P, SV)                                                                           \
   {                                                                                                \
-    auto k = seq_gru_h16_kernel<HH, P>;                                                            \
+    auto k = seq_gru_h16_kernel<HH, P, SV>;                                                        \
     hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);                \
   }
-  if (h == 32 && passes == 3) SEQ_H(32, 3)
-  else if (h == 32) SEQ_H(32, 4)
-  else if (passes == 3) SEQ_H(64, 3)
-  else SEQ_H(64, 4)
+  if (args.hs_save) {
+    if (h == 32) SEQ_H(32, 3, true)
+    else SEQ_H(64, 3, true)
+  } else if (h == 32 && passes == 3) SEQ_H(32, 3, false)
+  else if (h == 32) SEQ_H(32, 4, false)
+  else if (passes == 3) SEQ_H(64, 3, false)
+  else SEQ_H(64, 4, false)
 #undef SEQ_H
+  return hipGetLastError();
+}
+
+// U [H][3H] (unscaled) -> sigma_t U as fp16 (hi, lo) A fragments over (rows: state unit m, k: gate
+// unit in the chained order kperm(s, g, jj) = 16 (2 s + (jj >> 2)) + 4 g + (jj & 3)), the layout
+// of du's accumulator registers read as the B operand; then sigma_t's exponent.  One block.
+// Fragment f = (piece * NT + mt) * KS3 + s, KS3 = 3H / 32.
+__global__ __launch_bounds__(1024) void pack_ut_f16_kernel(const float* __restrict__ U, uint16_t* __restrict__ out,
+                                                          int H) {
+  const int NT = H / 16, KS3 = 3 * H / 32, n = H * 3 * H;
+  __shared__ float red[1024];
+  float m = 0.f;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) m = fmaxf(m, fabsf(U[e]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  m = red[0];
+  int es = m > 0.f ? 15 - ((__float_as_int(m) >> 23) - 126) : 0;
+  es = min(100, max(-100, es));
+  const float sigma = __int_as_float((127 + es) << 23);
+  const int64_t total = 2LL * NT * KS3 * 64 * 8;
+  for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
+    const int jj = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    int64_t f = e >> 9;
+    const int s = (int)(f % KS3); f /= KS3;
+    const int mt = (int)(f % NT);
+    const int piece = (int)(f / NT);
+    const int row = 16 * mt + (lane & 15);
+    const int k = 16 * (2 * s + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
+    const float v = sigma * U[(int64_t)row * 3 * H + k];
+    const _Float16 hi = (_Float16)v;
+    const _Float16 pc = piece == 0 ? hi : (_Float16)(v - (float)hi);
+    out[e] = __builtin_bit_cast(uint16_t, pc);
+  }
+  if (threadIdx.x == 0) reinterpret_cast<int*>(out)[total / 2] = es;
+}
+
+hipError_t launch_pack_ut_f16(const float* U, void* out, int H, hipStream_t st) {
+  if (H != 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_ut_f16_kernel, dim3(1), dim3(1024), 0, st, U, static_cast<uint16_t*>(out), H);
   return hipGetLastError();
 }
 

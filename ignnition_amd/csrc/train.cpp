@@ -535,7 +535,9 @@ int ign_forward_train_mp(ign_plan* p, ign_batch* b) {
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
         a.hs_save = mt.hs[it];
         if (cp.pk_ubf >= 0) a.Ubf = p->d_packed + cp.pk_ubf;
-        HIP_TRY(launch_seq_gru(a, cp.H, train_seq_variant(p), st));
+        if (cp.pk_uh >= 0) a.Uh = p->d_packed + cp.pk_uh;
+        a.hdr = mb.d_seq_hdr;
+        HIP_TRY(launch_seq_gru(a, cp.H, train_seq_variant(p, cp.H), st));
       } else {
         SumGruArgs a{hin, hout, sb, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, p->d_packed + cp.pk_w,
                      p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
@@ -799,9 +801,13 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
         a.db_rec = gb + H3;
         a.db_in = gb;
         a.scratch = t->bsum;
-        // gate recompute on the forward's split-bf16 path when the forward ran seq_gru_bf x6
-        // (bitwise the forward's gates); IGN_BWD_BF=0 keeps the f32 MFMA recompute
-        if (p->bwd_bf && H == 32 && cp.pk_ubf >= 0 && train_seq_variant(p) == 4) a.Ubf = p->d_packed + cp.pk_ubf;
+        // gate recompute on the forward's path (bitwise the forward's gates): split-fp16 x3 after
+        // seq_gru_h16<SAVE>, split-bf16 x6 after seq_gru_bf x6; IGN_BWD_BF=0 keeps the f32 MFMA recompute
+        if (p->bwd_bf && H == 32 && cp.pk_uh >= 0 && cp.pk_uth >= 0 && train_seq_variant(p, H) == 6) {
+          a.Uh = p->d_packed + cp.pk_uh;
+          a.Uth = p->d_packed + cp.pk_uth;
+        }
+        else if (p->bwd_bf && H == 32 && cp.pk_ubf >= 0 && train_seq_variant(p, H) == 4) a.Ubf = p->d_packed + cp.pk_ubf;
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
       } else {
         HIP_TRY(launch_seq_gru_bwd(a, H, st));

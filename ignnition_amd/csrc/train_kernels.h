@@ -30,6 +30,8 @@ struct SeqBwdArgs {
   float* db_in = nullptr;    // [3H] input-bias gradient (accumulated)
   float* scratch = nullptr;  // [(H + 1) * 3H] reduction target
   const void* Ubf = nullptr; // fused, H = 32: U's split-bf16 pieces (pack_u_bf16) -> gate recompute as seq_gru_bf x6
+  const void* Uh = nullptr;  // fused, H = 32: U's scaled fp16 pieces (pack_u_f16) -> gate recompute as seq_gru_h16 x3
+  const void* Uth = nullptr; // with Uh: U's scaled fp16 pieces as dh = du . U^T's A operand (pack_ut_f16)
 };
 
 // Backward of the sum update (AUX:752-765): one GRU step per destination row.

@@ -71,31 +71,48 @@ __global__ void pack_a_kernel(const float* __restrict__ M, int rows, int cols, f
 // k-step ks).  Each wave writes one (H + 2) x 3H partial (row H: the column sums of da = b_in's
 // gradient, row H + 1: those of du = b_rec's; they differ in the h gate only, dc vs dc r), so no
 // separate column-sum pass over ga is needed; launch_seq_gru_bwd reduces the partials in a fixed order.
-// BF (H = 32): the gate recompute h.U runs on the forward's split-bf16 path (seq_gru_bf x6: the
-// same pieces, MFMA order and bias seeding), so the recomputed gates are bitwise the forward's.
-template <int H, bool FUSE, bool BF = false>
+// RC, the gate recompute of h.U (H = 32), on the forward's own path so that the recomputed gates
+// are bitwise the forward's (the same pieces, scales, MFMA order and bias seeding):
+// 0: f32 MFMA (seq_gru2); 1: split-bf16 x6 (seq_gru_bf); 2: scaled split-fp16 x3 (seq_gru_h16<SAVE>,
+// the tile's state scale recomputed from its saved first states exactly as the forward formed it).
+template <int H, bool FUSE, int RC = 0>
 __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   constexpr int NT = H / 16, KH = H / 4, K3 = 3 * H / 4, KS = H / 32;
+  constexpr bool BF = RC == 1, H16 = RC == 2;
   constexpr bool LDSU = H <= 32;
   static_assert(!FUSE || LDSU, "fused dU: H 16 / 32");
-  static_assert(!BF || H == 32, "split-bf16 recompute: H 32");
-  constexpr int NUP = LDSU && !BF ? 3 * NT * KH * 64 : 1, NUT = LDSU ? NT * K3 * 64 : 1;
+  static_assert(RC == 0 || H == 32, "split recompute: H 32");
+  constexpr int KS3 = 3 * H / 32;                  // H16: k-steps of dh = du . U^T on 16x16x32
+  constexpr int NUP = LDSU && RC == 0 ? 3 * NT * KH * 64 : 1, NUT = LDSU && !H16 ? NT * K3 * 64 : 1;
   constexpr int NUB = BF ? 9 * NT * KS * 64 : 1;   // bf8 fragments of U's pieces
+  constexpr int NUH = H16 ? 6 * NT * KS * 64 : 1;  // h8 fragments of sigma U's fp16 pieces
+  constexpr int NUTH = H16 ? 2 * NT * KS3 * 64 : 1;   // h8 fragments of sigma_t U (dh's A operand)
   constexpr int NTR = FUSE ? 4 * 3 * H * 16 : 1;   // per-wave transpose tiles
   __shared__ float sUp[NUP];
   __shared__ bf8 sUb[NUB];
+  __shared__ h8 sUh[NUH];
+  __shared__ h8 sUth[NUTH];
   __shared__ float sUt[NUT];
   __shared__ float sT[NTR];
+  int es = 0, est = 0;   // H16: sigma's and sigma_t's exponents (pack_u_f16_kernel, pack_ut_f16_kernel)
   if constexpr (LDSU) {
     if constexpr (BF) {
       for (int e = threadIdx.x; e < NUB; e += blockDim.x)
         reinterpret_cast<u4v*>(sUb)[e] = static_cast<const u4v*>(a.Ubf)[e];
+    } else if constexpr (H16) {
+      for (int e = threadIdx.x; e < NUH; e += blockDim.x)
+        reinterpret_cast<u4v*>(sUh)[e] = static_cast<const u4v*>(a.Uh)[e];
+      es = __float_as_int(static_cast<const float*>(a.Uh)[(int64_t)NUH * 4]);
+      for (int e = threadIdx.x; e < NUTH; e += blockDim.x)
+        reinterpret_cast<u4v*>(sUth)[e] = static_cast<const u4v*>(a.Uth)[e];
+      est = __float_as_int(static_cast<const float*>(a.Uth)[(int64_t)NUTH * 4]);
     } else {
       for (int e = threadIdx.x; e < NUP / 4; e += blockDim.x)
         reinterpret_cast<f4*>(sUp)[e] = reinterpret_cast<const f4*>(a.Up)[e];
     }
-    for (int e = threadIdx.x; e < NUT / 4; e += blockDim.x)
-      reinterpret_cast<f4*>(sUt)[e] = reinterpret_cast<const f4*>(a.Ut)[e];
+    if constexpr (!H16)
+      for (int e = threadIdx.x; e < NUT / 4; e += blockDim.x)
+        reinterpret_cast<f4*>(sUt)[e] = reinterpret_cast<const f4*>(a.Ut)[e];
     __syncthreads();
   }
   const float* Up = LDSU ? sUp : a.Up;
@@ -134,21 +151,49 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
     f4 bh[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) bh[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+    // H16: the forward's tile scale, from the tile's first states (saved as read): S = 2^(15 - E),
+    // m = max(1, max |h_0|) = f 2^E; SS = S sigma, cS = 1 / SS
+    float S = 1.f, SS = 1.f, cS = 1.f;
+    if constexpr (H16) {
+      float m = 1.0f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f4 v = ld4(a.hs + hbase * H + 16 * t + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m = fmaxf(m, valid ? fabsf(v[r]) : 0.f);
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(m)) >> 23) - 126;
+      const int eS = 15 - E;
+      S = __int_as_float((127 + eS) << 23);
+      SS = __int_as_float((127 + eS + es) << 23);
+      cS = __int_as_float((127 - eS - es) << 23);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bh[t] *= SS;   // the candidate accumulator's seed, as sbn
+    }
 
+    // A step's state row and projected rows are loaded during the step before it (in the reverse
+    // order), before that step's stores: gfx9's vmcnt counts stores too, in issue order, so a load
+    // issued after a store would be waited for with it.  A lane past its sequence reads step 0.
+    f4 hp[NT], x[3][NT];
+    auto load_step = [&](int st, uint32_t code) __attribute__((always_inline)) {
+      const int64_t hr = hbase + (st < L ? st : 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
+#pragma unroll
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
+    };
+    auto code_of = [&](int st) { return a.step_code[sp + (st < L ? st : 0)]; };
+    load_step(Lmax - 1, code_of(Lmax - 1));
     for (int step = Lmax - 1; step >= 0; --step) {
       const bool act = step < L;
       const int64_t tt = act ? step : 0;
       const int64_t i = sp + tt;
       const int64_t hr = hbase + tt;
-      f4 hp[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
-      const uint32_t code = a.step_code[i];
-      f4 x[3][NT];
-#pragma unroll
-      for (int G = 0; G < 3; ++G)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
+      const uint32_t code_next = step > 0 ? code_of(step - 1) : 0u;
       // opaque lane offset: keeps the loop-invariant fragment reads inside the step loop (registers)
       int lofs = lane;
       asm volatile("" : "+v"(lofs));
@@ -159,7 +204,40 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         ar[t] = f4{0, 0, 0, 0};
         ah[t] = bh[t];
       }
-      if constexpr (BF) {
+      if constexpr (H16) {
+        h8 hf[2][KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          u4v w0, w1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e0 = 2 * q, e1 = 2 * q + 1;
+            const hpair p = split2h(S * hp[2 * s + (e0 >> 2)][e0 & 3], S * hp[2 * s + (e1 >> 2)][e1 & 3]);
+            w0[q] = p.hi;
+            w1[q] = p.lo;
+          }
+          hf[0][s] = __builtin_bit_cast(h8, w0);
+          hf[1][s] = __builtin_bit_cast(h8, w1);
+        }
+        // seq_gru_h16's order: U lo x h hi, then U hi x {h lo, h hi}
+#pragma unroll
+        for (int pu = 1; pu >= 0; --pu)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const h8 wz = sUh[(((pu * 3 + 0) * NT + t) * KS + s) * 64 + lofs];
+              const h8 wr = sUh[(((pu * 3 + 1) * NT + t) * KS + s) * 64 + lofs];
+              const h8 wh = sUh[(((pu * 3 + 2) * NT + t) * KS + s) * 64 + lofs];
+#pragma unroll
+              for (int ph = 1; ph >= 0; --ph) {
+                if (pu + ph > 1) continue;
+                az[t] = MFMA_H(wz, hf[ph][s], az[t]);
+                ar[t] = MFMA_H(wr, hf[ph][s], ar[t]);
+                ah[t] = MFMA_H(wh, hf[ph][s], ah[t]);
+              }
+            }
+      } else if constexpr (BF) {
         bf8 hf[3][KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -211,10 +289,19 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
       for (int t = 0; t < NT; ++t) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float z = sig2_(az[t][r] + x[0][t][r]);
-          const float rr = sig2_(ar[t][r] + x[1][t][r]);
-          const float c = tanh2_(x[2][t][r] + rr * ah[t][r]);
-          const float uh = ah[t][r] * kInv2Log2e;
+          float z, rr, c, uh;
+          if constexpr (H16) {   // seq_gru_h16's gate arithmetic on the scaled accumulators
+            z = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(az[t][r], cS, x[0][t][r])));
+            const float rc = rcpf_(fmaf(__builtin_amdgcn_exp2f(fmaf(ar[t][r], cS, x[1][t][r])), SS, SS));
+            c = tanh2_(fmaf(rc, ah[t][r], x[2][t][r]));
+            rr = rc * SS;
+            uh = ah[t][r] * cS * kInv2Log2e;
+          } else {
+            z = sig2_(az[t][r] + x[0][t][r]);
+            rr = sig2_(ar[t][r] + x[1][t][r]);
+            c = tanh2_(x[2][t][r] + rr * ah[t][r]);
+            uh = ah[t][r] * kInv2Log2e;
+          }
           const float d = act ? dh[t][r] : 0.f;
           const float dzp = d * (hp[t][r] - c) * z * (1.f - z);
           const float dcp = d * (1.f - z) * (1.f - c * c);
@@ -226,6 +313,16 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
           acc[t][r] = dh[t][r] * z;
         }
       }
+      f4 af[NT];
+      if constexpr (FUSE) {   // h_prev through the transpose tile, before hp is reloaded
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) R[(16 * t + 4 * g + q) * 16 + wofs] = hp[t][q];
+#pragma unroll
+        for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
+      }
+      if (step > 0) load_step(step - 1, code_next);
       if (act) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -242,13 +339,6 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         }
       }
       if constexpr (FUSE) {   // dU += h_prev^T du over the tile's 16 rows (inactive rows: du = 0)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) R[(16 * t + 4 * g + q) * 16 + wofs] = hp[t][q];
-        f4 af[NT];
-#pragma unroll
-        for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -274,12 +364,66 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         }
       }
       // dh_prev = dh' z + du . U^T   (k over the 3H gate units, gate-major)
+      if constexpr (H16) {
+        // scaled split-fp16 x3 on 16x16x32: du is already the chained B operand (k-step s = gate
+        // tiles 2s, 2s+1 = z, r, h for H = 32).  B's column n is the tile's row j, so each row
+        // gets a scale of its own, Sd = 2^(15 - E(max |du| over the row's 3H values: lanes j,
+        // j + 16, j + 32, j + 48)): its fp16 pieces neither overflow nor lose bits however the
+        // rows' gradients differ in size; the seed dh' z and the result carry Sd sigma_t per lane
+        uint32_t mb = 0;   // max |du| as the bit pattern (non-negative floats order as integers)
 #pragma unroll
-      for (int s = 0; s < K3; ++s) {
-        const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
-        const float b = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = MFMA(Ut[frag_idx(t, s, K3, lofs)], b, acc[t]);
+          for (int r = 0; r < 4; ++r)
+            mb = max(mb, max(__float_as_uint(fabsf(gz[t][r])),
+                             max(__float_as_uint(fabsf(gr[t][r])), __float_as_uint(fabsf(guh[t][r])))));
+        {
+          const auto s32 = __builtin_amdgcn_permlane32_swap(mb, mb, false, false);   // lanes l, l ^ 32
+          mb = max(s32[0], s32[1]);
+          const auto s16 = __builtin_amdgcn_permlane16_swap(mb, mb, false, false);   // lanes l, l ^ 16
+          mb = max(s16[0], s16[1]);
+        }
+        const int eSd = mb ? min(60, max(-100, 15 - ((int)(mb >> 23) - 126))) : 0;
+        const float Sd = __int_as_float((127 + eSd) << 23);
+        const float seed = __int_as_float((127 + eSd + est) << 23);
+        const float unseed = __int_as_float((127 - eSd - est) << 23);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] *= seed;
+        // one k-step at a time (its two B pieces live only for its 3 x NT products: registers)
+#pragma unroll
+        for (int s = 0; s < KS3; ++s) {
+          const f4* src = s == 0 ? gz : s == 1 ? gr : guh;
+          u4v w0, w1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e0 = 2 * q, e1 = 2 * q + 1;
+            const hpair p = split2h(Sd * src[e0 >> 2][e0 & 3], Sd * src[e1 >> 2][e1 & 3]);
+            w0[q] = p.hi;
+            w1[q] = p.lo;
+          }
+          const h8 bf[2] = {__builtin_bit_cast(h8, w0), __builtin_bit_cast(h8, w1)};
+#pragma unroll
+          for (int pu = 1; pu >= 0; --pu)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const h8 w = sUth[((pu * NT + t) * KS3 + s) * 64 + lofs];
+#pragma unroll
+              for (int ph = 1; ph >= 0; --ph) {
+                if (pu + ph > 1) continue;
+                acc[t] = MFMA_H(w, bf[ph], acc[t]);
+              }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] *= unseed;
+      } else {
+#pragma unroll
+        for (int s = 0; s < K3; ++s) {
+          const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
+          const float b = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = MFMA(Ut[frag_idx(t, s, K3, lofs)], b, acc[t]);
+        }
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -946,7 +1090,7 @@ bool seq_bwd_fused_supported(int h) { return h == 16 || h == 32; }
 
 int64_t seq_bwd_partial_floats(int h) { return (int64_t)(kBwdMaxWaves + kTsSegs) * (h + 2) * 3 * h; }
 
-template <int H, bool BF>
+template <int H, int RC>
 static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
   static int cus = 0;
   if (!cus) {
@@ -956,12 +1100,12 @@ static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
     if (cus <= 0) cus = 256;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, seq_gru_bwd_kernel<H, true, BF>, 256, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, seq_gru_bwd_kernel<H, true, RC>, 256, 0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 1;
   const int64_t tiles = (a.n_dst + 15) / 16;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>({(tiles + 3) / 4, (int64_t)per_cu * cus, kBwdMaxWaves / 4}));
-  hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true, BF>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true, RC>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // rows 0..H (dU, da sums) into scratch, row H + 1 (du sums) straight into db_rec
@@ -977,15 +1121,15 @@ hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
   if (a.n_dst == 0) return hipSuccess;
   if (a.part) {   // fused dU / b_rec(h) gradients
     if (!a.dU || !a.db_rec || !a.db_in || !a.scratch) return hipErrorInvalidValue;
-    if (h == 16) return seq_bwd_fused<16, false>(a, st);
-    if (h == 32) return a.Ubf ? seq_bwd_fused<32, true>(a, st) : seq_bwd_fused<32, false>(a, st);
+    if (h == 16) return seq_bwd_fused<16, 0>(a, st);
+    if (h == 32) return a.Uh ? seq_bwd_fused<32, 2>(a, st) : a.Ubf ? seq_bwd_fused<32, 1>(a, st) : seq_bwd_fused<32, 0>(a, st);
     return hipErrorInvalidValue;
   }
   if (!a.gu) return hipErrorInvalidValue;
   dim3 grid((unsigned)((a.n_dst + 63) / 64));
-  if (h == 16) hipLaunchKernelGGL((seq_gru_bwd_kernel<16, false>), grid, dim3(256), 0, st, a);
-  else if (h == 32) hipLaunchKernelGGL((seq_gru_bwd_kernel<32, false>), grid, dim3(256), 0, st, a);
-  else if (h == 64) hipLaunchKernelGGL((seq_gru_bwd_kernel<64, false>), grid, dim3(256), 0, st, a);
+  if (h == 16) hipLaunchKernelGGL((seq_gru_bwd_kernel<16, false, 0>), grid, dim3(256), 0, st, a);
+  else if (h == 32) hipLaunchKernelGGL((seq_gru_bwd_kernel<32, false, 0>), grid, dim3(256), 0, st, a);
+  else if (h == 64) hipLaunchKernelGGL((seq_gru_bwd_kernel<64, false, 0>), grid, dim3(256), 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

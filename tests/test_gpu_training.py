@@ -231,24 +231,58 @@ def test_gradients_readout_operations(case):
     _check(desc, dims, graphs, labels, prm)
 
 
+def _rel_err_vs_oracle(desc, dims, graphs, labels, prm, gflat, layout):
+    """Relative L2 error of a flat engine gradient against torch autograd of the float64 restatement."""
+    _, _, og, _ = TorchOracle(desc, dims, prm).loss_and_grads(graphs, labels)
+    named = {name: gflat[off:off + int(np.prod(shape))].reshape(shape) for name, shape, off in layout}
+    num = sum(float(np.sum((named[k].astype(np.float64) - v) ** 2)) for k, v in og.items())
+    return (num / sum(float(np.sum(v ** 2)) for v in og.values())) ** 0.5
+
+
 def test_fused_backward_is_deterministic_and_matches_unfused(monkeypatch):
     """The ordered backward forms dU from per-wave partials reduced in a fixed order: two runs are
-    bitwise equal, and the result agrees with the du-buffer + row-contraction form (IGN_BWD_FUSE=0)
-    to fp32 reassociation."""
-    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "synth50", 24)
+    bitwise equal.  Against the du-buffer + row-contraction form (IGN_BWD_FUSE=0, which also runs
+    the split-bf16 training forward): both within the same distance of float64 autograd.  (On
+    synth50 batches every fp32 evaluation of this gradient sits ~7e-5 (relative L2) from float64,
+    dominated by the forward's rounding, so two forms whose FORWARDS round differently differ by
+    that much)"""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "synth50", 6)
     prm = MPPlan.from_model_info(mi).init_params(11, bias_scale=0.1)
-    g1 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    eng, _, _, _, _, g1 = _engine_grads(desc, dims, graphs, labels, prm)
+    g1 = g1.cpu().numpy()
     g2 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
     np.testing.assert_array_equal(g1, g2)
     monkeypatch.setenv("IGN_BWD_FUSE", "0")
     g3 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
-    assert np.linalg.norm(g1.astype(np.float64) - g3) <= 1e-5 * np.linalg.norm(g3)
+    e1 = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g1, eng.layout)
+    e3 = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g3, eng.layout)
+    print("vs float64 autograd: fused %.3g, unfused %.3g" % (e1, e3))
+    assert e1 <= max(1.25 * e3, 1e-6) and e1 <= GTOL
 
 
-@pytest.mark.parametrize("switch", ["IGN_TSGEMM_BF", "IGN_BWD_BF", "IGN_TRAIN_DENSE_BF", "IGN_TRAIN_DENSE_H16"])
+@pytest.mark.parametrize("switch", ["IGN_BWD_BF", "IGN_TRAIN_SEQ_H16"])
+def test_split_ordered_training_is_fp32_accurate(monkeypatch, switch):
+    """The training forward's split-fp16 ordered update (seq_gru_h16<SAVE>) with the backward's
+    bitwise gate recompute and split-fp16 dh = du . U^T (per-row du scales), against the split-bf16
+    forward + f32 recompute (IGN_BWD_BF=0) and the split-bf16 forward + recompute
+    (IGN_TRAIN_SEQ_H16=0): bitwise deterministic, and no farther from float64 autograd."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "synth50", 6)
+    prm = MPPlan.from_model_info(mi).init_params(13, bias_scale=0.1)
+    eng, _, _, _, _, g1 = _engine_grads(desc, dims, graphs, labels, prm)
+    g1 = g1.cpu().numpy()
+    np.testing.assert_array_equal(g1, _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy())
+    monkeypatch.setenv(switch, "0")
+    g0 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    assert not np.array_equal(g0, g1)   # the switch took effect
+    e1 = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g1, eng.layout)
+    e0 = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g0, eng.layout)
+    print("%s: vs float64 autograd, default %.3g, off %.3g" % (switch, e1, e0))
+    assert e1 <= max(1.25 * e0, 1e-6) and e1 <= GTOL
+
+
+@pytest.mark.parametrize("switch", ["IGN_TSGEMM_BF", "IGN_TRAIN_DENSE_BF", "IGN_TRAIN_DENSE_H16"])
 def test_split_bf16_backward_matches_f32(monkeypatch, switch):
-    """The split-bf16 weight-gradient contractions (tsgemm_bf) and the split-bf16 gate recompute of
-    the ordered backward (the forward's x6 path) against their f32-MFMA forms, and the training
+    """The split-bf16 weight-gradient contractions (tsgemm_bf) against their f32-MFMA form, and the training
     Dense layers' split-fp16 row GEMMs (IGN_TRAIN_DENSE_H16, forward and backward) against their
     split-bf16 form: bitwise deterministic, and equal to fp32 reassociation (relative L2 <= 1e-5)
     on 24 synth50 graphs."""
