@@ -245,9 +245,6 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   // projected rows together.  No branch guards a load.
   int64_t tile = xcd_block(a.xcd_remap) * 4 + wave;
   i4v hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile, n_tiles - 1) * 16 + j));
-  // the previous tile's new states, stored once this tile's loads are issued (vmcnt: see SAVE)
-  f4 hout[NT];
-  int out_row = -1;
   for (; tile < n_tiles; tile += tile_stride) {
     const int64_t pos = tile * 16 + j;
     const bool valid = pos < a.n_dst;
@@ -272,12 +269,6 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
         for (int i = 0; i < NT; ++i) x[G][i] = ld4(p + G * H + 16 * i);
     }
     uint32_t code = codes[1];
-    // every store is issued after the loads it would otherwise hold up (gfx9's vmcnt counts
-    // stores too, in issue order: a load issued after a store is waited for only with it)
-    if (out_row >= 0) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)out_row * H + 16 * t + 4 * g, hout[t]);
-    }
     if constexpr (SAVE) {
       if (valid) {
 #pragma unroll
@@ -399,22 +390,16 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
     for (int t = 0;;) {
       if (t < Lmin) step(t, x, std::false_type{});
       else step(t, x, std::true_type{});
-      if (++t >= Lmax) {
-        save(t - 1);
-        break;
-      }
+      save(t);
+      if (++t >= Lmax) break;
       load_x(code, x);
       code = codes[t + 1];
-      save(t - 1);
     }
+    if (valid) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) hout[t] = h[t] * iS;
-    out_row = valid ? row : -1;
+      for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t] * iS);
+    }
   }  // tile loop
-  if (out_row >= 0) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)out_row * H + 16 * t + 4 * g, hout[t]);
-  }
 }
 
 // U (pre-scaled as for pack_gru) -> sigma U as fp16 (hi, lo) A fragments of seq_gru_h16 (layout of
