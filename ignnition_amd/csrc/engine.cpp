@@ -520,8 +520,16 @@ int ign_plan_set_params(ign_plan* p, const float* params, int32_t on_device) {
   return IGN_OK;
 }
 
+namespace {
+// timed launches record event pairs into a ring on the plan; they are resolved lazily
+constexpr int kMaxPendingEvents = 1 << 14;
+int flush_timing(ign_plan* p);
+void drop_timing(ign_plan* p);
+}  // namespace
+
 int ign_plan_set_timing(ign_plan* p, int32_t enabled) {
   if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  drop_timing(p);
   p->timing = enabled != 0;
   p->stats = ign_stats_t{};
   return IGN_OK;
@@ -529,6 +537,7 @@ int ign_plan_set_timing(ign_plan* p, int32_t enabled) {
 
 int ign_plan_set_timing_kinds(ign_plan* p, uint32_t kinds) {
   if (!p) return fail(IGN_ERR_INVALID, "null plan");
+  drop_timing(p);
   p->timing_kinds = kinds;
   p->stats = ign_stats_t{};
   return IGN_OK;
@@ -538,6 +547,7 @@ int ign_plan_set_stream(ign_plan* p, void* s) {
   if (!p) return fail(IGN_ERR_INVALID, "null plan");
   int rc = ensure_device(p);
   if (rc) return rc;
+  if ((rc = flush_timing(p))) return rc;   // pending event pairs were recorded on the old stream
   if (p->own_stream && p->stream) {
     hipStreamSynchronize(p->stream);
     hipStreamDestroy(p->stream);
@@ -1101,6 +1111,7 @@ struct Timer {
   void begin(int kind, double flops, double bytes, double mfma_bf16 = 0, double mfma_f32 = 0) {
     on = p->timing && ((p->timing_kinds >> kind) & 1u);
     if (!on) return;
+    if (p->ev_slot >= kMaxPendingEvents) flush_timing(p);
     const int slot = p->ev_slot;
     size_t need = 2 * (slot + 1);
     while (p->ev.size() < need) {
@@ -1169,7 +1180,6 @@ int check_pb(ign_plan* p, ign_batch* b) {
 int ign_forward_begin(ign_plan* p, ign_batch* b) {
   int rc = check_pb(p, b);
   if (rc) return rc;
-  p->ev_slot = 0;
   Timer tm{p};
   for (int e = 0; e < (int)p->ents.size(); ++e) {   // GM:396-400 (owned rows; halo rows come from peers)
     const int H = p->ents[e].hidden_dim, F = p->ents[e].feature_total;
@@ -1355,6 +1365,22 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
 
 namespace {
 
+int accumulate_stats(ign_plan* p, int n, const int* kind, const EvCost* cost);
+
+// Resolve the pending event pairs of timed launches into the statistics (one host wait).
+int flush_timing(ign_plan* p) {
+  if (p->ev_slot == 0) return IGN_OK;
+  const int n = p->ev_slot;
+  p->ev_slot = 0;
+  return accumulate_stats(p, n, p->ev_kind.data(), p->ev_cost.data());
+}
+
+// Forget the pending event pairs (the statistics are being reset).
+void drop_timing(ign_plan* p) {
+  if (p->ev_slot && p->stream) hipStreamSynchronize(p->stream);
+  p->ev_slot = 0;
+}
+
 int accumulate_stats(ign_plan* p, int n, const int* kind, const EvCost* cost) {
   HIP_TRY(hipStreamSynchronize(p->stream));
   ign_stats_t& s = p->stats;
@@ -1502,11 +1528,7 @@ int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
   int rc = check_pb(p, b);
   if (rc) return rc;
   if ((rc = readout(p, b))) return rc;
-  if ((rc = copy_out(p, b, pred_out))) return rc;
-  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_cost.data())))
-    return rc;
-  p->ev_slot = 0;
-  return IGN_OK;
+  return copy_out(p, b, pred_out);   // timed launches stay pending until ign_stats (flush_timing)
 }
 
 int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
@@ -1529,11 +1551,9 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
     return IGN_OK;
   }
   if ((rc = forward_body(p, b))) return rc;
-  if ((rc = copy_out(p, b, pred_out))) return rc;
-  if (p->timing && (rc = accumulate_stats(p, p->ev_slot, p->ev_kind.data(), p->ev_cost.data())))
-    return rc;
-  p->ev_slot = 0;
-  return IGN_OK;
+  // the event pairs stay pending (no host wait per forward, so the next forward queues behind
+  // this one); ign_stats resolves them
+  return copy_out(p, b, pred_out);
 }
 
 int ign_batch_mp_split(const ign_batch* b, int32_t mi, int64_t* interior, int64_t* boundary) {
@@ -1599,6 +1619,8 @@ int ign_batch_state(ign_plan* p, ign_batch* b, int32_t e, float* host_out) {
 
 int ign_stats(const ign_plan* p, ign_stats_t* out) {
   if (!p || !out) return fail(IGN_ERR_INVALID, "null argument");
+  int rc = flush_timing(const_cast<ign_plan*>(p));   // the plan's own bookkeeping; the ABI keeps const
+  if (rc) return rc;
   *out = p->stats;
   return IGN_OK;
 }

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include "kernels.h"
 
@@ -28,6 +29,10 @@ int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) {
   }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  // IGN_PERSIST_CAP (probe): at most this many resident blocks per CU, leaving the other wave
+  // slots to a kernel on another stream
+  static const int cap = getenv("IGN_PERSIST_CAP") ? atoi(getenv("IGN_PERSIST_CAP")) : 0;
+  if (cap > 0) per_cu = std::min(per_cu, cap);
   const int64_t g = (int64_t)per_cu * cus;
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, n_blocks_of_work));
 }
