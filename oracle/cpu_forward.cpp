@@ -58,40 +58,82 @@ inline T act(T x, int a) {
   }
 }
 
+// act over a row, the switch hoisted so that each arm vectorises (libmvec expf under -ffast-math)
+template <typename T>
+void act_row(T* __restrict__ x, int n, int a) {
+  switch (a) {
+    case IGN_ACT_RELU:
+      for (int j = 0; j < n; ++j) x[j] = act(x[j], IGN_ACT_RELU);
+      break;
+    case IGN_ACT_SELU:
+      for (int j = 0; j < n; ++j) x[j] = act(x[j], IGN_ACT_SELU);
+      break;
+    case IGN_ACT_SIGMOID:
+      for (int j = 0; j < n; ++j) x[j] = act(x[j], IGN_ACT_SIGMOID);
+      break;
+    case IGN_ACT_TANH:
+      for (int j = 0; j < n; ++j) x[j] = act(x[j], IGN_ACT_TANH);
+      break;
+    default:
+      break;
+  }
+}
+
 struct Cell {
   int din, H;
   const float *W, *U, *b;   // [din][3H], [H][3H], [2][3H]
 };
 
+// R Keras GRU steps of independent rows: out[r] = GRU(x[r], h[r]), for the compile-time widths of
+// the example models.
+template <int DIN, int H, typename T, int R>
+void gru_rows_t(const Cell& c, const T* const* x, const T* const* h, T* const* out) {
+  constexpr int H3 = 3 * H, VL = 32 / sizeof(T), NV = 3, JB = NV * VL;
+  static_assert(H3 % JB == 0, "column blocks");
+  typedef T V __attribute__((vector_size(32)));
+  T mx[R][H3], mh[R][H3];
+  // R rows x NV vectors of accumulators (12 AVX2 registers at R = 4): each weight vector loaded
+  // from L1/L2 feeds R FMAs (the 2 x 64 x 192 weights of H = 64 do not fit L1)
+  auto block = [&](const T* const* in, const float* __restrict__ M, const float* bias, int K, T (*dst)[H3],
+                   int j0) __attribute__((always_inline)) {
+    V a[R][NV];
+    for (int v = 0; v < NV; ++v) {
+      V bv;
+      for (int l = 0; l < VL; ++l) bv[l] = bias[j0 + v * VL + l];
+      for (int r = 0; r < R; ++r) a[r][v] = bv;
+    }
+    for (int k = 0; k < K; ++k) {
+      const float* w = M + (int64_t)k * H3 + j0;
+      V wv[NV];
+      for (int v = 0; v < NV; ++v)
+        for (int l = 0; l < VL; ++l) wv[v][l] = w[v * VL + l];
+      for (int r = 0; r < R; ++r) {
+        const T xv = in[r][k];
+        for (int v = 0; v < NV; ++v) a[r][v] += xv * wv[v];
+      }
+    }
+    for (int r = 0; r < R; ++r) memcpy(&dst[r][j0], a[r], sizeof a[r]);
+  };
+  for (int j0 = 0; j0 < H3; j0 += JB) {
+    block(x, c.W, c.b, DIN, mx, j0);
+    block(h, c.U, c.b + H3, H, mh, j0);
+  }
+  for (int r = 0; r < R; ++r) {
+    T* __restrict__ zx = mx[r];
+    T* __restrict__ zh = mh[r];
+    // z | r; the argument is clamped to +-80 so that no exp overflows (-ffast-math assumes finite
+    // values; sigmoid is saturated there: exp(-80) is below float32's resolution of 1)
+    for (int j = 0; j < 2 * H; ++j) zx[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), zx[j] + zh[j]))));
+    for (int j = 0; j < H; ++j) zh[j] = std::tanh(zx[2 * H + j] + zx[H + j] * zh[2 * H + j]);
+    for (int j = 0; j < H; ++j) out[r][j] = zx[j] * h[r][j] + (T(1) - zx[j]) * zh[j];
+  }
+}
+
 // one Keras GRU step for one row: out = GRU(x, h).  The loops are written so that the compiler
-// vectorises them (libmvec expf / tanhf under -ffast-math) and, for the compile-time widths of
-// the example models, keeps the 3H accumulators in registers across the k loop: this is the
-// timed CPU line.
+// vectorises them (libmvec expf / tanhf under -ffast-math); this is the timed CPU line.
 template <int DIN, int H, typename T>
-void gru_step_t(const Cell& c, const T* __restrict__ x, const T* __restrict__ h, T* __restrict__ out) {
-  constexpr int H3 = 3 * H;
-  T mx[H3], mh[H3];
-  for (int j = 0; j < H3; ++j) {
-    mx[j] = c.b[j];
-    mh[j] = c.b[H3 + j];
-  }
-  for (int k = 0; k < DIN; ++k) {
-    const T xv = x[k];
-    const float* __restrict__ w = c.W + k * H3;
-#pragma GCC unroll 16
-    for (int j = 0; j < H3; ++j) mx[j] += xv * w[j];
-  }
-  for (int k = 0; k < H; ++k) {
-    const T hv = h[k];
-    const float* __restrict__ u = c.U + k * H3;
-#pragma GCC unroll 16
-    for (int j = 0; j < H3; ++j) mh[j] += hv * u[j];
-  }
-  // z | r; the argument is clamped to +-80 so that no exp overflows (-ffast-math assumes finite
-  // values; sigmoid is saturated there: exp(-80) is below float32's resolution of 1)
-  for (int j = 0; j < 2 * H; ++j) mx[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), mx[j] + mh[j]))));
-  for (int j = 0; j < H; ++j) mh[j] = std::tanh(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);
-  for (int j = 0; j < H; ++j) out[j] = mx[j] * h[j] + (T(1) - mx[j]) * mh[j];
+void gru_step_t(const Cell& c, const T* x, const T* h, T* out) {
+  gru_rows_t<DIN, H, T, 1>(c, &x, &h, &out);
 }
 
 template <typename T>
@@ -127,6 +169,15 @@ inline void gru_step(const Cell& c, const T* x, const T* h, T* out, T* mx, T* mh
   gru_step_any<T>(c, x, h, out, mx, mh);
 }
 
+// four rows at once where a compile-time width exists (false: the caller steps them one by one)
+template <typename T>
+inline bool gru_rows4(const Cell& c, const T* const* x, const T* const* h, T* const* out) {
+  if (c.din == 32 && c.H == 32) return gru_rows_t<32, 32, T, 4>(c, x, h, out), true;
+  if (c.din == 64 && c.H == 64) return gru_rows_t<64, 64, T, 4>(c, x, h, out), true;
+  if (c.din == 16 && c.H == 16) return gru_rows_t<16, 16, T, 4>(c, x, h, out), true;
+  return false;
+}
+
 struct Graph {            // graph-local views of one graph of the batch
   std::vector<int64_t> n;                 // rows per entity
   std::vector<const float*> feat;         // per entity
@@ -158,73 +209,94 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
     for (int64_t r = 0; r < g.n[e]; ++r)
       for (int f = 0; f < F; ++f) S[e][r * H + f] = g.feat[e][r * F + f];
   }
+  // Per MP, the messages of each destination (CSR, message order within a destination) and the
+  // sequence lengths: they depend on the graph only, so they are built once, not per iteration
+  // (serial work that dominated one large graph's time under OpenMP).
+  struct Msg { int64_t pos; int s; int64_t row; };
+  struct Prep {
+    std::vector<int64_t> ptr, flen;
+    std::vector<Msg> msgs;
+  };
+  std::vector<Prep> preps(p->num_mps);
+  for (int mi = 0; mi < p->num_mps; ++mi) {
+    const ign_mp_desc& mp = p->mps[mi];
+    const int dst = mp.dst_entity, NS = mp.num_sources;
+    const int64_t ND = g.n[dst];
+    const bool sorted = mp.aggregation != IGN_AGGR_SUM;
+    const bool axis2 = mp.aggregation == IGN_AGGR_CONCAT && mp.concat_axis == 2;
+    std::vector<int64_t> lmax(NS, 0);
+    std::vector<int64_t>& flen = preps[mi].flen;
+    flen.assign(ND, 0);
+    int64_t total = 0;
+    std::vector<int64_t> ilflat;
+    for (int s = 0; s < NS; ++s) {
+      const int a = mp.sources[s].adjacency;
+      int64_t mx = -1;
+      for (int64_t k = 0; k < g.ne[a]; ++k) mx = std::max(mx, g.seq[a][k]);
+      if (mx < 0) { msg = "adjacency with no edges (reduce_max of an empty seq, GM:484)"; return IGN_ERR_INVALID; }
+      lmax[s] = mx + 1;
+      total += lmax[s];
+      if (mp.aggregation == IGN_AGGR_INTERLEAVE) {
+        const int il = mp.sources[s].interleave;
+        ilflat.insert(ilflat.end(), g.il[il], g.il[il] + g.nil[il]);
+      }
+    }
+    if (axis2) total = lmax[0];
+    // messages by destination (CSR, message order within a destination)
+    std::vector<int64_t>& ptr = preps[mi].ptr;
+    ptr.assign(ND + 1, 0);
+    for (int s = 0; s < NS; ++s) {
+      const int a = mp.sources[s].adjacency, se = mp.sources[s].entity;
+      for (int64_t k = 0; k < g.ne[a]; ++k) {
+        const int64_t si = g.src[a][k], di = g.dst[a][k];
+        if (si < 0 || si >= g.n[se] || di < 0 || di >= ND) { msg = "index out of range (gather, GM:432)"; return IGN_ERR_INVALID; }
+        ptr[di + 1]++;
+      }
+    }
+    for (int64_t r = 0; r < ND; ++r) ptr[r + 1] += ptr[r];
+    std::vector<Msg>& msgs = preps[mi].msgs;
+    msgs.resize(ptr[ND]);
+    std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
+    int64_t off = 0;
+    if (mp.aggregation == IGN_AGGR_INTERLEAVE && (int64_t)ilflat.size() != total) {
+      msg = "interleave indices do not cover the slots (AUX:435)";
+      return IGN_ERR_INVALID;
+    }
+    for (int s = 0; s < NS; ++s) {
+      const int a = mp.sources[s].adjacency;
+      for (int64_t k = 0; k < g.ne[a]; ++k) {
+        const int64_t si = g.src[a][k], di = g.dst[a][k];
+        int64_t pos = axis2 ? g.seq[a][k] : off + g.seq[a][k];
+        if (mp.aggregation == IGN_AGGR_INTERLEAVE) {
+          pos = ilflat[pos];
+          if (pos < 0 || pos >= total) { msg = "interleave index out of range (AUX:435)"; return IGN_ERR_INVALID; }
+        }
+        msgs[fill[di]++] = {pos, s, si};
+        if (!axis2 || s == 0) flen[di]++;
+      }
+      off += lmax[s];
+    }
+    if (sorted && ND) {
+      int64_t mxl = 0;
+      for (int64_t d = 0; d < ND; ++d) {
+        if (flen[d] == 0) { msg = "a destination receives no message (gather_nd -1, AUX:793-795)"; return IGN_ERR_INVALID; }
+        if (flen[d] > total) { msg = "final_len beyond the padded length (AUX:793-795)"; return IGN_ERR_INVALID; }
+        mxl = std::max(mxl, flen[d]);
+      }
+      if (mxl < total) { msg = "sequence_mask(final_len) narrower than the padded sequence (AUX:785-790)"; return IGN_ERR_INVALID; }
+    }
+  }
   for (int it = 0; it < p->num_iterations; ++it) {
     for (int mi = 0; mi < p->num_mps; ++mi) {
       const ign_mp_desc& mp = p->mps[mi];
       const Cell& c = m.cells[mp.cell];
-      const int dst = mp.dst_entity, H = c.H, NS = mp.num_sources;
+      const int dst = mp.dst_entity, H = c.H;
       const int64_t ND = g.n[dst];
       const bool sorted = mp.aggregation != IGN_AGGR_SUM;
       const bool axis2 = mp.aggregation == IGN_AGGR_CONCAT && mp.concat_axis == 2;
-      // per destination: (position, source slot, source row), in source then edge order
-      std::vector<int64_t> lmax(NS, 0), flen(ND, 0);
-      int64_t total = 0;
-      std::vector<int64_t> ilflat;
-      for (int s = 0; s < NS; ++s) {
-        const int a = mp.sources[s].adjacency;
-        int64_t mx = -1;
-        for (int64_t k = 0; k < g.ne[a]; ++k) mx = std::max(mx, g.seq[a][k]);
-        if (mx < 0) { msg = "adjacency with no edges (reduce_max of an empty seq, GM:484)"; return IGN_ERR_INVALID; }
-        lmax[s] = mx + 1;
-        total += lmax[s];
-        if (mp.aggregation == IGN_AGGR_INTERLEAVE) {
-          const int il = mp.sources[s].interleave;
-          ilflat.insert(ilflat.end(), g.il[il], g.il[il] + g.nil[il]);
-        }
-      }
-      if (axis2) total = lmax[0];
-      // messages by destination (CSR, message order within a destination)
-      struct Msg { int64_t pos; int s; int64_t row; };
-      std::vector<int64_t> ptr(ND + 1, 0);
-      for (int s = 0; s < NS; ++s) {
-        const int a = mp.sources[s].adjacency, se = mp.sources[s].entity;
-        for (int64_t k = 0; k < g.ne[a]; ++k) {
-          const int64_t si = g.src[a][k], di = g.dst[a][k];
-          if (si < 0 || si >= g.n[se] || di < 0 || di >= ND) { msg = "index out of range (gather, GM:432)"; return IGN_ERR_INVALID; }
-          ptr[di + 1]++;
-        }
-      }
-      for (int64_t r = 0; r < ND; ++r) ptr[r + 1] += ptr[r];
-      std::vector<Msg> msgs(ptr[ND]);
-      std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
-      int64_t off = 0;
-      if (mp.aggregation == IGN_AGGR_INTERLEAVE && (int64_t)ilflat.size() != total) {
-        msg = "interleave indices do not cover the slots (AUX:435)";
-        return IGN_ERR_INVALID;
-      }
-      for (int s = 0; s < NS; ++s) {
-        const int a = mp.sources[s].adjacency;
-        for (int64_t k = 0; k < g.ne[a]; ++k) {
-          const int64_t si = g.src[a][k], di = g.dst[a][k];
-          int64_t pos = axis2 ? g.seq[a][k] : off + g.seq[a][k];
-          if (mp.aggregation == IGN_AGGR_INTERLEAVE) {
-            pos = ilflat[pos];
-            if (pos < 0 || pos >= total) { msg = "interleave index out of range (AUX:435)"; return IGN_ERR_INVALID; }
-          }
-          msgs[fill[di]++] = {pos, s, si};
-          if (!axis2 || s == 0) flen[di]++;
-        }
-        off += lmax[s];
-      }
-      if (sorted && ND) {
-        int64_t mxl = 0;
-        for (int64_t d = 0; d < ND; ++d) {
-          if (flen[d] == 0) { msg = "a destination receives no message (gather_nd -1, AUX:793-795)"; return IGN_ERR_INVALID; }
-          if (flen[d] > total) { msg = "final_len beyond the padded length (AUX:793-795)"; return IGN_ERR_INVALID; }
-          mxl = std::max(mxl, flen[d]);
-        }
-        if (mxl < total) { msg = "sequence_mask(final_len) narrower than the padded sequence (AUX:785-790)"; return IGN_ERR_INVALID; }
-      }
+      const std::vector<int64_t>& ptr = preps[mi].ptr;
+      const std::vector<int64_t>& flen = preps[mi].flen;
+      const std::vector<Msg>& msgs = preps[mi].msgs;
       std::vector<T>& out_s = S2[dst];
       out_s.assign(ND * H, T(0));
       const int DIN = c.din;
@@ -261,16 +333,44 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
         }
         std::copy(h.begin(), h.end(), out_s.begin() + d * H);
       };
+      // sum MPs: four destinations per GRU call where a compile-time width exists (gru_rows4)
+      auto run4 = [&](int64_t d0, std::vector<T>& x4, std::vector<T>& h, std::vector<T>& hn,
+                      std::vector<T>& mx, std::vector<T>& mh) {
+        if (sorted || d0 + 4 > ND) {
+          for (int64_t d = d0; d < std::min(d0 + 4, ND); ++d) run(d, x4, h, hn, mx, mh);
+          return;
+        }
+        std::fill(x4.begin(), x4.end(), T(0));
+        const T* xs[4];
+        const T* hs[4];
+        T* os[4];
+        for (int r = 0; r < 4; ++r) {
+          const int64_t d = d0 + r;
+          T* x = x4.data() + (size_t)r * DIN;
+          for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
+            const Msg& q = msgs[i];
+            const int se = mp.sources[q.s].entity;
+            const T* v = S[se].data() + q.row * p->entities[se].hidden_dim;
+            for (int k = 0; k < DIN; ++k) x[k] += v[k];
+          }
+          xs[r] = x;
+          hs[r] = S[dst].data() + d * H;
+          os[r] = out_s.data() + d * H;
+        }
+        if (!gru_rows4(c, xs, hs, os))
+          for (int r = 0; r < 4; ++r) gru_step(c, xs[r], hs[r], os[r], mx.data(), mh.data());
+      };
+      const int64_t nblk = (ND + 3) / 4;
       if (par) {
 #pragma omp parallel
         {
-          std::vector<T> x(DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
-#pragma omp for schedule(dynamic, 64)
-          for (int64_t d = 0; d < ND; ++d) run(d, x, h, hn, mx, mh);
+          std::vector<T> x4(4 * DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
+#pragma omp for schedule(dynamic, 16)
+          for (int64_t b = 0; b < nblk; ++b) run4(4 * b, x4, h, hn, mx, mh);
         }
       } else {
-        std::vector<T> x(DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
-        for (int64_t d = 0; d < ND; ++d) run(d, x, h, hn, mx, mh);
+        std::vector<T> x4(4 * DIN), h(H), hn(H), mx(3 * H), mh(3 * H);
+        for (int64_t b = 0; b < nblk; ++b) run4(4 * b, x4, h, hn, mx, mh);
       }
       std::swap(S[dst], S2[dst]);   // GM:602: the destination's state is overwritten
     }
@@ -279,58 +379,71 @@ int graph_forward(const Model& m, const Graph& g, float* out, bool par, std::str
   const int64_t R = g.n[p->readout_inputs[0]];
   int width = 0;
   for (int i = 0; i < p->num_readout_inputs; ++i) width += p->entities[p->readout_inputs[i]].hidden_dim;
-  // one row of the readout; rows are independent, so one large graph splits them over the
-  // threads in static chunks (the serial loop was most of the 25k-node graph's CPU time)
-  auto readout_row = [&](int64_t r, std::vector<T>& a, std::vector<T>& b2) {
-    int col = 0;
-    for (int i = 0; i < p->num_readout_inputs; ++i) {
-      const int e = p->readout_inputs[i], H = p->entities[e].hidden_dim;
-      std::copy(S[e].begin() + r * H, S[e].begin() + (r + 1) * H, a.begin() + col);
-      col += H;
+  // RB rows of the readout at a time (rows are independent; a block reuses each weight row it
+  // loads RB times, where one row at a time streamed the 256x256 layer from L2 per row); one large
+  // graph splits the blocks over the threads in static chunks
+  constexpr int RB = 3, CB = 32;   // 12 AVX2 accumulators (float)
+  int maxw = width;
+  for (const auto& L : m.dense) maxw = std::max(maxw, L.out);
+  auto readout_rows = [&](int64_t r0, std::vector<T>& a, std::vector<T>& b2) {
+    const int nr = (int)std::min<int64_t>(RB, R - r0);
+    a.assign((size_t)RB * maxw, T(0));
+    b2.assign((size_t)RB * maxw, T(0));
+    for (int i = 0; i < nr; ++i) {
+      int col = 0;
+      for (int q = 0; q < p->num_readout_inputs; ++q) {
+        const int e = p->readout_inputs[q], H = p->entities[e].hidden_dim;
+        std::copy(S[e].begin() + (r0 + i) * H, S[e].begin() + (r0 + i + 1) * H, a.begin() + (size_t)i * maxw + col);
+        col += H;
+      }
     }
-    std::vector<T>& cur = a;
+    T* cur = a.data();
+    T* nxt = b2.data();
+    int width_out = width;
     for (const auto& L : m.dense) {
-      b2.assign(L.out, T(0));
-      for (int j0 = 0; j0 < L.out; j0 += 64) {   // 64 output columns at a time (register-resident)
-        const int nj = std::min(64, L.out - j0);
-        T acc[64];
-        for (int j = 0; j < 64; ++j) acc[j] = j < nj && L.b ? T(L.b[j0 + j]) : T(0);
-        if (nj == 64) {
+      for (int j0 = 0; j0 < L.out; j0 += CB) {   // CB output columns of RB rows (register-resident)
+        const int nj = std::min(CB, L.out - j0);
+        T acc[RB][CB];
+        for (int i = 0; i < RB; ++i)
+          for (int j = 0; j < CB; ++j) acc[i][j] = j < nj && L.b ? T(L.b[j0 + j]) : T(0);
+        if (nj == CB) {
           for (int k = 0; k < L.in; ++k) {
-            const T v = cur[k];
             const float* __restrict__ w = L.W + (int64_t)k * L.out + j0;
-
-            for (int j = 0; j < 64; ++j) acc[j] += v * w[j];
+            for (int i = 0; i < RB; ++i) {
+              const T v = cur[(size_t)i * maxw + k];
+              for (int j = 0; j < CB; ++j) acc[i][j] += v * w[j];
+            }
           }
         } else {
           for (int k = 0; k < L.in; ++k) {
-            const T v = cur[k];
             const float* w = L.W + (int64_t)k * L.out + j0;
-            for (int j = 0; j < nj; ++j) acc[j] += v * w[j];
+            for (int i = 0; i < RB; ++i) {
+              const T v = cur[(size_t)i * maxw + k];
+              for (int j = 0; j < nj; ++j) acc[i][j] += v * w[j];
+            }
           }
         }
-        for (int j = 0; j < nj; ++j) b2[j0 + j] = act(acc[j], L.act);
+        for (int i = 0; i < RB; ++i)
+          for (int j = 0; j < nj; ++j) nxt[(size_t)i * maxw + j0 + j] = acc[i][j];
       }
-      cur.swap(b2);
+      for (int i = 0; i < RB; ++i) act_row(nxt + (size_t)i * maxw, L.out, L.act);
+      std::swap(cur, nxt);
+      width_out = L.out;
     }
-    for (size_t j = 0; j < cur.size(); ++j) out[r * (int64_t)cur.size() + j] = (float)cur[j];
+    for (int i = 0; i < nr; ++i)
+      for (int j = 0; j < width_out; ++j) out[(r0 + i) * (int64_t)width_out + j] = (float)cur[(size_t)i * maxw + j];
   };
+  const int64_t nblk = (R + RB - 1) / RB;
   if (par) {
 #pragma omp parallel
     {
-      std::vector<T> a(width), b2;
+      std::vector<T> a, b2;
 #pragma omp for schedule(static)
-      for (int64_t r = 0; r < R; ++r) {
-        a.resize(width);
-        readout_row(r, a, b2);
-      }
+      for (int64_t bI = 0; bI < nblk; ++bI) readout_rows(bI * RB, a, b2);
     }
   } else {
-    std::vector<T> a(width), b2;
-    for (int64_t r = 0; r < R; ++r) {
-      a.resize(width);
-      readout_row(r, a, b2);
-    }
+    std::vector<T> a, b2;
+    for (int64_t bI = 0; bI < nblk; ++bI) readout_rows(bI * RB, a, b2);
   }
   return IGN_OK;
 }
