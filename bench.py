@@ -56,6 +56,9 @@ def parse():
                          "next batches built on a worker thread")
     ap.add_argument("--no-prefetch", action="store_true", help="with --fresh-batches: build each batch inline")
     ap.add_argument("--input-workers", type=int, default=8, help="with --fresh-batches: batch-building threads")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="forward: the rank's graphs as this many sub-batches, one engine / HIP stream each, "
+                         "launched back to back in every step (their kernels co-run)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -236,13 +239,34 @@ def main():
     import numpy as np
 
     from ignnition_amd import workloads
-    from ignnition_amd.engine import Batch, Engine, MPPlan
+    from ignnition_amd.engine import Batch, Engine, MPPlan, SplitBatch
 
-    def barrier_sync(eng):
-        eng.synchronize()
+    engines = []   # every engine of the step (--streams: one per sub-batch)
+    subs = []      # --streams: the sub-batches
+
+    def barrier_sync(_eng=None):
+        for e in engines:
+            e.synchronize()
         if dist is not None:
             dist.barrier()
-            eng.synchronize()
+            for e in engines:
+                e.synchronize()
+
+    def set_timing(on, kinds=None):
+        for e in engines:
+            e.set_timing(on, kinds=kinds)
+
+    def stats_all():   # per kind, summed over the engines
+        tot = None
+        for e in engines:
+            st = e.stats()
+            if tot is None:
+                tot = st
+            else:
+                for kind, v in st.items():
+                    for f, x in v.items():
+                        tot[kind][f] += x
+        return tot
 
     synthetic = args.model == "synthetic"
     cleanup = []
@@ -273,6 +297,7 @@ def main():
             cpu_cxx = cpu_baseline_cxx(plan, mi, prm, graphs, args.cpu_seconds)
     eng = Engine(plan, device if world > 1 else 0)
     eng.set_params(prm)
+    engines.append(eng)
     t_build = time.perf_counter()
     halo_rows = 0
     if synthetic and world > 1:
@@ -322,6 +347,7 @@ def main():
         gm.set_model_info(mi)
         trainer = Trainer(mi, params=prm, device=device if world > 1 else 0, dist=dist)
         eng = trainer.engine
+        engines[:] = [eng]
         probe = Batch(eng, graphs)
         edges, gru_steps = probe.edges_per_forward, probe.gru_steps_per_forward
         probe.close()
@@ -336,6 +362,16 @@ def main():
             trainer.train_prepared(*next(batches))
         if not args.no_prefetch:
             cleanup.append(batches.close)
+    elif args.streams > 1 and not args.train and len(graphs) > 1:
+        # the rank's batch as K sub-batches of consecutive graphs on K plans / HIP streams
+        # (engine.SplitBatch): the memory-bound sum update of one co-runs with the issue-bound
+        # ordered update of another.  The same graphs and work per step as one batch.
+        sb = SplitBatch(eng, graphs, args.streams)
+        engines[:] = sb.engines
+        subs += sb.parts
+        step = lambda: sb.forward(to_host=False)
+        edges = sb.edges_per_forward
+        gru_steps = sb.gru_steps_per_forward
     else:
         batch = Batch(eng, graphs)
         step = lambda: batch.forward(to_host=False)
@@ -365,19 +401,30 @@ def main():
     # Warm-up with every launch timed (per-kind breakdown, picks the dominant kernel); the timed
     # region then records HIP event pairs around the dominant kernel's launches only, since each
     # pair adds a few microseconds of queue time (all ~35 launches per step: ~5 %).
-    eng.set_timing(not args.no_timing)
+    set_timing(not args.no_timing)
     for _ in range(max(args.warmup, 1)):
         step()
-    barrier_sync(eng)
-    warm = eng.stats()
+    barrier_sync()
+    warm = stats_all()
     dom = max(("seq_gru", "sum_gru", "readout"), key=lambda k: warm[k]["ms"])
-    eng.set_timing(not args.no_timing, kinds=[dom])
+    set_timing(not args.no_timing, kinds=[dom])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    barrier_sync(eng)
+    barrier_sync()
     dt = time.perf_counter() - t0
-    stats = eng.stats()
+    stats = stats_all()
+    isolated = None
+    if len(subs) > 1 and not args.no_timing and not args.train:
+        # isolated leg, after the timed region: sub-batch 0 alone on the chip, its dominant kernel's
+        # launches timed (in the timed region the sub-batches' kernels co-run, so there a launch's
+        # duration is its share of a chip it does not have to itself)
+        set_timing(False)
+        engines[0].set_timing(True, kinds=[dom])
+        for _ in range(3):
+            subs[0].forward(to_host=False)
+        engines[0].synchronize()
+        isolated = engines[0].stats()[dom]
     for fn in cleanup:
         fn()
     dev = None
@@ -425,6 +472,7 @@ def main():
                 "hbm_frac_alg": round(bytes_launch / avg_s / 1e9 / PEAK_HBM_GBS, 4),
                 "mfma_frac_alg": round(flops_launch / avg_s / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
                 "timed_launches": s["launches"],
+                "streams": len(engines),
                 # the matrix pipe the kernel actually runs on: FLOPs its MFMAs execute (bf16 piece
                 # products on the split-bf16 kernels) per launch time, against that pipe's dense peak
                 "mfma_pipe": pipe(s),
@@ -448,6 +496,16 @@ def main():
                    "sum_update": (H16 % 3 if plan.hidden[0] == 64 and sum_v == 8 else BF % 6)
                    if plan.hidden[0] in (32, 64) and sum_v in (7, 8) else "f32 MFMA",
                    "projection": "f32 MFMA"}
+    if roof is not None and isolated and isolated["launches"]:
+        il = isolated["launches"]
+        iavg = isolated["ms"] / il / 1e3
+        iach = (isolated["bytes"] / il / iavg / 1e9) if roof["unit"] == "GB/s" else (isolated["flops"] / il / iavg / 1e12)
+        roof["isolated"] = {"what": "sub-batch 0 (%d graphs) alone on the chip, after the timed region"
+                                    % subs[0].num_graphs,
+                            "launches": il, "avg_launch_ms": round(iavg * 1e3, 4),
+                            "alg_flops_per_launch": isolated["flops"] / il, "alg_bytes_per_launch": isolated["bytes"] / il,
+                            "achieved": round(iach, 3), "frac": round(iach / roof["peak"], 4),
+                            "mfma_pipe": pipe(isolated)}
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,
                                                                                               "sum_update")]
@@ -466,7 +524,7 @@ def main():
                    "parallelism": ("edge-cut over %d ranks, RCCL halo all-to-all per iteration (rank 0 halo rows: %d)"
                                    % (world, halo_rows)) if synthetic else
                                   "graph-sharded (%d ranks), no collective in the forward" % world,
-                   "batch_build_s": round(t_build, 3), "contraction": contraction,
+                   "batch_build_s": round(t_build, 3), "contraction": contraction, "streams": len(engines),
                    "samples_per_s": round(args.graphs * world * args.steps / dt, 1)},
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -101,9 +101,9 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get", "ign_dataset_batch_create",
            "ign_dataset_batch_get", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json", "ign_forward_train_begin", "ign_forward_train_mp",
            "ign_forward_train_end", "ign_backward_begin", "ign_backward_mp", "ign_backward_end",
-           "ign_batch_train_buffers"]
+           "ign_batch_train_buffers", "ign_batch_read_predictions"]
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -174,6 +174,7 @@ def _load():
         "ign_backward_mp": (C.c_int, [VP, VP]),
         "ign_backward_end": (C.c_int, [VP, VP]),
         "ign_batch_train_buffers": (C.c_int, [VP, i32, P(VP), P(VP)]),
+        "ign_batch_read_predictions": (C.c_int, [VP, VP, VP]),
     }
     ab = "IGN_LIB_PATH" in os.environ   # an A/B build of an older tree may lack newer entry points
     for name, (res, args) in sig.items():

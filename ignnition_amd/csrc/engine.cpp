@@ -1556,6 +1556,13 @@ int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
   return copy_out(p, b, pred_out);
 }
 
+int ign_batch_read_predictions(ign_plan* p, ign_batch* b, float* host_out) {
+  int rc = check_pb(p, b);
+  if (rc) return rc;
+  if (!host_out) return fail(IGN_ERR_INVALID, "null argument");
+  return copy_out(p, b, host_out);
+}
+
 int ign_batch_mp_split(const ign_batch* b, int32_t mi, int64_t* interior, int64_t* boundary) {
   if (!b || !interior || !boundary) return fail(IGN_ERR_INVALID, "null argument");
   if (mi < 0 || mi >= (int)b->mp.size()) return fail(IGN_ERR_INVALID, "mp index %d out of range", mi);

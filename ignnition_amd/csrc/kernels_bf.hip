@@ -1795,7 +1795,13 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
 
 template <int DIN, int ACT>
 static void readout_h16_launch(const Readout3Args& args, const h8* w, hipStream_t st) {
-  constexpr int WAVES = 8, RT = 2;
+// 4 waves per block (1 per SIMD): two blocks per CU (VGPR-bound: 212 each) that do not share
+// barriers, so one block's layer-1 / selu phase runs beside the other's layer-2 MFMAs
+// (0.64 -> 0.59-0.61 ms per launch against 8 waves, same box)
+#ifndef IGN_READOUT_WAVES
+#define IGN_READOUT_WAVES 4
+#endif
+  constexpr int WAVES = IGN_READOUT_WAVES, RT = 2;
   auto k = readout_h16_kernel<DIN, ACT, WAVES, RT>;
   const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
   hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w);

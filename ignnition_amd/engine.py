@@ -369,6 +369,8 @@ class Engine:
         h = C.c_void_p()
         check(lib.ign_plan_create(C.byref(desc), device, C.byref(h)))
         self.handle = h
+        self.params_version = 0   # bumped by every parameter update (SplitBatch re-syncs its replicas)
+        self._replicas = []
         _LIVE_ENGINES.add(self)
         n = C.c_int64()
         check(lib.ign_plan_num_params(h, C.byref(n)))
@@ -402,6 +404,7 @@ class Engine:
             v = np.ascontiguousarray(v).reshape(-1)
             flat[off:off + v.size] = v
         check(lib.ign_plan_set_params(self.handle, flat.ctypes.data_as(C.c_void_p), 0))
+        self.params_version += 1
 
     def set_timing(self, on: bool, kinds=None):
         """Per-launch HIP event timing (resets the statistics); ``kinds``: kernel kind names to
@@ -450,6 +453,22 @@ class Engine:
 
     def adam_step(self, grads, m, v, iteration: int, lr: float, beta1=0.9, beta2=0.999, epsilon=1e-7):
         check(lib.ign_adam_step(self.handle, _ptr(grads), _ptr(m), _ptr(v), int(iteration), lr, beta1, beta2, epsilon))
+        self.params_version += 1
+
+    def replicas(self, n: int) -> list:
+        """``n`` more plans of this model on this device (each its own HIP stream), created once and
+        kept; their parameters follow this engine's (SplitBatch re-syncs them when they changed)."""
+        while len(self._replicas) < n:
+            r = Engine(self.plan, self.device)
+            r._synced = -1
+            self._replicas.append(r)
+        for r in self._replicas[:n]:
+            if r._synced != self.params_version:
+                flat = np.empty(self.n_params, np.float32)
+                check(lib.ign_plan_get_params(self.handle, flat.ctypes.data_as(C.c_void_p)))
+                check(lib.ign_plan_set_params(r.handle, flat.ctypes.data_as(C.c_void_p), 0))
+                r._synced = self.params_version
+        return self._replicas[:n]
 
     def gather_rows(self, src, idx, dst):
         """dst[i] = src[idx[i]] (device tensors: src [R, C] fp32, idx [n] int32, dst [n, C])."""
@@ -459,6 +478,9 @@ class Engine:
                                   n, cols, C.c_void_p(dst.data_ptr())))
 
     def close(self):
+        for r in getattr(self, "_replicas", []):
+            r.close()
+        self._replicas = []
         h = getattr(self, "handle", None)
         if h:
             lib.ign_plan_destroy(h)
@@ -704,6 +726,54 @@ class Batch:
         if h:
             lib.ign_batch_destroy(h)
             self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class SplitBatch:
+    """The graphs as ``parts`` sub-batches of consecutive graphs, sub-batch i on the engine's
+    replica i (its own plan and HIP stream; replica 0 is the engine itself).  ``forward`` enqueues
+    every sub-batch before waiting, so the kernels of different sub-batches co-run: the
+    memory-bound sum update of one beside the issue-bound ordered update of another (DESIGN §3b'').
+    The predictions are the batch's, in graph order, bitwise those of one ``Batch`` (graphs are
+    independent: GM:712-724)."""
+
+    def __init__(self, engine: Engine, graphs, parts: int = 2):
+        graphs = list(graphs)
+        parts = max(1, min(int(parts), len(graphs)))
+        self.engine = engine
+        self.engines = [engine] + engine.replicas(parts - 1)
+        cuts = [len(graphs) * i // parts for i in range(parts + 1)]
+        self.parts = [Batch(e, graphs[cuts[i]:cuts[i + 1]]) for i, e in enumerate(self.engines)]
+        self.num_graphs = sum(b.num_graphs for b in self.parts)
+        self.predictions = sum(b.predictions for b in self.parts)
+        self.output_units = self.parts[0].output_units
+        self.edges_per_forward = sum(b.edges_per_forward for b in self.parts)
+        self.gru_steps_per_forward = sum(b.gru_steps_per_forward for b in self.parts)
+        self.graph_predictions = np.concatenate([b.graph_predictions for b in self.parts])
+
+    def forward(self, to_host: bool = True):
+        self.engine.replicas(len(self.parts) - 1)   # re-sync replica parameters if they changed
+        for b in self.parts:
+            b.forward(to_host=False)
+        if not to_host:
+            return None
+        out = np.empty((self.predictions, self.output_units), np.float32)
+        row = 0
+        for b in self.parts:
+            check(lib.ign_batch_read_predictions(b.engine.handle, b.handle,
+                                                 out[row:row + b.predictions].ctypes.data_as(C.c_void_p)))
+            row += b.predictions
+        return out
+
+    def synchronize(self):
+        for e in self.engines:
+            e.synchronize()
+
+    def close(self):
+        for b in self.parts:
+            b.close()
 
     def __del__(self):
         self.close()

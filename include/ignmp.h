@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 9
+#define IGN_ABI_VERSION 10
 
 enum ign_status {
   IGN_OK = 0,
@@ -259,6 +259,10 @@ int  ign_forward(ign_plan* plan, ign_batch* batch, float* pred_out);
 int  ign_synchronize(ign_plan* plan);
 /* Device pointer of the batch's prediction buffer (valid until ign_batch_destroy). */
 int  ign_batch_predictions(ign_batch* batch, const float** dev_ptr);
+/* Copy the batch's predictions [n_pred][units] to host after the forwards enqueued on the plan's
+ * stream (waits for that stream only): the host side of a forward launched with pred_out NULL,
+ * e.g. one of several sub-batches on several plans launched before any wait (ABI 10). */
+int  ign_batch_read_predictions(ign_plan* plan, ign_batch* batch, float* host_out);
 /* Copy the current hidden state of an entity (after ign_forward) to host [rows][H]. */
 int  ign_batch_state(ign_plan* plan, ign_batch* batch, int32_t entity, float* host_out);
 int  ign_stats(const ign_plan* plan, ign_stats_t* out);
