@@ -40,6 +40,10 @@ def test_split_batch_equals_one_batch(kind, topo, n, parts):
     sb.forward(to_host=False)
     assert np.array_equal(sb.forward(), whole)
     assert sb.edges_per_forward == Batch(eng, graphs).edges_per_forward
+    # timed forwards launch directly (no graph replay): same bits
+    eng.set_timing(True)
+    assert np.array_equal(sb.forward(), whole)
+    eng.set_timing(False)
 
 
 def test_split_batch_replicas_follow_parameter_updates():
