@@ -77,12 +77,15 @@ template <typename T> inline T SIGX(T x) {
 def build(tmp):
     src = open(os.path.join(REPO, "oracle", "cpu_forward.cpp")).read()
     src = src.replace('#include "../include/ignmp.h"', '#include "%s"' % os.path.join(REPO, "include", "ignmp.h"))
-    sig = ("for (int j = 0; j < 2 * H; ++j) mx[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), "
-           "mx[j] + mh[j]))));")
-    tnh = "for (int j = 0; j < H; ++j) mh[j] = std::tanh(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);"
-    assert src.count(sig) == 2 and src.count(tnh) == 2, "oracle/cpu_forward.cpp gate lines changed"
-    src = src.replace(sig, "for (int j = 0; j < 2 * H; ++j) mx[j] = SIGX(mx[j] + mh[j]);")
-    src = src.replace(tnh, "for (int j = 0; j < H; ++j) mh[j] = TANHX(mx[2 * H + j] + mx[H + j] * mh[2 * H + j]);")
+    # the gate lines of gru_rows_t (zx / zh) and gru_step_any (mx / mh)
+    for a, b in (("zx", "zh"), ("mx", "mh")):
+        sig = ("for (int j = 0; j < 2 * H; ++j) %s[j] = T(1) / (T(1) + std::exp(-std::min(T(80), std::max(T(-80), "
+               "%s[j] + %s[j]))));" % (a, a, b))
+        tnh = "for (int j = 0; j < H; ++j) %s[j] = std::tanh(%s[2 * H + j] + %s[H + j] * %s[2 * H + j]);" % (b, a, a, b)
+        assert src.count(sig) == 1 and src.count(tnh) == 1, "oracle/cpu_forward.cpp gate lines changed"
+        src = src.replace(sig, "for (int j = 0; j < 2 * H; ++j) %s[j] = SIGX(%s[j] + %s[j]);" % (a, a, b))
+        src = src.replace(tnh, "for (int j = 0; j < H; ++j) %s[j] = TANHX(%s[2 * H + j] + %s[H + j] * %s[2 * H + j]);"
+                          % (b, a, a, b))
     src = src.replace("namespace {", PRELUDE, 1)
     path = os.path.join(tmp, "cpu_forward_emu.cpp")
     open(path, "w").write(src)
