@@ -35,6 +35,7 @@ struct MPTrain {
   int32_t* amdst = nullptr;   // attention MPs: destination row of every CSR message
   std::vector<int32_t*> asptr, asidx;   // attention MPs, per slot: source row -> CSR messages
   int64_t hs_rows = 0;
+  int32_t* hdrb = nullptr;    // sorted MPs: the ordered backward's tile headers (launch_seq_bwd_hdr)
   std::vector<int32_t*> tptr, tidx;   // per source slot: source row -> steps (sorted) / dst rows (sum)
   hvec<int64_t> trows;         // (a source with a message network: its rows are the edges)
   // message networks, per source slot: state row -> its edges (ascending), for the hs_source /
@@ -287,6 +288,15 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         float* f = nullptr;
         if ((rc = talloc(t.get(), &f, mt.hs_rows * H))) return rc;
         mt.hs.push_back(f);
+      }
+      {
+        const int64_t n_pos = (mb.n_dst + 15) / 16 * 16;
+        float* f = nullptr;
+        if ((rc = talloc(t.get(), &f, 4 * n_pos))) return rc;
+        mt.hdrb = reinterpret_cast<int32_t*>(f);
+        // on the upload stream, behind the block's IGN_POOL_POISON fill (pool_alloc) and before the
+        // synchronisation at the end of this call: a launch on the plan stream could land first
+        HIP_TRY(launch_seq_bwd_hdr(mb.d_seq_hdr, mb.d_step_code, n_pos, mt.hdrb, upload_stream()));
       }
       // source row -> steps whose input contains it (directly or through a pre-summed row)
       build_csrs(S, tkeys, [&](auto&& emit) {
@@ -793,6 +803,7 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
       SeqBwdArgs a{mt.hs[rec.it], mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
                    t->ga, t->gu, mb.n_dst};
+      a.hdr = mt.hdrb;
       if (p->bwd_fuse && seq_bwd_fused_supported(H)) {
         // dU and both bias gradients (column sums of da and du) inside the kernel
         a.gu = nullptr;

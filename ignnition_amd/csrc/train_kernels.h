@@ -32,6 +32,8 @@ struct SeqBwdArgs {
   const void* Ubf = nullptr; // fused, H = 32: U's split-bf16 pieces (pack_u_bf16) -> gate recompute as seq_gru_bf x6
   const void* Uh = nullptr;  // fused, H = 32: U's scaled fp16 pieces (pack_u_f16) -> gate recompute as seq_gru_h16 x3
   const void* Uth = nullptr; // with Uh: U's scaled fp16 pieces as dh = du . U^T's A operand (pack_ut_f16)
+  const int32_t* hdr = nullptr;   // per order position, padded to whole tiles: {row, len, step_ptr,
+                                  // the code of the last step} (launch_seq_bwd_hdr)
 };
 
 // Backward of the sum update (AUX:752-765): one GRU step per destination row.
@@ -54,6 +56,10 @@ struct SumBwdArgs {
 hipError_t launch_pack_a(const float* M, int rows, int cols, float* out, hipStream_t st);
 bool bwd_shape_supported(int din, int h);
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st);
+// the ordered backward's tile headers from the forward's (SeqGruArgs::hdr: {row, len, step_ptr,
+// first code}): the same with the code of each position's last step; n_pos padded to whole tiles
+hipError_t launch_seq_bwd_hdr(const int32_t* fwd_hdr, const uint32_t* step_code, int64_t n_pos, int32_t* out,
+                              hipStream_t st);
 bool seq_bwd_fused_supported(int h);
 int64_t seq_bwd_partial_floats(int h);
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);

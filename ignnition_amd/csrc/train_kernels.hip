@@ -134,36 +134,69 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
   // transpose-tile offsets: write (unit 16t + 4g + q, row j); read (unit 16x + j, rows 4g .. 4g+3)
   const int wofs = j ^ (4 * g), rofs = j * 16 + 4 * (g ^ ((j >> 2) & 3));
   const int64_t n_tiles = (a.n_dst + 15) / 16;
+  f4 bh0[NT];   // the candidate's recurrent bias (the accumulator seed; H16: times the tile's SS)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bh0[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+  const int64_t tile_stride = FUSE ? (int64_t)gridDim.x * 4 : n_tiles;
+  // hdr (seq_bwd_hdr_kernel, padded to whole tiles): per position {row, len, step_ptr, the code of
+  // its last step}.  The wave loads its next tile's headers while the current tile runs, so a tile
+  // starts by issuing its dh rows, first states and last step's rows together (one round trip).
+  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  i4v hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile, n_tiles - 1) * 16 + j));
   // FUSE: persistent waves (static tile order: deterministic partials); otherwise one tile per wave
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += FUSE ? (int64_t)gridDim.x * 4 : n_tiles) {
+  for (; tile < n_tiles; tile += tile_stride) {
     const int64_t pos = tile * 16 + j;
     const bool valid = pos < a.n_dst;
-    const int row = valid ? a.order[pos] : 0;
-    const int L = valid ? a.len[pos] : 0;
-    const int64_t sp = valid ? a.step_ptr[pos] : 0;
+    const int row = hd[0];
+    const int L = hd[1];
+    const int64_t sp = valid ? hd[2] : 0;
+    const uint32_t code_last = (uint32_t)hd[3];
     const int64_t hbase = valid ? sp + pos : 0;
     f4 dh[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) dh[t] = valid ? ld4(a.dh_in + (int64_t)row * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-    int Lmax = L;
+    f4 h0[NT];   // H16: the tile's first states, for the forward's tile scale
+    if constexpr (H16) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+      for (int t = 0; t < NT; ++t) h0[t] = ld4(a.hs + hbase * H + 16 * t + 4 * g);
+    }
+    // positions are sorted by length, descending: lane 0 (position tile * 16) is the longest
+    const int Lmax = __builtin_amdgcn_readfirstlane(L);
+    // A step's state row and projected rows are loaded during the step before it (in the reverse
+    // order), before that step's stores: gfx9's vmcnt counts stores too, in issue order, so a load
+    // issued after a store would be waited for with it.  A lane past its sequence reads step 0 (the
+    // first loaded step, Lmax - 1: its own last step; masked either way).  Step codes are loaded
+    // two steps ahead, so a step's row loads never wait for its code.
+    f4 hp[NT], x[3][NT];
+    auto load_rows = [&](int64_t hr, uint32_t code) __attribute__((always_inline)) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
+#pragma unroll
+      for (int G = 0; G < 3; ++G)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
+    };
+    auto code_of = [&](int st) { return a.step_code[sp + (st < L ? st : 0)]; };
+    load_rows(hbase + (L > 0 ? L - 1 : 0), code_last);
+    uint32_t code_n1 = Lmax >= 2 ? code_of(Lmax - 2) : 0u;   // the code of step `step - 1`
+    hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile + tile_stride, n_tiles - 1) * 16 + j));
     f4 bh[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) bh[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+    for (int t = 0; t < NT; ++t) bh[t] = bh0[t];
     // H16: the forward's tile scale, from the tile's first states (saved as read): S = 2^(15 - E),
-    // m = max(1, max |h_0|) = f 2^E; SS = S sigma, cS = 1 / SS
+    // m = max(1, max |h_0|) = f 2^E; SS = S sigma, cS = 1 / SS.  After the first iteration every
+    // |h| <= 1, so a ballot settles m and the cross-lane reduction runs only for a larger state
     float S = 1.f, SS = 1.f, cS = 1.f;
     if constexpr (H16) {
       float m = 1.0f;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const f4 v = ld4(a.hs + hbase * H + 16 * t + 4 * g);
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) m = fmaxf(m, valid ? fabsf(v[r]) : 0.f);
+        for (int r = 0; r < 4; ++r) m = fmaxf(m, valid ? fabsf(h0[t][r]) : 0.f);
+      if (__ballot(m > 1.0f) != 0) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
       }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
       const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(m)) >> 23) - 126;
       const int eS = 15 - E;
       S = __int_as_float((127 + eS) << 23);
@@ -173,27 +206,13 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
       for (int t = 0; t < NT; ++t) bh[t] *= SS;   // the candidate accumulator's seed, as sbn
     }
 
-    // A step's state row and projected rows are loaded during the step before it (in the reverse
-    // order), before that step's stores: gfx9's vmcnt counts stores too, in issue order, so a load
-    // issued after a store would be waited for with it.  A lane past its sequence reads step 0.
-    f4 hp[NT], x[3][NT];
-    auto load_step = [&](int st, uint32_t code) __attribute__((always_inline)) {
-      const int64_t hr = hbase + (st < L ? st : 0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
-#pragma unroll
-      for (int G = 0; G < 3; ++G)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) x[G][t] = ld4(a.table + (int64_t)code * (3 * H) + G * H + 16 * t + 4 * g);
-    };
-    auto code_of = [&](int st) { return a.step_code[sp + (st < L ? st : 0)]; };
-    load_step(Lmax - 1, code_of(Lmax - 1));
     for (int step = Lmax - 1; step >= 0; --step) {
       const bool act = step < L;
       const int64_t tt = act ? step : 0;
       const int64_t i = sp + tt;
       const int64_t hr = hbase + tt;
-      const uint32_t code_next = step > 0 ? code_of(step - 1) : 0u;
+      const uint32_t code_next = code_n1;
+      if (step >= 2) code_n1 = code_of(step - 2);
       // opaque lane offset: keeps the loop-invariant fragment reads inside the step loop (registers)
       int lofs = lane;
       asm volatile("" : "+v"(lofs));
@@ -322,7 +341,7 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
 #pragma unroll
         for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
       }
-      if (step > 0) load_step(step - 1, code_next);
+      if (step > 0) load_rows(hbase + (step - 1 < L ? step - 1 : 0), code_next);
       if (act) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -482,6 +501,15 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         st4(Pu + 2 * H + u, bsum[t]);
       }
     }
+  }
+}
+
+__global__ void seq_bwd_hdr_kernel(const int32_t* __restrict__ hdr, const uint32_t* __restrict__ step_code,
+                                   int64_t n, int32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    i4v h = *reinterpret_cast<const i4v*>(hdr + 4 * i);
+    h[3] = (int32_t)step_code[(int64_t)h[2] + max(h[1], 1) - 1];   // padding: len 0, step_ptr = the pad slot
+    *reinterpret_cast<i4v*>(out + 4 * i) = h;
   }
 }
 
@@ -1115,6 +1143,14 @@ static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
     return e;
   if ((e = launch_axpy(a.dU, a.scratch, 1.f, (int64_t)H * 3 * H, st)) != hipSuccess) return e;
   return launch_axpy(a.db_in, a.scratch + (int64_t)H * 3 * H, 1.f, 3 * H, st);
+}
+
+hipError_t launch_seq_bwd_hdr(const int32_t* fwd_hdr, const uint32_t* step_code, int64_t n_pos, int32_t* out,
+                              hipStream_t st) {
+  if (n_pos <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n_pos + 255) / 256, 4096);
+  hipLaunchKernelGGL(seq_bwd_hdr_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fwd_hdr, step_code, n_pos, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
