@@ -482,13 +482,15 @@ def main():
                                        "mfma_pipe": pipe(v)}
                                    for k, v in warm.items() if v["launches"]}}
     seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "6"))
+    seq_v = seq_v if seq_v in (2, 4) else 6          # the engine's mapping (engine.cpp)
     ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "4"))
+    ro_v = ro_v if ro_v in (1, 2) else 4
     sum_v = int(os.environ.get("IGN_SUM_VARIANT", "8"))
     BF = "split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
     H16 = ("split-fp16: power-of-two-scaled 2-piece fp16 operands (RNE, 2^-22 relative), %d products, "
            "fp32 accumulate")
-    seq_c = {2: "f32 MFMA", 4: BF % 6, 5: BF % 9, 6: H16 % 3, 7: H16 % 4}
-    ro_c = {1: "f32 MFMA", 2: BF % 6, 3: BF % 9, 4: "both layers " + H16 % 3}
+    seq_c = {2: "f32 MFMA", 4: BF % 6, 6: H16 % 3}
+    ro_c = {1: "f32 MFMA", 2: BF % 6, 4: "both layers " + H16 % 3}
     contraction = {"ordered_update_hU": seq_c.get(seq_v, "f32 MFMA") if plan.hidden[0] in (32, 64) else "f32 MFMA",
                    "readout": ro_c.get(ro_v, BF % 6),
                    # sum variants 8 (default) / 7: split-fp16 / split-bf16 x.W and h.U at DIN = H = 64,

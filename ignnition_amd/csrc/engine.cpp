@@ -211,7 +211,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   std::unique_ptr<ign_plan> p(new ign_plan());
   p->device = device;
   if (const char* v = getenv("IGN_FUSE_PROJ")) p->fuse_proj = atoi(v) != 0;
-  if (const char* v = getenv("IGN_SEQ_VARIANT")) p->seq_variant = std::min(7, std::max(2, atoi(v)));
+  if (const char* v = getenv("IGN_SEQ_VARIANT")) {   // 6 (default), 4 or 2; anything else: 6
+    const int sv = atoi(v);
+    p->seq_variant = sv == 2 || sv == 4 ? sv : 6;
+  }
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 || atoi(v) == 8 ? atoi(v) : 3;
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
@@ -221,7 +224,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_TSGEMM_BF")) p->tsgemm_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_SEQ_H16")) p->train_seq_h16 = atoi(v) != 0;
-  if (const char* v = getenv("IGN_READOUT_VARIANT")) p->readout_variant = std::min(4, std::max(1, atoi(v)));
+  if (const char* v = getenv("IGN_READOUT_VARIANT")) {   // 4 (default), 2 or 1; anything else: 4
+    const int rv = atoi(v);
+    p->readout_variant = rv == 1 || rv == 2 ? rv : 4;
+  }
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
   for (size_t e = 0; e < p->ents.size(); ++e) {
@@ -1282,7 +1288,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
     {   // MFMAs per wave step: split-fp16 / split-bf16 (variants 6, 7 / 4, 5; H = 32 / 64) passes x
         // 3 gates x H/16 x H/32 on the 16x16x32 pipe; f32 (seq_gru2) 3 gates x H/16 x H/4
       const int v = p->seq_variant;
-      const int passes = v == 6 ? 3 : v == 7 ? 4 : v == 5 ? 9 : 6;
+      const int passes = v == 6 ? 3 : 6;
       const bool bf = v >= 4 && (cp.H == 32 || cp.H == 64) && a.Ubf;
       const double ws = (double)mb.wave_steps;
       tm.begin(K_SEQ, mb.flops, mb.bytes,
@@ -1441,13 +1447,12 @@ int readout(ign_plan* p, ign_batch* b) {
     // variant 4: both layers x3 (16x16x32 f16, the bf16 rate)
     const double kh = 3.0 * k1;
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0),
-             h16 ? tiles * kh * kMfmaBf16Flops : bf ? tiles * k1 * (p->readout_variant == 3 ? 9 : 6) * kMfmaBf16Flops : 0,
+             h16 ? tiles * kh * kMfmaBf16Flops : bf ? tiles * k1 * 6 * kMfmaBf16Flops : 0,
              bf ? 0 : tiles * k1f * kMfmaF32Flops);
     if (h16)
       HIP_TRY(launch_readout_h16(a, p->d_packed + l2.pk_h, l1.in, st));
     else if (bf)
-      HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in,
-                                p->readout_variant == 3 ? 9 : 6, st));
+      HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in, 6, st));
     else
       HIP_TRY(launch_readout3(a, l1.in, l1.out, l2.out, st));
     tm.end();

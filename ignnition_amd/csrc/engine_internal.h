@@ -246,13 +246,11 @@ struct ign_plan {
   float* d_packed = nullptr;
   bool params_set = false;
   bool fused_readout = false;
-  int readout_variant = 4;        // fused readout: 4 = layer 2 on split-fp16 (3 products), 1 = f32 MFMA
-                                  // (readout3), 2 / 3 = split-bf16 with 6 / 9
-                                  // piece products (readout_bf); IGN_READOUT_VARIANT
+  int readout_variant = 4;        // fused readout: 4 = both layers on split-fp16 (3 products), 1 = f32
+                                  // MFMA (readout3), 2 = split-bf16 x6 (readout_bf); IGN_READOUT_VARIANT
   int ro_width = 0;
-  int seq_variant = 6;            // ordered update: 4 / 5 = split-bf16 h.U with 6 / 9 piece products,
-                                  // 6 / 7 = split-fp16 with 3 / 4 (inference; H = 32, 64), 2 = f32
-                                  // MFMA; IGN_SEQ_VARIANT
+  int seq_variant = 6;            // ordered update: 6 = split-fp16 h.U with 3 piece products (H = 32,
+                                  // 64), 4 = split-bf16 x6, 2 = f32 MFMA; IGN_SEQ_VARIANT
   int xcd_remap = 0;              // XCD-aware tile order in the GRU kernels (placement only; off:
                                   // measured slower, profiles/r02/seq_experiments)
   bool fuse_proj = true;          // sum_gru_g32 projects for the next ordered MP (IGN_FUSE_PROJ=0: off)
@@ -283,7 +281,7 @@ struct ign_plan {
 };
 
 // the ordered update of the training forward saves every step's state, which the split-fp16 kernels
-// (variants 6 / 7, inference only) do not: training runs the x6 split-bf16 form for them
+// (variant 6 at H = 64) do not: training runs the x6 split-bf16 form there
 // the training forward's ordered update: split-fp16 x3 with state saving (seq_gru_h16<SAVE>) where
 // the backward can recompute its gates bitwise (fused seq_gru_bwd, H = 32; IGN_TRAIN_SEQ_H16=0: the
 // split-bf16 x6 form), else split-bf16 x6 / f32

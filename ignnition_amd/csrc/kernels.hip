@@ -944,14 +944,11 @@ static int persistent_grid(K kernel, int64_t n_blocks_of_work, int block = 256) 
 
 hipError_t launch_seq_gru(const SeqGruArgs& args, int h, int variant, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  // 6 / 7: split-fp16 h.U with 3 / 4 piece products (the state-saving training forward: 6 only);
-  // 4 / 5: split-bf16 h.U with 6 / 9 piece products (kernels_bf.hip; H = 32, 64); 2: f32 MFMA
-  if ((variant == 6 || variant == 7) && (h == 32 || h == 64) && args.Uh && args.hdr &&
-      (!args.hs_save || variant == 6))
-    return launch_seq_gru_h16(args, h, variant == 6 ? 3 : 4, st);
-  if (variant >= 6) variant = 4;
-  if ((variant == 4 || variant == 5) && (h == 32 || h == 64))
-    return launch_seq_gru_bf(args, h, variant == 5 ? 9 : 6, st);
+  // 6: split-fp16 h.U, 3 piece products; 4: split-bf16 h.U, 6 piece products (kernels_bf.hip;
+  // H = 32, 64); 2: f32 MFMA.  (Round 3 dropped the 4-product fp16 and 9-product bf16 forms: no
+  // caller after the full-batch precision study)
+  if (variant == 6 && (h == 32 || h == 64) && args.Uh && args.hdr) return launch_seq_gru_h16(args, h, 3, st);
+  if (variant >= 4 && (h == 32 || h == 64)) return launch_seq_gru_bf(args, h, 6, st);
   const int64_t work = grid_for(args.n_dst, 64);
   if (h == 32) {
     auto k = args.hs_save ? seq_gru2_kernel<32, true> : seq_gru2_kernel<32, false>;

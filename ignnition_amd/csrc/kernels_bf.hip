@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   constexpr int NT = H / 16, KS = H / 32;
   constexpr int NF = 6 * NT * KS;            // fragments: 2 pieces x 3 gates x NT tiles x KS k-steps
   static_assert(H == 32 || H == 64, "split-fp16 ordered update: 32 or 64 units");
-  static_assert(PASSES == 3 || PASSES == 4, "3 or 4 piece products");
+  static_assert(PASSES == 3, "3 piece products (lo*lo dropped)");
   __shared__ float sbias[H];
   __shared__ float sbn[4][H];                // per wave: the candidate's recurrent bias times SS
   __shared__ h8 su[NF * 64];
@@ -1732,17 +1732,15 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
 
 hipError_t launch_seq_gru_bf(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (!args.Ubf || (h != 32 && h != 64) || (passes != 6 && passes != 9)) return hipErrorInvalidValue;
+  if (!args.Ubf || (h != 32 && h != 64) || passes != 6) return hipErrorInvalidValue;
   const int64_t work = grid_for(args.n_dst, 64);
 #define SEQ_BF(HH, P)                                                                              \
   {                                                                                                \
     auto k = args.hs_save ? seq_gru_bf_kernel<HH, true, P> : seq_gru_bf_kernel<HH, false, P>;      \
     hipLaunchKernelGGL(k, dim3(persistent_grid(k, work)), dim3(256), 0, st, args);                \
   }
-  if (h == 32 && passes == 6) SEQ_BF(32, 6)
-  else if (h == 32) SEQ_BF(32, 9)
-  else if (passes == 6) SEQ_BF(64, 6)
-  else SEQ_BF(64, 9)
+  if (h == 32) SEQ_BF(32, 6)
+  else SEQ_BF(64, 6)
 #undef SEQ_BF
   return hipGetLastError();
 }
@@ -1776,8 +1774,9 @@ bool readout_bf_supported(int din, int n1, int n2, int act1, int act2) {
 hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
                              hipStream_t st) {
   if (args.n_rows == 0) return hipSuccess;
-  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f) return hipErrorInvalidValue;
-  // default (passes 6): two 16-row tiles per wave sharing every W2 fragment read, 8-wave blocks
+  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !W1f || !W2f || passes != 6)
+    return hipErrorInvalidValue;
+  // split-bf16 x6 (the x9 form was dropped in round 3: no caller after the precision study): two 16-row tiles per wave sharing every W2 fragment read, 8-wave blocks
   // (246 VGPRs, 2 waves/SIMD): 1.03-1.05 ms against 1.13-1.16 ms for one tile per wave in 12-wave
   // blocks, 1.18 ms with 32-unit W2 chunks, 1.39-1.41 ms with 4-wave blocks (512 x synth50, round 1)
   // persistent blocks (W1 staged once per block, W2 chunk 0 carried over): 3.54-3.56 vs 3.58-3.59
@@ -1786,10 +1785,10 @@ hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const vo
   // launch, 3.51 vs 3.58-3.59 ms/step (same box, round 2); b1/b2/w3 read from LDS (no vmcnt wait in the
   // loops, which would also have waited for the DMA): 0.983-0.989 vs 1.020-1.042 ms
   if (din == 32)
-    return passes == 9 ? readout_bf_din<32, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<32, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
+    return readout_bf_din<32, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
   // DIN 64 (the 1M-node graph): W1's pieces (96 KB) in LDS beside the W2 double buffer (48 KB),
   // persistent blocks: 5.01-5.02 vs 5.14-5.25 ms/step with W1 read from L2 per wave (round 2)
-  return passes == 9 ? readout_bf_din<64, 12, 9, 1>(args, W1f, W2f, st) : readout_bf_din<64, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
+  return readout_bf_din<64, 8, 6, 1, true, 2, true>(args, W1f, W2f, st);
 }
 
 
@@ -1964,7 +1963,7 @@ hipError_t launch_pack_dense_bf16(const float* W, void* out, int IN, int OUT, in
 
 hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStream_t st) {
   if (args.n_dst == 0) return hipSuccess;
-  if (!args.Uh || !args.hdr || (h != 32 && h != 64) || (passes != 3 && passes != 4) ||
+  if (!args.Uh || !args.hdr || (h != 32 && h != 64) || passes != 3 ||
       (args.hs_save && passes != 3))
     return hipErrorInvalidValue;
   const int64_t work = grid_for(args.n_dst, 64);
@@ -1976,10 +1975,8 @@ hipError_t launch_seq_gru_h16(const SeqGruArgs& args, int h, int passes, hipStre
   if (args.hs_save) {
     if (h == 32) SEQ_H(32, 3, true)
     else SEQ_H(64, 3, true)
-  } else if (h == 32 && passes == 3) SEQ_H(32, 3, false)
-  else if (h == 32) SEQ_H(32, 4, false)
-  else if (passes == 3) SEQ_H(64, 3, false)
-  else SEQ_H(64, 4, false)
+  } else if (h == 32) SEQ_H(32, 3, false)
+  else SEQ_H(64, 3, false)
 #undef SEQ_H
   return hipGetLastError();
 }

@@ -289,9 +289,9 @@ def _scaled_err(got, exp):
 
 @pytest.mark.parametrize("hidden", [32, 64])
 def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
-    """Ordered-update variants 4 / 5 and readout variants 2 / 3 form their contractions from
-    exact 3-piece bf16 splits (6 / 9 piece products, fp32 accumulation); ordered-update variants
-    6 / 7 and readout variant 4's layer 2 from scaled 2-piece fp16 splits (3 / 4 piece products).  Their error vs the
+    """Ordered-update variant 4 and readout variant 2 form their contractions from exact 3-piece
+    bf16 splits (6 piece products, fp32 accumulation); ordered-update variant 6 and readout
+    variant 4 from scaled 2-piece fp16 splits (3 piece products).  Their error vs the
     float64 oracle stays at the level of the native f32-MFMA kernels (seq 2, readout 1): within
     4x of it (or 1e-6), far inside the 1e-4 parity tolerance."""
     desc = model_examples.routenet(hidden=hidden, iterations=8)
@@ -302,8 +302,7 @@ def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
     prm = plan.init_params(5, bias_scale=0.2)
     ref = DenseOracle(desc, dims, prm).forward(graphs)
     errs = {}
-    for seq, ro in (("2", "1"), ("4", "1"), ("5", "1"), ("6", "1"), ("7", "1"), ("2", "2"), ("2", "3"), ("4", "2"),
-                    ("2", "4"), ("6", "4")):
+    for seq, ro in (("2", "1"), ("4", "1"), ("6", "1"), ("2", "2"), ("4", "2"), ("2", "4"), ("6", "4")):
         monkeypatch.setenv("IGN_SEQ_VARIANT", seq)
         monkeypatch.setenv("IGN_READOUT_VARIANT", ro)
         eng = Engine(plan, 0)
@@ -322,7 +321,7 @@ def test_split_bf16_contractions_are_fp32_accurate(monkeypatch, hidden):
 @pytest.mark.parametrize("hidden", [32, 64])
 @pytest.mark.parametrize("scale", [1e-3, 1.0, 3e4])
 def test_split_fp16_scaling(monkeypatch, hidden, scale):
-    """Ordered-update variants 6 / 7 scale the state by a power of two per 16-row tile (from the
+    """Ordered-update variant 6 scales the state by a power of two per 16-row tile (from the
     tile's max |h|, which the GRU never exceeds along the sequence) and U by one at pack time;
     readout variant 4 scales each row tile's layer-2 input from a bound on the layer-1
     activations (max |x| of the tile, W1's column norms, b1) and W2 at pack time.  So the fp16
@@ -340,7 +339,7 @@ def test_split_fp16_scaling(monkeypatch, hidden, scale):
     prm = plan.init_params(11, bias_scale=0.2)
     ref = DenseOracle(desc, dims, prm).forward(graphs)
     errs = {}
-    for seq, ro in (("2", "1"), ("6", "1"), ("7", "1"), ("2", "4"), ("6", "4")):
+    for seq, ro in (("2", "1"), ("6", "1"), ("2", "4"), ("6", "4")):
         monkeypatch.setenv("IGN_SEQ_VARIANT", seq)
         monkeypatch.setenv("IGN_READOUT_VARIANT", ro)
         eng = Engine(plan, 0)
