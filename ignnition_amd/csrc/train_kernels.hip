@@ -975,6 +975,8 @@ __global__ void reduce_seg_kernel(const float* __restrict__ part, int64_t nchunk
   const int s = blockIdx.y;
   if (i >= size) return;
   float acc = 0.f;
+  // unrolled: the loads of 8 chunks are in flight at once (the adds keep the chunk order)
+#pragma unroll 8
   for (int64_t c = s; c < nchunks; c += S) acc += part[c * size + i];
   seg[(int64_t)s * size + i] = acc;
 }
@@ -985,6 +987,7 @@ __global__ void reduce_final_kernel(const float* __restrict__ seg, int S, int M,
   const int64_t size = (int64_t)(M + ones) * N;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < size; i += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.f;
+#pragma unroll 16
     for (int s = 0; s < S; ++s) acc += seg[(int64_t)s * size + i];
     if (i < (int64_t)M * N) C[i] += acc;
     else Cb[i - (int64_t)M * N] += acc;
