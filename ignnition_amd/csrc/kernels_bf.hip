@@ -954,12 +954,16 @@ __global__ __launch_bounds__(256) void tsgemm_bf_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int Mx = M + ones;
-  const int tiles_m = (Mx + 63) / 64, tiles_n = (N + 63) / 64;
+  // M a multiple of 64 (the readout's 256-wide layers): the ones column would be a tile row of its
+  // own whose waves load and split B for column sums only; the m0 = 0 tiles sum B's columns
+  // instead (every wave holds its B columns anyway; the same sums in the same order)
+  const bool fold = ones && M > 0 && M % 64 == 0;
+  const int tiles_m = fold ? M / 64 : (Mx + 63) / 64, tiles_n = (N + 63) / 64;
   const int tile = blockIdx.y * (blockDim.x >> 6) + wave;
   if (tile >= tiles_m * tiles_n) return;
   const int m0 = (tile / tiles_n) * 64, n0 = (tile % tiles_n) * 64;
   const int na = max(0, min(4, (M - m0 + 15) / 16)), nb = min(4, (N - n0 + 15) / 16);
-  const bool has_ones = ones && M >= m0 && M < m0 + 64;
+  const bool has_ones = ones && (fold ? m0 == 0 : M >= m0 && M < m0 + 64);
   const int64_t r0 = (int64_t)blockIdx.x * chunk;
   const int64_t r1 = std::min<int64_t>(n_rows, r0 + chunk);
   const int g = lane >> 4, c = lane & 15;
@@ -2071,6 +2075,7 @@ hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t
 
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
                             int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st) {
+  if (ones && M > 0 && M % 64 == 0) tiles = (M / 64) * ((N + 63) / 64);   // the ones row folded (kernel)
   dim3 grid((unsigned)chunks, (unsigned)((tiles + wpb - 1) / wpb));
   hipLaunchKernelGGL(tsgemm_bf_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, part);
   return hipGetLastError();
