@@ -502,6 +502,8 @@ def main():
         il = isolated["launches"]
         iavg = isolated["ms"] / il / 1e3
         iach = (isolated["bytes"] / il / iavg / 1e9) if roof["unit"] == "GB/s" else (isolated["flops"] / il / iavg / 1e12)
+        roof["note"] = ("timed region: %d sub-batches on %d streams, so each launch of the kernel shares the chip "
+                        "with the other sub-batches' kernels; 'isolated' is the same kernel alone" % (len(subs), len(subs)))
         roof["isolated"] = {"what": "sub-batch 0 (%d graphs) alone on the chip, after the timed region"
                                     % subs[0].num_graphs,
                             "launches": il, "avg_launch_ms": round(iavg * 1e3, 4),
