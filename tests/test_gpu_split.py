@@ -63,3 +63,29 @@ def test_split_batch_replicas_follow_parameter_updates():
     stepped = sb.forward()
     assert not np.array_equal(stepped, after)
     assert np.array_equal(stepped, Batch(eng, graphs).forward())
+
+
+def test_bench_line_with_sub_batch_streams():
+    """bench.py's default step (two sub-batch streams) on a small batch: one JSON line whose
+    roofline carries the timed region's figure and the isolated one; --streams 1 has no isolated leg."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lines = {}
+    for streams in (2, 1):
+        r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--graphs", "16", "--steps", "2",
+                            "--warmup", "1", "--no-cpu", "--streams", str(streams)],
+                           capture_output=True, text=True, timeout=300, cwd=repo)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+        assert len(out) == 1
+        lines[streams] = out[0]
+    two, one = lines[2], lines[1]
+    assert two["config"]["streams"] == 2 and one["config"]["streams"] == 1
+    assert two["config"]["edges_per_step_per_gpu"] == one["config"]["edges_per_step_per_gpu"]
+    assert two["value"] > 0 and one["value"] > 0
+    iso = two["roofline"]["isolated"]
+    assert iso["launches"] > 0 and 0 < iso["frac"] and "note" in two["roofline"]
+    assert "isolated" not in one["roofline"]
