@@ -731,6 +731,15 @@ class Batch:
         self.close()
 
 
+def split_cuts(n_graphs: int, parts: int) -> list:
+    """Boundaries of ``parts`` sub-batches of consecutive graphs (at most one per graph, at least
+    one): sub-batch i is graphs [cuts[i], cuts[i + 1]), sizes differing by at most one."""
+    if n_graphs < 1:
+        raise ValueError("SplitBatch: no graphs")
+    parts = max(1, min(int(parts), n_graphs))
+    return [n_graphs * i // parts for i in range(parts + 1)]
+
+
 class SplitBatch:
     """The graphs as ``parts`` sub-batches of consecutive graphs, sub-batch i on the engine's
     replica i (its own plan and HIP stream; replica 0 is the engine itself).  ``forward`` enqueues
@@ -741,10 +750,10 @@ class SplitBatch:
 
     def __init__(self, engine: Engine, graphs, parts: int = 2):
         graphs = list(graphs)
-        parts = max(1, min(int(parts), len(graphs)))
+        cuts = split_cuts(len(graphs), parts)
+        parts = len(cuts) - 1
         self.engine = engine
         self.engines = [engine] + engine.replicas(parts - 1)
-        cuts = [len(graphs) * i // parts for i in range(parts + 1)]
         self.parts = [Batch(e, graphs[cuts[i]:cuts[i + 1]]) for i, e in enumerate(self.engines)]
         self.num_graphs = sum(b.num_graphs for b in self.parts)
         self.predictions = sum(b.predictions for b in self.parts)

@@ -235,3 +235,16 @@ def test_python_input_stream_has_its_own_rng(example_dir):
         random.shuffle(list(range(10)))
         r1 = lab(next(ranks[1])[1])
         assert r0 + r1 == g
+
+
+def test_split_cuts_partition_graphs_evenly():
+    """engine.SplitBatch's sub-batches: consecutive graphs, every graph once, sizes within one."""
+    from ignnition_amd.engine import split_cuts
+    for n in (1, 2, 3, 5, 16, 511, 512):
+        for parts in (1, 2, 3, 4, 8):
+            c = split_cuts(n, parts)
+            assert c[0] == 0 and c[-1] == n and len(c) == min(parts, n) + 1
+            sizes = [b - a for a, b in zip(c, c[1:])]
+            assert min(sizes) >= 1 and max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        split_cuts(0, 2)
