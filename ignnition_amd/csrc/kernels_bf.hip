@@ -1864,7 +1864,20 @@ static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const voi
 template <bool BWD, int NP = 3>
 static hipError_t dense_bf_any(const float* x, int64_t n, int K, int x_stride, const void* W, const float* bias, int M,
                                int act, float* y, const float* aprev, int accumulate, hipStream_t st) {
-  // stages of <= 24 KB: G 16-unit tiles of K x 16 x NP pieces (M % 128 == 0: G divides M / 16)
+  // G 16-unit tiles of K x 16 x NP pieces per stage (M % 128 == 0: G divides M / 16).  NP = 2: 32 KB
+  // stages, so each pass writes >= 128 B (whole lines) of every row: 0.949 -> 0.877 ms for the
+  // 256-wide training readout layer, 19.9 -> 19.8 ms per step; NP = 3: <= 24 KB
+#ifndef IGN_DENSE_G256
+#define IGN_DENSE_G256 2
+#endif
+  if constexpr (NP == 2) {
+    switch (K) {
+      case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+      case 64: return dense_bf_ks<2, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+      case 128: return dense_bf_ks<4, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+      default: return dense_bf_ks<8, IGN_DENSE_G256, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    }
+  }
   switch (K) {
     case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
     case 64: return dense_bf_ks<2, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);

@@ -1,0 +1,14 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+mkdir -p gpurun_out/ab31
+for n in g2 g4; do
+  IGN_LIB_PATH=$PWD/ignnition_amd/ab/lib_$n.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab31/$n -o $n --output-format csv -- python3 bench.py --train --steps 2 --warmup 1 --no-cpu > gpurun_out/ab31/$n.log 2>&1 || exit 1
+done
+for r in 1 2; do
+  for n in g2 g4; do
+    IGN_LIB_PATH=$PWD/ignnition_amd/ab/lib_$n.so timeout -k 10 200 python bench.py --no-cpu --train --steps 10 > gpurun_out/ab31/t-$n-$r.json 2>&1 || exit 1
+  done
+done
+for n in g2 g4; do
+  IGN_LIB_PATH=$PWD/ignnition_amd/ab/lib_$n.so timeout -k 10 600 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab31/train_tests_$n.log 2>&1 || exit 1
+done
