@@ -1060,6 +1060,134 @@ __global__ __launch_bounds__(256) void tsgemm_bf_kernel(const float* __restrict_
   }
 }
 
+// tsgemm_bf_kernel for M % 64 == N % 64 == 0 with the pieces split once per block: a block of
+// mtb x tiles_n waves holds the tiles of mtb 64-column groups of A against all of B.  Per 32-row
+// step every (column, 8-row group) pair of the block's A columns and of B is loaded once (64 lanes =
+// 64 consecutive columns of one row per load), split into its three bf16 pieces and written to LDS
+// as 16-B fragments [piece][column][row group]; the waves read their MFMA operands from there (one
+// contiguous 1 KB per fragment read).  The next step's loads are in flight during the MFMAs.  The
+// old kernel split every value once per wave that used it (4 times at 256 x 256).  Same products in
+// the same order per accumulator and the same column-sum order: bitwise the old kernel's partials.
+constexpr int kTsLdsCols = 384;   // A columns of the block + N
+__global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restrict__ A, int lda,
+                                                            const float* __restrict__ B, int ldb, int64_t n_rows,
+                                                            int M, int N, int ones, int64_t chunk, int mtb,
+                                                            float* __restrict__ part) {
+  constexpr int NTH = 512, KP = (kTsLdsCols * 4 + NTH - 1) / NTH;
+  __shared__ u4v sp[3 * kTsLdsCols * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int tiles_n = N / 64, AC = 64 * mtb, COLS = AC + N;
+  const int mg0 = blockIdx.y * AC;   // the block's first A column
+  const int mt = wave / tiles_n, nt = wave % tiles_n;
+  const bool tile_ok = mt < mtb && mg0 + 64 * mt < M;
+  const bool sums = ones && blockIdx.y == 0;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk;
+  const int64_t r1 = std::min<int64_t>(n_rows, r0 + chunk);
+  // the thread's (column, row group) pairs: p = tid + NTH k, row group p / COLS, column p % COLS
+  const float* src[KP];
+  int64_t ld[KP];
+  int gp[KP];
+  bool pok[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int p = tid + NTH * k;
+    const int col = p % COLS;
+    gp[k] = p / COLS;
+    pok[k] = p < 4 * COLS && (col >= AC || mg0 + col < M);
+    src[k] = col < AC ? A + (pok[k] ? mg0 + col : 0) : B + (col - AC);
+    ld[k] = col < AC ? lda : ldb;
+  }
+  float v[KP][8];
+  auto load = [&](int64_t r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int64_t rr = r + 8 * gp[k] + jj;
+        v[k][jj] = (pok[k] && rr < r1) ? src[k][rr * ld[k]] : 0.f;
+      }
+  };
+  float cs[KP] = {};
+  f4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f4{0, 0, 0, 0};
+  if (r0 < r1) load(r0);
+  for (int64_t r = r0; r < r1; r += 32) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const int p = tid + NTH * k;
+      if (p >= 4 * COLS) continue;
+      const int col = p % COLS;
+      u4v w0, w1, w2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a0, a1, a2, b0, b1, b2;
+        split3(v[k][2 * q], a0, a1, a2);
+        split3(v[k][2 * q + 1], b0, b1, b2);
+        w0[q] = pack_hi16(a0, b0);
+        w1[q] = pack_hi16(a1, b1);
+        w2[q] = pack_hi16(a2, b2);
+      }
+      sp[(0 * COLS + col) * 4 + gp[k]] = w0;
+      sp[(1 * COLS + col) * 4 + gp[k]] = w1;
+      sp[(2 * COLS + col) * 4 + gp[k]] = w2;
+      if (sums && col >= AC) {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) cs[k] += v[k][jj];
+      }
+    }
+    __syncthreads();
+    if (r + 32 < r1) load(r + 32);
+    if (tile_ok) {
+      const int ac = 64 * mt + c, bc = AC + 64 * nt + c;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        bf8 bp[3];
+#pragma unroll
+        for (int pb = 0; pb < 3; ++pb)
+          bp[pb] = __builtin_bit_cast(bf8, sp[(pb * COLS + bc + 16 * y) * 4 + g]);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          bf8 ap[3];
+#pragma unroll
+          for (int pa = 0; pa < 3; ++pa)
+            ap[pa] = __builtin_bit_cast(bf8, sp[(pa * COLS + ac + 16 * x) * 4 + g]);
+#pragma unroll
+          for (int pa = 2; pa >= 0; --pa)
+#pragma unroll
+            for (int pb = 2 - pa; pb >= 0; --pb) acc[x][y] = MFMA_BF(ap[pa], bp[pb], acc[x][y]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int Mx = M + ones;
+  float* P = part + (int64_t)blockIdx.x * Mx * N;
+  if (tile_ok) {
+    const int m0 = mg0 + 64 * mt, n0 = 64 * nt;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) P[(int64_t)(m0 + 16 * x + 4 * g + q) * N + n0 + 16 * y + c] = acc[x][y][q];
+  }
+  if (sums) {   // (s0 + s1) + (s2 + s3) over the four row groups, as the old kernel's two shuffles
+    float* cl = reinterpret_cast<float*>(sp);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const int p = tid + NTH * k;
+      const int col = p % COLS;
+      if (p < 4 * COLS && col >= AC) cl[(col - AC) * 4 + gp[k]] = cs[k];
+    }
+    __syncthreads();
+    for (int n = tid; n < N; n += NTH) P[(int64_t)M * N + n] = (cl[4 * n] + cl[4 * n + 1]) + (cl[4 * n + 2] + cl[4 * n + 3]);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fused readout MLP on the bf16 matrix path, fp32-exact operands (device_common.h, split-bf16):
 // y = act2(act1(X W1 + b1) W2 + b2) . w3 + b3 with every contraction formed from exact 3-piece
@@ -2088,6 +2216,16 @@ hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t
 
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
                             int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st) {
+#ifdef IGN_TSGEMM_LDS
+  if (M > 0 && N > 0 && M % 64 == 0 && N % 64 == 0 && N <= 256 && (M / 64) * (N / 64) >= 4) {
+    const int tiles_m = M / 64, tiles_n = N / 64;
+    const int mtb = std::min(std::min(tiles_m, 8 / tiles_n), (kTsLdsCols - N) / 64);
+    const dim3 g2((unsigned)chunks, (unsigned)((tiles_m + mtb - 1) / mtb));
+    hipLaunchKernelGGL(tsgemm_bf_lds_kernel, g2, dim3(512), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, mtb,
+                       part);
+    return hipGetLastError();
+  }
+#endif
   if (ones && M > 0 && M % 64 == 0) tiles = (M / 64) * ((N + 63) / 64);   // the ones row folded (kernel)
   dim3 grid((unsigned)chunks, (unsigned)((tiles + wpb - 1) / wpb));
   hipLaunchKernelGGL(tsgemm_bf_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, part);
