@@ -1074,7 +1074,11 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
                                                             int M, int N, int ones, int64_t chunk, int mtb,
                                                             float* __restrict__ part) {
   constexpr int NTH = 512, KP = (kTsLdsCols * 4 + NTH - 1) / NTH;
+#ifdef IGN_TSGEMM_DB
+  __shared__ u4v sp[2 * 3 * kTsLdsCols * 4];
+#else
   __shared__ u4v sp[3 * kTsLdsCols * 4];
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int tiles_n = N / 64, AC = 64 * mtb, COLS = AC + N;
@@ -1114,8 +1118,8 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
   for (int x = 0; x < 4; ++x)
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f4{0, 0, 0, 0};
-  if (r0 < r1) load(r0);
-  for (int64_t r = r0; r < r1; r += 32) {
+  // split the loaded pairs into buffer bo's fragments (and the bias column sums)
+  auto split_store = [&](u4v* bo) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
       const int p = tid + NTH * k;
@@ -1131,39 +1135,61 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
         w1[q] = pack_hi16(a1, b1);
         w2[q] = pack_hi16(a2, b2);
       }
-      sp[(0 * COLS + col) * 4 + gp[k]] = w0;
-      sp[(1 * COLS + col) * 4 + gp[k]] = w1;
-      sp[(2 * COLS + col) * 4 + gp[k]] = w2;
+      bo[(0 * COLS + col) * 4 + gp[k]] = w0;
+      bo[(1 * COLS + col) * 4 + gp[k]] = w1;
+      bo[(2 * COLS + col) * 4 + gp[k]] = w2;
       if (sums && col >= AC) {
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) cs[k] += v[k][jj];
       }
     }
-    __syncthreads();
-    if (r + 32 < r1) load(r + 32);
-    if (tile_ok) {
-      const int ac = 64 * mt + c, bc = AC + 64 * nt + c;
+  };
+  auto contract = [&](const u4v* bi) __attribute__((always_inline)) {
+    if (!tile_ok) return;
+    const int ac = 64 * mt + c, bc = AC + 64 * nt + c;
 #pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        bf8 bp[3];
+    for (int y = 0; y < 4; ++y) {
+      bf8 bp[3];
 #pragma unroll
-        for (int pb = 0; pb < 3; ++pb)
-          bp[pb] = __builtin_bit_cast(bf8, sp[(pb * COLS + bc + 16 * y) * 4 + g]);
+      for (int pb = 0; pb < 3; ++pb) bp[pb] = __builtin_bit_cast(bf8, bi[(pb * COLS + bc + 16 * y) * 4 + g]);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          bf8 ap[3];
+      for (int x = 0; x < 4; ++x) {
+        bf8 ap[3];
 #pragma unroll
-          for (int pa = 0; pa < 3; ++pa)
-            ap[pa] = __builtin_bit_cast(bf8, sp[(pa * COLS + ac + 16 * x) * 4 + g]);
+        for (int pa = 0; pa < 3; ++pa) ap[pa] = __builtin_bit_cast(bf8, bi[(pa * COLS + ac + 16 * x) * 4 + g]);
 #pragma unroll
-          for (int pa = 2; pa >= 0; --pa)
+        for (int pa = 2; pa >= 0; --pa)
 #pragma unroll
-            for (int pb = 2 - pa; pb >= 0; --pb) acc[x][y] = MFMA_BF(ap[pa], bp[pb], acc[x][y]);
-        }
+          for (int pb = 2 - pa; pb >= 0; --pb) acc[x][y] = MFMA_BF(ap[pa], bp[pb], acc[x][y]);
       }
     }
+  };
+#ifdef IGN_TSGEMM_DB
+  // two buffers, one barrier per step: step s+1's pieces are split while step s's MFMAs run
+  if (r0 < r1) {
+    load(r0);
+    split_store(sp);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int64_t r = r0; r < r1; r += 32) {
+    const bool more = r + 32 < r1;
+    if (more) load(r + 32);
+    contract(sp + cur * (3 * kTsLdsCols * 4));
+    if (more) split_store(sp + (cur ^ 1) * (3 * kTsLdsCols * 4));
+    __syncthreads();
+    cur ^= 1;
+  }
+#else
+  if (r0 < r1) load(r0);
+  for (int64_t r = r0; r < r1; r += 32) {
+    split_store(sp);
+    __syncthreads();
+    if (r + 32 < r1) load(r + 32);
+    contract(sp);
     __syncthreads();
   }
+#endif
   const int Mx = M + ones;
   float* P = part + (int64_t)blockIdx.x * Mx * N;
   if (tile_ok) {
