@@ -62,6 +62,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--no-edge-cut", action="store_true",
+                    help="skip the edge-cut leg (the 1M-node / 10M-edge graph of BASELINE configs[4] split across "
+                         "the same ranks, RCCL halo all-to-all per MP; at N=1 the whole graph on one GPU), which "
+                         "otherwise runs after the main measurement and is reported under 'edge_cut_1m'")
+    ap.add_argument("--edge-cut-nodes", type=int, default=1_000_000, help="edge-cut leg: synthetic graph size")
+    ap.add_argument("--edge-cut-steps", type=int, default=0, help="edge-cut leg: timed forwards (0: --steps)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: every rank builds its shard's host inputs and runs the barrier / max-over-ranks "
                          "timing / edge-sum reduction around K empty steps (gloo); rank 0 prints the line with "
@@ -208,6 +214,136 @@ def cpu_baseline_cxx(plan, mi, prm, graphs, budget_s, what="synth50 graphs"):
     return {"value": edges / dt, "unit": "edges/s", "cores": n, "kind": "port", "cpu_model": _cpu_model(),
             "sample": "%d forwards of %s (full T=8 each) in %.1f s, OpenMP %d threads, C++ float32 restatement "
                       "(oracle/cpu_forward.cpp: packed per destination, no padded work)" % (done, what, dt, n)}
+
+
+def _reduce(dist, vals, op, device=None):
+    """Element-wise MAX or SUM of a list of numbers over the ranks (unchanged without ``dist``)."""
+    if dist is None:
+        return [float(v) for v in vals]
+    import torch
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return t.cpu().tolist()
+
+
+def edge_cut_key(nodes: int) -> str:
+    return "edge_cut_1m" if nodes == 1_000_000 else "edge_cut_%dn" % nodes
+
+
+def edge_cut_parts(args, dist, rank, world):
+    """The edge-cut leg's host side: the seeded synthetic graph (every rank generates the same one),
+    its plan, and this rank's partition with its halo send lists (one all-to-all of ids)."""
+    from ignnition_amd import partition, workloads
+    from ignnition_amd.engine import MPPlan
+    desc, dims, mi, graphs, _ = workloads.make_synthetic_inputs(n_nodes=args.edge_cut_nodes)
+    plan = MPPlan.from_model_info(mi)
+    part = None
+    if world > 1:
+        part = partition.local_part(graphs[0], plan, rank, world)
+    return mi, plan, graphs, part
+
+
+def edge_cut_leg(args, dist, rank, world, device, backend):
+    """SURVEY §8(e) / BASELINE configs[4], run in the same ranks after the main measurement: the
+    synthetic 1M-node / 10M-edge graph (H=64, T=8, sum + GRU, predict readout) edge-cut across the
+    ``world`` ranks.  Contiguous node ranges, owner computes by destination; before every MP the
+    halo rows go to their readers with one RCCL ``all_to_all_single`` while the interior
+    destinations run (partition.EdgeCutForward).  At N=1 the whole graph runs on one GPU
+    (Batch.forward), so the driver's N=1 and N=8 lines time the same work (strong scaling).
+    Returns the JSON object of the leg (identical on every rank)."""
+    import torch
+    from ignnition_amd import partition, workloads
+    from ignnition_amd.engine import Batch, Engine
+    steps = args.edge_cut_steps or args.steps
+    t_build = time.perf_counter()
+    mi, plan, graphs, part = edge_cut_parts(args, dist, rank, world)
+    name, H, T = plan.entities[0], plan.hidden[0], plan.iterations
+    torch.cuda.set_device(device)
+    eng = Engine(plan, device)
+    eng.set_params(plan.init_params(seed=0, bias_scale=0.05))
+    dev = torch.device("cuda", device) if backend == "nccl" else None
+    fw = batch = None
+    halo = send = 0
+    if world > 1:
+        if backend == "nccl":
+            comm = partition.TorchComm(dist, torch.device("cuda", device))
+        else:   # gloo rehearsal (several ranks on one GPU): rows staged through host memory
+            comm = partition.TorchComm(dist, None, host_staged=True)
+        partition.exchange_requests([part], comm)
+        fw = partition.EdgeCutForward(eng, [part], comm)
+        step = lambda: fw.forward(to_host=False)
+        edges = fw.edges_per_forward
+        halo, send = part.halos[name].n_halo, len(part.halos[name].send_rows)
+        interior, boundary = fw.batches[0].mp_split(0)
+    else:
+        batch = Batch(eng, graphs)
+        step = lambda: batch.forward(to_host=False)
+        edges = batch.edges_per_forward
+        interior, boundary = batch.rows[0], 0
+    t_build = time.perf_counter() - t_build
+
+    def sync():
+        torch.cuda.synchronize(device)
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize(device)
+
+    def timed(fn, k):
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        sync()
+        return time.perf_counter() - t0
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    dt = timed(step, steps)
+    res = {"metric": "message-passing edges/sec, synthetic 1M-node / 10M-edge graph (BASELINE configs[4])",
+           "unit": "edges/s", "n_ranks": dist.get_world_size() if dist is not None else 1, "steps": steps,
+           "warmup": max(args.warmup, 1), "scaling": "strong", "nodes": args.edge_cut_nodes, "hidden": H,
+           "iterations": T}
+    ex_ms = nov_ms = None
+    if fw is not None:
+        # the same forward with every exchange completed before its MP starts (no interior overlap)
+        fw.overlap = False
+        for _ in range(2):
+            step()
+        nov = timed(step, steps)
+        fw.overlap = True
+        # one exchange alone (halo pack + all_to_all_single), repeated: what one MP's exchange costs
+        reps = 4 * T
+        for _ in range(2):
+            fw._exchange(name, False).wait()
+        ex = timed(lambda: fw._exchange(name, False).wait(), reps)
+        dt, nov, ex = _reduce(dist, [dt, nov, ex], "max", dev)
+        ex_ms, nov_ms = ex / reps * 1e3, nov / steps * 1e3
+    else:
+        dt, = _reduce(dist, [dt], "max", dev)
+    tot_edges, tot_halo, tot_send, tot_int, tot_bnd = _reduce(dist, [edges, halo, send, interior, boundary], "sum",
+                                                              dev)
+    max_halo, = _reduce(dist, [halo], "max", dev)
+    whole = workloads.edges_per_forward(mi, graphs)
+    res.update({"value": tot_edges * steps / dt, "ms_per_step": dt / steps * 1e3,
+                "edges_per_step": int(tot_edges), "edges_per_step_whole_graph": int(whole),
+                "partition": ("contiguous node ranges over %d ranks, owner computes by destination; halo rows "
+                              "exchanged per MP with RCCL all_to_all_single, interior destinations overlapped"
+                              % world) if world > 1 else "whole graph on one GPU (no exchange)",
+                "halo_rows": {"max_rank": int(max_halo), "total": int(tot_halo)},
+                "halo_bytes_per_exchange": {"max_rank": int(max_halo) * H * 4, "total": int(tot_halo) * H * 4},
+                "exchanges_per_step": T if world > 1 else 0,
+                "exchange_ms_isolated": None if ex_ms is None else round(ex_ms, 4),
+                "ms_per_step_no_overlap": None if nov_ms is None else round(nov_ms, 4),
+                "interior_destinations": int(tot_int), "boundary_destinations": int(tot_bnd),
+                "transport": ("RCCL" if backend == "nccl" else "gloo, host-staged (rehearsal)") if world > 1 else None,
+                "edges_match_whole_graph": int(tot_edges) == int(whole),
+                "build_s": round(t_build, 3)})
+    if fw is not None:
+        fw.close()
+    if batch is not None:
+        batch.close()
+    eng.close()
+    return res
 
 
 def main():
@@ -434,6 +570,11 @@ def main():
     dt, total_edges_step = workloads.reduce_step_stats(dist, dt, edges, dev)
     total_edges = total_edges_step * args.steps
     value = total_edges / dt
+    edge_cut = None
+    if not (synthetic or args.train or args.no_edge_cut):
+        # BASELINE configs[4] in the same ranks: the 1M-node graph edge-cut over
+        # RCCL at N>1, whole on one GPU at N=1; the main line's value stays the RouteNet metric
+        edge_cut = edge_cut_leg(args, dist, rank, world, device if world > 1 else 0, backend)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -534,6 +675,8 @@ def main():
         "cpu_baseline": cpu,
         "cpu_baseline_cxx": cpu_cxx,
     }
+    if edge_cut is not None:
+        line[edge_cut_key(args.edge_cut_nodes)] = edge_cut
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
@@ -557,13 +700,34 @@ def dry_run(args, dist, rank, world, mi, graphs, synthetic):
         dist.barrier()
     dt = time.perf_counter() - t0
     dt, total = workloads.reduce_step_stats(dist, dt, edges)
+    edge_cut = None
+    if not (synthetic or args.train or args.no_edge_cut):
+        # the edge-cut leg's host side: every rank's partition of the seeded graph and the setup
+        # all-to-all of halo requests (gloo); the partitions' edges must add up to the graph's
+        from ignnition_amd import partition
+        emi, eplan, egraphs, part = edge_cut_parts(args, dist, rank, world)
+        name = eplan.entities[0]
+        halo = send = 0
+        if part is not None:
+            partition.exchange_requests([part], partition.TorchComm(dist, None))
+            halo, send = part.halos[name].n_halo, len(part.halos[name].send_rows)
+            e_local = workloads.edges_per_forward(emi, [part.inputs])
+        else:
+            e_local = workloads.edges_per_forward(emi, egraphs)
+        tot_e, tot_halo, tot_send = _reduce(dist, [e_local, halo, send], "sum")
+        whole = workloads.edges_per_forward(emi, egraphs)
+        edge_cut = {"value": None, "unit": "edges/s", "n_ranks": world, "nodes": args.edge_cut_nodes,
+                    "edges_per_step": int(tot_e), "edges_per_step_whole_graph": int(whole),
+                    "edges_match_whole_graph": int(tot_e) == int(whole),
+                    "halo_rows": {"total": int(tot_halo)}, "send_rows_total": int(tot_send), "dry_run": True}
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
                           "scaling": "strong" if synthetic else "weak", "vs_baseline": None, "dtype": "fp32",
                           "data": "dry run (no GPU)",
                           "config": {"workload": "%s_%s_x%d" % (args.model, args.topology, args.graphs),
-                                     "edges_per_step_total": total, "dry_run": True}}))
+                                     "edges_per_step_total": total, "dry_run": True},
+                          **({edge_cut_key(args.edge_cut_nodes): edge_cut} if edge_cut else {})}))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -176,7 +176,9 @@ def _load():
         "ign_batch_train_buffers": (C.c_int, [VP, i32, P(VP), P(VP)]),
         "ign_batch_read_predictions": (C.c_int, [VP, VP, VP]),
     }
-    ab = "IGN_LIB_PATH" in os.environ   # an A/B build of an older tree may lack newer entry points
+    # an A/B build of an older tree may lack newer entry points: only the A/B tools, which set
+    # IGN_AB_LIB=1 next to IGN_LIB_PATH, skip them; any other library must export every symbol
+    ab = os.environ.get("IGN_AB_LIB") == "1"
     for name, (res, args) in sig.items():
         if ab and not hasattr(lib, name):
             continue

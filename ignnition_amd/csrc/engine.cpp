@@ -554,10 +554,11 @@ int ign_plan_set_stream(ign_plan* p, void* s) {
   int rc = ensure_device(p);
   if (rc) return rc;
   if ((rc = flush_timing(p))) return rc;   // pending event pairs were recorded on the old stream
-  if (p->own_stream && p->stream) {
-    hipStreamSynchronize(p->stream);
-    hipStreamDestroy(p->stream);
-  }
+  // Pooled blocks of destroyed batches carry a fence recorded on the plan's stream at destroy time;
+  // from here on fences go to the new stream, so work still queued on the old one (own or external)
+  // must finish before a block it reads can be handed out again.
+  if (p->stream && p->stream != static_cast<hipStream_t>(s)) HIP_TRY(hipStreamSynchronize(p->stream));
+  if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
   p->own_stream = false;
   p->external_stream = true;
   p->stream = static_cast<hipStream_t>(s);

@@ -220,6 +220,21 @@ __global__ __launch_bounds__(256) void seq_gru_bf_kernel(SeqGruArgs a) {
 // SAVE (training forward, PASSES 3): also writes every state of the sequence to hs_save as
 // seq_gru_bf<SAVE> does (the state before, then the state after each step, unscaled), for the
 // backward's bitwise gate recompute (train_kernels.hip seq_gru_bwd_kernel<H, true, 2>).
+#ifdef IGN_SEQ_STAMP
+// Diagnostic build only (tools/build_ab.sh NAME -DIGN_SEQ_STAMP; tools/probes/seq_stamps.py): per
+// wave of the inference ordered update, s_memtime sums of its segments (cdna_hip_programming.md §7,
+// In-kernel stamps).  The stamps' waits and sched barriers change the schedule: read the shares.
+__device__ unsigned long long ign_seq_stamps[4096 * 8];
+#define IGN_STAMP(v)                                                                      \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+extern "C" int ign_debug_seq_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ign_seq_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int H, int PASSES, bool SAVE = false>
 __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   constexpr int NT = H / 16, KS = H / 32;
@@ -250,7 +265,15 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   // projected rows together.  No branch guards a load.
   int64_t tile = xcd_block(a.xcd_remap) * 4 + wave;
   i4v hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (min(tile, n_tiles - 1) * 16 + j));
+#ifdef IGN_SEQ_STAMP
+  unsigned long long s_pro = 0, s_mma = 0, s_gate = 0, s_epi = 0, n_tl = 0, n_st = 0, t_0, t_1, t_2, t_3;
+  IGN_STAMP(t_0);
+  const unsigned long long t_begin = t_0;
+#endif
   for (; tile < n_tiles; tile += tile_stride) {
+#ifdef IGN_SEQ_STAMP
+    IGN_STAMP(t_0);
+#endif
     const int64_t pos = tile * 16 + j;
     const bool valid = pos < a.n_dst;
     const int row = hd[0];
@@ -364,6 +387,12 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
         }
       }
       const bool act = t < L;
+#ifdef IGN_SEQ_STAMP
+      if constexpr (!SAVE) {
+        IGN_STAMP(t_2);
+        s_mma += t_2 - t_1;
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
@@ -392,19 +421,50 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
     // Lmin: final_len of the tile's last valid position (sorted descending); padding lanes of
     // the last tile run the unmasked steps too, harmlessly (their rows are never stored)
     const int Lmin = __builtin_amdgcn_readlane(L, (int)min<int64_t>(15, a.n_dst - 1 - tile * 16));
+#ifdef IGN_SEQ_STAMP
+    IGN_STAMP(t_1);
+    s_pro += t_1 - t_0;
+#endif
     for (int t = 0;;) {
+#ifdef IGN_SEQ_STAMP
+      IGN_STAMP(t_1);
+#endif
       if (t < Lmin) step(t, x, std::false_type{});
       else step(t, x, std::true_type{});
       save(t);
+#ifdef IGN_SEQ_STAMP
+      IGN_STAMP(t_3);
+      s_gate += t_3 - t_2;
+      ++n_st;
+#endif
       if (++t >= Lmax) break;
       load_x(code, x);
       code = codes[t + 1];
     }
+#ifdef IGN_SEQ_STAMP
+    IGN_STAMP(t_1);
+#endif
     if (valid) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) st4(a.h_out + (int64_t)row * H + 16 * t + 4 * g, h[t] * iS);
     }
+#ifdef IGN_SEQ_STAMP
+    IGN_STAMP(t_2);
+    s_epi += t_2 - t_1;
+    ++n_tl;
+#endif
   }  // tile loop
+#ifdef IGN_SEQ_STAMP
+  if constexpr (!SAVE) {
+    IGN_STAMP(t_3);
+    const int gw = blockIdx.x * 4 + wave;
+    if (lane == 0 && gw < 4096) {
+      unsigned long long* o = ign_seq_stamps + 8 * gw;
+      o[0] = s_pro; o[1] = s_mma; o[2] = s_gate; o[3] = s_epi; o[4] = n_tl; o[5] = n_st;
+      o[6] = t_3 - t_begin; o[7] = 1;
+    }
+  }
+#endif
 }
 
 // U (pre-scaled as for pack_gru) -> sigma U as fp16 (hi, lo) A fragments of seq_gru_h16 (layout of

@@ -402,7 +402,10 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
           const auto s16 = __builtin_amdgcn_permlane16_swap(mb, mb, false, false);   // lanes l, l ^ 16
           mb = max(s16[0], s16[1]);
         }
-        const int eSd = mb ? min(60, max(-100, 15 - ((int)(mb >> 23) - 126))) : 0;
+        // Sd's exponent, clamped so that the seed and unseed exponents (eSd + est, -(eSd + est))
+        // stay inside [-126, 126]: normal powers of two whatever du and sigma_t are
+        const int eSd = mb ? min(min(60, 126 - est), max(max(-100, -126 - est), 15 - ((int)(mb >> 23) - 126)))
+                           : min(max(0, -126 - est), 126 - est);
         const float Sd = __int_as_float((127 + eSd) << 23);
         const float seed = __int_as_float((127 + eSd + est) << 23);
         const float unseed = __int_as_float((127 - eSd - est) << 23);

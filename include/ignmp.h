@@ -193,8 +193,11 @@ typedef struct {
   int64_t rows[8];                 /* total rows per entity (first 8 entities) */
 } ign_batch_info_t;
 
-/* Per-kernel timing of the last forward (HIP events on the plan stream, enabled by
- * ign_plan_set_timing).  kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 project, 5 other */
+/* Per-kernel timing (HIP events on the plan stream, enabled by ign_plan_set_timing), accumulated
+ * over every timed launch since the last ign_plan_set_timing / ign_plan_set_timing_kinds.  The
+ * event pairs are resolved lazily: ign_stats waits for the plan's stream and then reads them, so
+ * it blocks, and like every call on a plan it must come from the plan's one host thread.
+ * kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 project, 5 other */
 typedef struct {
   int32_t kinds;
   int64_t launches[8];
@@ -240,6 +243,8 @@ int  ign_plan_set_timing(ign_plan* plan, int32_t enabled);   /* also resets the 
 /* Restrict the event pairs to kernel kinds in the bit mask (bit k = kind k of ign_stats_t);
  * default all.  Each event pair costs a few microseconds of queue time. */
 int  ign_plan_set_timing_kinds(ign_plan* plan, uint32_t kinds);
+/* Run the plan on an external stream from now on.  Waits for the plan's previous stream (its own
+ * or an earlier external one) first, so buffers of destroyed batches are never reused early. */
 int  ign_plan_set_stream(ign_plan* plan, void* hip_stream);
 /* Give the plan's idle cached device blocks (kept for the next batches, IGN_POOL_CACHE_GB) and the
  * process's idle pinned host blocks (IGN_HOST_CACHE_GB) back to the runtime, waiting for the

@@ -5,8 +5,8 @@
 # Output under gpurun_out/prof_<tag>/ ; summarise with profiles/summarize.py.
 set -o pipefail
 TAG=${1:-r01}
-ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu"}
-TRACE_ARGS=${TRACE_ARGS-""}     # the trace pass runs the bench command as given (default: bench.py's defaults)
+ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu --no-edge-cut"}
+XX
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -213,13 +213,25 @@ def test_bench_gpus_n_launches_n_ranks():
     itself (torch.distributed.run as a child process) and print exactly one line, from rank 0,
     with n_gpus N and the edges of every rank's shard summed."""
     r, lines = _bench(["--gpus", "2", "--dry-run", "--topology", "nsfnet", "--graphs", "2", "--steps", "3",
-                       "--warmup", "1"])
+                       "--warmup", "1", "--edge-cut-nodes", "20000"])
     assert r.returncode == 0, r.stderr[-2000:]
     assert len(lines) == 1, r.stdout
     line = lines[0]
     assert line["n_gpus"] == 2 and line["steps"] == 3 and line["scaling"] == "weak"
     _, _, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 4)
     assert line["config"]["edges_per_step_total"] == workloads.edges_per_forward(mi, graphs)
+    # the edge-cut leg (BASELINE configs[4]) in the same ranks: the two partitions' in-edges add up to
+    # the whole graph's, and every halo row a rank reads is sent by exactly one owner
+    ec = line["edge_cut_20000n"]
+    _, _, smi, sgraphs, _ = workloads.make_synthetic_inputs(n_nodes=20000)
+    whole = workloads.edges_per_forward(smi, sgraphs)
+    assert ec["n_ranks"] == 2 and ec["edges_per_step"] == whole == ec["edges_per_step_whole_graph"]
+    assert ec["edges_match_whole_graph"] and ec["halo_rows"]["total"] == ec["send_rows_total"] > 0
+    # --no-edge-cut drops the leg
+    r, lines = _bench(["--gpus", "2", "--dry-run", "--topology", "nsfnet", "--graphs", "2", "--steps", "1",
+                       "--no-edge-cut"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1 and not any(k.startswith("edge_cut") for k in lines[0])
 
 
 def test_bench_single_rank_dry_run_and_world_mismatch():

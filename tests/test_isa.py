@@ -65,5 +65,7 @@ def test_default_ordered_update_keeps_four_waves(asm):
         scratch = re.search(r"ScratchSize: (\d+)", meta)
         if "Lb0E" in name:   # the inference form; the state-saving training form (Lb1E) may use more
             assert vgpr and int(vgpr.group(1)) <= 128, (name, vgpr and vgpr.group(1))
+        else:                # the training forward at H = 32 (138 VGPRs in round 3): keep its 3 waves per SIMD
+            assert vgpr and int(vgpr.group(1)) <= 168, (name, vgpr and vgpr.group(1))
         assert scratch and int(scratch.group(1)) == 0, name
     assert found

@@ -49,7 +49,7 @@ def main():
     os.makedirs(os.path.join(REPO, "gpurun_out", "ab"), exist_ok=True)
     for name in a.libs:
         f = os.path.join(REPO, "gpurun_out", "ab", "pred_%s.npy" % name)
-        env = dict(os.environ, IGN_LIB_PATH=os.path.join(REPO, "ignnition_amd", "ab", "lib_%s.so" % name))
+        env = dict(os.environ, IGN_AB_LIB="1", IGN_LIB_PATH=os.path.join(REPO, "ignnition_amd", "ab", "lib_%s.so" % name))
         subprocess.run([sys.executable, "-c", CHILD % (REPO, a.model, a.topology, a.graphs, a.train, f, f)], env=env, check=True,
                        timeout=300)
         outs[name] = np.load(f)

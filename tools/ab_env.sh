@@ -6,7 +6,7 @@ mkdir -p gpurun_out/ab
 for r in $(seq $REPS); do
   for v in $VALS; do
     f=gpurun_out/ab/$VAR-${v//\//_}-$r
-    env $VAR=$v timeout -k 10 200 python -u bench.py --no-cpu "$@" > $f.json 2> $f.err || { echo "run $v failed"; exit 1; }
+    env $VAR=$v timeout -k 10 200 python -u bench.py --no-cpu --no-edge-cut "$@" > $f.json 2> $f.err || { echo "run $v failed"; exit 1; }
     python - "$VAR=$v" $f.json <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])

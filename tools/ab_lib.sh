@@ -6,7 +6,7 @@ mkdir -p gpurun_out/ab
 for r in $(seq $REPS); do
   for n in $NAMES; do
     f=gpurun_out/ab/lib-$n-$r
-    IGN_LIB_PATH=$PWD/ignnition_amd/ab/lib_$n.so timeout -k 10 200 python -u bench.py --no-cpu "$@" > $f.json 2> $f.err || { echo "run $n failed"; tail -5 $f.err; exit 1; }
+    IGN_AB_LIB=1 IGN_LIB_PATH=$PWD/ignnition_amd/ab/lib_$n.so timeout -k 10 200 python -u bench.py --no-cpu --no-edge-cut "$@" > $f.json 2> $f.err || { echo "run $n failed"; tail -5 $f.err; exit 1; }
     python - "$n" $f.json <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])

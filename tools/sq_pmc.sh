@@ -4,7 +4,7 @@
 # each), then profiles/summarize.py-style per-kernel averages in gpurun_out/pmc_TAG/summary.json.
 set -o pipefail
 TAG=$1; shift
-ARGS=${*:-"--steps 3 --warmup 1 --no-cpu"}
+ARGS=${*:-"--steps 3 --warmup 1 --no-cpu --no-edge-cut"}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -7,7 +7,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for v in $VALS; do
   env $VAR=$v timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE \
-    -d $OUT/$VAR-$v -o x --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu \
+    -d $OUT/$VAR-$v -o x --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-edge-cut \
     > $OUT/$VAR-$v.log 2>&1 || { echo "pass $v failed"; exit 1; }
 done
 python3 - "$VAR" "$VALS" "$PAT" <<'PY'
