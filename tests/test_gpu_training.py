@@ -80,6 +80,28 @@ def test_gradients_synthetic_graph():
     _check(desc, dims, graphs, [np.asarray(l, np.float32) for l in labels], prm)
 
 
+def test_backward_extreme_scales():
+    """The ordered backward's split-fp16 dh = du U^T (train_kernels.hip) scales du per row by Sd and
+    folds Uᵀ's pack scale sigma_t into the seed / unseed powers of two: with a tiny recurrent kernel
+    (sigma_t ~ 2^76) and tiny path gradients (the output layer scaled by 2^-50, so du ~ 2^-50) their
+    exponents must stay normal.  Every gradient tensor within 1e-4 relative of the float64
+    oracle (no absolute slack: all of them are tiny here)."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 1)
+    prm = MPPlan.from_model_info(mi).init_params(3, bias_scale=0.1)
+    prm["path_update/recurrent_kernel"] = prm["path_update/recurrent_kernel"] * np.float32(2.0 ** -60)
+    prm["readout_model_0/Output_layer/kernel"] = prm["readout_model_0/Output_layer/kernel"] * np.float32(2.0 ** -50)
+    eng, b, pred, loss, g, _ = _engine_grads(desc, dims, graphs, labels, prm)
+    _, _, o_g, o_pred = TorchOracle(desc, dims, prm).loss_and_grads(graphs, labels)
+    np.testing.assert_allclose(pred.reshape(-1), o_pred, rtol=1e-4, atol=1e-4)
+    for name, og in o_g.items():
+        assert np.all(np.isfinite(g[name])), name
+        ref = np.linalg.norm(og)
+        if ref == 0:
+            continue
+        err = np.linalg.norm(g[name].astype(np.float64) - og)
+        assert err <= GTOL * ref, "%s: rel err %.3g (|g| %.3g)" % (name, err / ref, ref)
+
+
 def test_adam_step_matches_keras_restatement():
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 2)
     prm = MPPlan.from_model_info(mi).init_params(1, bias_scale=0.1)
