@@ -988,8 +988,10 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
       // windowed aggregation pays where each destination gathers many messages (one lane per
       // destination otherwise walks a long dependent chain): auto threshold 64 per destination
-      const bool window = p->sum_window > 0 ||
-                          (p->sum_window < 0 && ND > 0 && (double)mdst.size() >= 64.0 * (double)ND);
+      // IGN_SUM_WINDOW: -1 auto (the high-degree rule), 0 off, 1 windowed, 2 segmented
+      const bool high = ND > 0 && (double)mdst.size() >= 64.0 * (double)ND;
+      const bool window = p->sum_window == 1 || (p->sum_window < 0 && high);
+      const bool seg = p->sum_window == 2;
       if (window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
@@ -1032,6 +1034,18 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if ((rc = dev_upload(b.get(), &mb.d_win_wg, wg)) || (rc = dev_upload(b.get(), &mb.d_win_dst, wdst)) ||
             (rc = dev_upload(b.get(), &mb.d_win_ptr, wptr)) || (rc = dev_upload(b.get(), &mb.d_win_src, wsrc)) ||
             (rc = dev_upload(b.get(), &mb.d_id_ptr, id_ptr)) || (rc = dev_upload(b.get(), &mb.d_id_src, id_src)) ||
+            (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
+          return rc;
+      } else if (seg && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() && b->halo[mp.src[0].entity] == 0 &&
+                 (DIN == 16 || DIN == 32 || DIN == 64)) {
+        // segmented sum (sum_seg_kernel over the MP's own CSR, one wave per destination), then the
+        // GRU step on x through an identity CSR, as for the windowed sum
+        hvec<int32_t> id_ptr(ND + 1);
+        hvec<uint32_t> id_src(ND);
+        for (int64_t i = 0; i <= ND; ++i) id_ptr[i] = (int32_t)i;
+        for (int64_t i = 0; i < ND; ++i) id_src[i] = (uint32_t)order[i];   // slot 0: the x table
+        mb.sum_seg = true;
+        if ((rc = dev_upload(b.get(), &mb.d_id_ptr, id_ptr)) || (rc = dev_upload(b.get(), &mb.d_id_src, id_src)) ||
             (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
           return rc;
       }
@@ -1310,16 +1324,22 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       if ((rc = attention_weights(p, b, mp, mb, sbases.base, hin, st))) return rc;
       tm.end();
     }
-    if (count > 0 && mb.n_win_wg > 0 && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
-      // windowed aggregation, then the GRU step on x (one message per destination: x itself)
+    if (count > 0 && (mb.n_win_wg > 0 || mb.sum_seg) && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
+      // windowed or segmented aggregation, then the GRU step on x (one message per destination: x
+      // itself)
       const float* srcs = sbases.base[0];
-      SumWinArgs wa{srcs, mb.d_win_wg, mb.d_win_dst, mb.d_win_ptr, mb.d_win_src, mb.d_xsum, mb.n_win_wg};
       SrcBases xb{};
       xb.base[0] = mb.d_xsum;
       SumGruArgs a{hin, hout, xb, mb.d_order, mb.d_id_ptr, mb.d_id_src, p->d_packed + cp.pk_w,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
       tm.begin(K_SUM, mb.flops, mb.bytes, 0, sum_mfma_f32(mb.n_dst, mp.din, cp.H));
-      HIP_TRY(launch_sum_win(wa, mp.din, st));
+      if (mb.sum_seg) {
+        SumSegArgs sa{srcs, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, mb.d_xsum, mb.n_dst};
+        HIP_TRY(launch_sum_seg(sa, mp.din, st));
+      } else {
+        SumWinArgs wa{srcs, mb.d_win_wg, mb.d_win_dst, mb.d_win_ptr, mb.d_win_src, mb.d_xsum, mb.n_win_wg};
+        HIP_TRY(launch_sum_win(wa, mp.din, st));
+      }
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
       tm.end();
     } else if (count > 0) {

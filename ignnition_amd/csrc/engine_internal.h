@@ -174,6 +174,7 @@ struct MPB {
   // windowed sum (SumWinArgs; single-source sums over graph-local rows): the aggregation runs per
   // (graph, destination chunk) from LDS windows, then the GRU step reads x through an identity CSR
   int64_t n_win_wg = 0;
+  bool sum_seg = false;        // segmented sum (sum_seg_kernel) into d_xsum, then the GRU step
   int64_t* d_win_wg = nullptr;
   int32_t* d_win_dst = nullptr;
   int32_t* d_win_ptr = nullptr;

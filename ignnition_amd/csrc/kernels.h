@@ -146,6 +146,17 @@ struct SumWinArgs {
   int64_t n_wg;
 };
 hipError_t launch_sum_win(const SumWinArgs& args, int din, hipStream_t st);
+// High-degree sum (IGN_SUM_WINDOW=2 / auto): one wave per destination, xsum[order[p]] = sum of its
+// messages (single-source MP, slot 0), RS = 64 / (DIN / 4) message rows per load instruction
+struct SumSegArgs {
+  const float* src;        // source states [rows][DIN]
+  const int32_t* order;    // [n_dst] destination rows
+  const int32_t* msg_ptr;  // [n_dst + 1] message range per order position (the sum MP's CSR)
+  const uint32_t* msg_src; // [messages] source codes (slot 0)
+  float* xsum;             // [rows][DIN]
+  int64_t n_dst;
+};
+hipError_t launch_sum_seg(const SumSegArgs& args, int din, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

@@ -537,6 +537,63 @@ __global__ __launch_bounds__(1024) void sum_win_kernel(SumWinArgs a) {
   }
 }
 
+// High-degree sum (Q-size's path -> node MP: ~140 messages per node over few destinations): one
+// wave per destination instead of four lanes, so a destination's messages are gathered RS rows per
+// load instruction (RS = 64 / F4, F4 = DIN / 4 lanes per 16-B row piece), U loads in flight per
+// lane with the next round's codes prefetched, and the long per-destination chains of the lane
+// form become short ones across many waves.  Lane l adds message slots q = l / F4, q + RS, ... in
+// CSR order (columns 4 (l % F4) .. + 3); the RS partial sums are then added pairwise across lanes
+// (xor RS/2 ... 1 in units of F4 lanes): a fixed summation order, bitwise reproducible.
+template <int DIN, int U>
+__global__ __launch_bounds__(256) void sum_seg_kernel(SumSegArgs a) {
+  constexpr int F4 = DIN / 4, RS = 64 / F4;
+  const int lane = threadIdx.x & 63;
+  const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pos >= a.n_dst) return;   // whole waves: no lane of a live wave leaves early
+  const int c = lane % F4, q = lane / F4;
+  const int64_t m0 = a.msg_ptr[pos], m1 = a.msg_ptr[pos + 1];
+  const int64_t last = m1 > m0 ? m1 - 1 : m0;
+  f4 acc = {0, 0, 0, 0};
+  uint32_t cc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = m0 + u * RS + q;
+    cc[u] = m1 > m0 ? a.msg_src[i < last ? i : last] : 0u;
+  }
+  for (int64_t m = m0; m < m1; m += U * RS) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld4(a.src + (int64_t)(cc[u] & IGN_ROW_MASK) * DIN + 4 * c);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // the next round's codes, clamped into the range: no branch
+      const int64_t i = m + (U + u) * RS + q;
+      cc[u] = a.msg_src[i < last ? i : last];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool on = m + u * RS + q < m1;
+      const f4 s = acc + v[u];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = on ? s[k] : acc[k];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= F4; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], o);
+  if (q == 0) st4(a.xsum + (int64_t)a.order[pos] * DIN + 4 * c, acc);
+}
+
+hipError_t launch_sum_seg(const SumSegArgs& args, int din, hipStream_t st) {
+  if (args.n_dst == 0) return hipSuccess;
+  const dim3 grid((unsigned)((args.n_dst + 3) / 4)), block(256);
+  if (din == 32) hipLaunchKernelGGL((sum_seg_kernel<32, 4>), grid, block, 0, st, args);
+  else if (din == 16) hipLaunchKernelGGL((sum_seg_kernel<16, 4>), grid, block, 0, st, args);
+  else if (din == 64) hipLaunchKernelGGL((sum_seg_kernel<64, 4>), grid, block, 0, st, args);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 // Attention softmax weights: one wave per (graph, position) group.
 __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63;

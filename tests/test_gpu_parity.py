@@ -425,12 +425,13 @@ def test_split_bf16_sum_update_is_fp32_accurate(monkeypatch, model):
         assert not np.array_equal(outs["7"], outs["8"])
 
 
-@pytest.mark.parametrize("window", ["0", "1", None])
+@pytest.mark.parametrize("window", ["0", "1", "2", None])
 def test_windowed_sum_matches_oracle(monkeypatch, window):
     """Windowed sum aggregation (per (graph, destination chunk) workgroups, source rows staged in
-    LDS): forced off, forced on, and the default auto rule (on for MPs with >= 64 messages per
-    destination: Q-size's node update on synth50, ~140 per node) all match the float64 oracle.
-    The synth50 topology and batch shape of the Q-size bench, 6 graphs."""
+    LDS), the segmented sum (one wave per destination, IGN_SUM_WINDOW=2), forced off, and the
+    default auto rule (for MPs with >= 64 messages per destination: Q-size's node update on
+    synth50, ~140 per node) all match the float64 oracle.  The synth50 topology and batch shape of
+    the Q-size bench, 6 graphs."""
     if window is None:
         monkeypatch.delenv("IGN_SUM_WINDOW", raising=False)
     else:

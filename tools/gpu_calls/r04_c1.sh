@@ -23,3 +23,11 @@ BENCH_ARGS="--topology geant2 --no-cpu --no-edge-cut --steps 3 --warmup 1" TRACE
 IGN_AB_LIB=1 IGN_LIB_PATH=$PWD/ignnition_amd/ab/lib_stamp.so timeout -k 10 200 python -u tools/probes/seq_stamps.py \
   > $O/seq_stamps.json 2> $O/seq_stamps.err || { tail -20 $O/seq_stamps.err; exit 1; }
 echo "stamps done"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "windowed" \
+  > $O/test_windowed.log 2>&1 || { tail -30 $O/test_windowed.log; exit 1; }
+echo "windowed tests done"
+for w in 1 2 0 1 2; do
+  IGN_SUM_WINDOW=$w timeout -k 10 200 python -u bench.py --model qsize --no-cpu --no-edge-cut --steps 20 \
+    > $O/qsize_win$w.json 2> $O/qsize_win$w.err || { tail -20 $O/qsize_win$w.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('$O/qsize_win$w.json').read().splitlines()[-1]); print('win $w', round(d['ms_per_step'],4), {k: round(v['ms_total']/max(1,v['launches']),4) for k,v in d['roofline']['warmup_kernels'].items()})"
+done
