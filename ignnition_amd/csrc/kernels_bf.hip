@@ -1617,24 +1617,34 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
   const int es2 = hdr[0];
   const float A1 = __int_as_float(hdr[1]), B1 = __int_as_float(hdr[2]);
   const int64_t n_groups = (a.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
+  // the layer-1 input rows of a row group (out-of-range rows read as zeros)
+  f4 xl[RT][KS1][2];
+  auto load_x = [&](int64_t grp) __attribute__((always_inline)) {
+    const int64_t rr = (grp * WAVES + wave) * (16 * RT) + j;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const int64_t r = rr + 16 * t;
+      const bool ok = r < a.n_rows;
+      const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) {
+        xl[t][s][0] = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
+        xl[t][s][1] = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+      }
+    }
+  };
+  load_x(blockIdx.x);
   for (int64_t grp = blockIdx.x; grp < n_groups; grp += (int64_t)gridDim.x) {
   const int64_t r0 = (grp * WAVES + wave) * (16 * RT) + j;
-  // per row tile: the layer-1 input, its max |x|, and the scales derived from it
-  f4 xl[RT][KS1][2];
+  // per row tile: its max |x| and the scales derived from it (xl: loaded during the previous group)
   float mx[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
-    const int64_t r = r0 + 16 * t;
-    const bool ok = r < a.n_rows;
-    const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
     mx[t] = 0.f;
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) {
-      xl[t][s][0] = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
-      xl[t][s][1] = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+    for (int s = 0; s < KS1; ++s)
 #pragma unroll
       for (int q = 0; q < 4; ++q) mx[t] = fmaxf(mx[t], fmaxf(fabsf(xl[t][s][0][q]), fabsf(xl[t][s][1][q])));
-    }
   }
 #pragma unroll
   for (int t = 0; t < RT; ++t) mx[t] = wave_max_nonneg(mx[t]);
@@ -1664,6 +1674,11 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
       xf[t][s][1] = __builtin_bit_cast(h8, w1);
     }
   }
+#ifndef IGN_RO_NOPREFETCH
+  // the next row group's input rows load during this group's two layers (xl is dead from here on);
+  // without it every group opened with an exposed global-load round trip
+  if (grp + gridDim.x < n_groups) load_x(grp + gridDim.x);
+#endif
   __syncthreads();
   // layer 1 (x3 fp16) -> S_t act(z) in accumulator layout -> the layer-2 fp16 B fragments
   h8 hf[RT][KS2][2];
@@ -1779,6 +1794,9 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
       a.y[r] = act_apply(fmaf(yt, cSS[t], b3), a.act3);
     }
   }
+#ifdef IGN_RO_NOPREFETCH
+  if (grp + gridDim.x < n_groups) load_x(grp + gridDim.x);
+#endif
   }  // row groups
 }
 

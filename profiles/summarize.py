@@ -37,6 +37,15 @@ def main(d, out=None):
         for k, v in dur.items():
             res[k]["launches"] = len(v)
             res[k]["avg_ms"] = sum(v) / len(v)
+        # per kernel instance (template arguments included): kinds with several kernels (a sum MP
+        # on the windowed / segmented path, the 32- and 64-wide sum updates) split apart
+        byname = defaultdict(list)
+        for row in csv.DictReader(open(tr[0])):
+            if kind_of(row["Kernel_Name"]) or "sum_win" in row["Kernel_Name"] or "sum_seg" in row["Kernel_Name"]:
+                byname[row["Kernel_Name"].split("(")[0]].append(
+                    (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
+        res["by_name"] = {n: {"launches": len(v), "avg_ms": sum(v) / len(v), "total_ms": sum(v)}
+                          for n, v in sorted(byname.items(), key=lambda kv: -sum(kv[1]))}
     for p in ("fetch", "write", "sq", "sq2", "tcc"):
         fs = glob.glob(os.path.join(d, p, "**", "*counter_collection.csv"), recursive=True)
         if not fs:

@@ -24,7 +24,7 @@ def main(prof_dir, workload, rnd):
     traffic = json.load(open(path)) if os.path.exists(path) else {}
     entry = {}
     for kind, r in res.items():
-        if "hbm_bytes_per_launch" not in r:
+        if kind == "by_name" or "hbm_bytes_per_launch" not in r:
             continue
         entry[kind] = {"hbm_bytes_per_launch": r["hbm_bytes_per_launch"], "fetch_size_kib": r["FETCH_SIZE"],
                        "write_size_kib": r["WRITE_SIZE"], "avg_ms_rocprof": r.get("avg_ms"),
