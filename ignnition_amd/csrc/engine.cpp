@@ -988,10 +988,12 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
       // windowed aggregation pays where each destination gathers many messages (one lane per
       // destination otherwise walks a long dependent chain): auto threshold 64 per destination
-      // IGN_SUM_WINDOW: -1 auto (the high-degree rule), 0 off, 1 windowed, 2 segmented
+      // IGN_SUM_WINDOW: -1 auto (segmented for MPs with >= 64 messages per destination, Q-size's
+      // path -> node update: 4.36-4.39 ms/step against 5.19 windowed and 5.51 lane-walk), 0 off (one
+      // lane group per destination walks its messages), 1 windowed, 2 segmented for every sum MP
       const bool high = ND > 0 && (double)mdst.size() >= 64.0 * (double)ND;
-      const bool window = p->sum_window == 1 || (p->sum_window < 0 && high);
-      const bool seg = p->sum_window == 2;
+      const bool window = p->sum_window == 1;
+      const bool seg = p->sum_window == 2 || (p->sum_window < 0 && high);
       if (window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
@@ -1324,28 +1326,15 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       if ((rc = attention_weights(p, b, mp, mb, sbases.base, hin, st))) return rc;
       tm.end();
     }
-    if (count > 0 && (mb.n_win_wg > 0 || mb.sum_seg) && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM) {
-      // windowed or segmented aggregation, then the GRU step on x (one message per destination: x
-      // itself)
-      const float* srcs = sbases.base[0];
+    if (count > 0) {
+      // windowed or segmented aggregation (sum MPs over all destinations): the sum kernel writes x,
+      // then the GRU step reads it through an identity CSR (one message per destination: x itself)
+      const bool pre = (mb.n_win_wg > 0 || mb.sum_seg) && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM;
       SrcBases xb{};
       xb.base[0] = mb.d_xsum;
-      SumGruArgs a{hin, hout, xb, mb.d_order, mb.d_id_ptr, mb.d_id_src, p->d_packed + cp.pk_w,
-                   p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, mb.n_dst, p->xcd_remap};
-      tm.begin(K_SUM, mb.flops, mb.bytes, 0, sum_mfma_f32(mb.n_dst, mp.din, cp.H));
-      if (mb.sum_seg) {
-        SumSegArgs sa{srcs, mb.d_order, mb.d_msg_ptr, mb.d_msg_src, mb.d_xsum, mb.n_dst};
-        HIP_TRY(launch_sum_seg(sa, mp.din, st));
-      } else {
-        SumWinArgs wa{srcs, mb.d_win_wg, mb.d_win_dst, mb.d_win_ptr, mb.d_win_src, mb.d_xsum, mb.n_win_wg};
-        HIP_TRY(launch_sum_win(wa, mp.din, st));
-      }
-      HIP_TRY(launch_sum_gru(a, mp.din, cp.H, p->sum_variant, st));
-      tm.end();
-    } else if (count > 0) {
-      SumGruArgs a{hin, hout, sbases, mb.d_order + first, mb.d_msg_ptr + first, mb.d_msg_src,
-                   p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count,
-                   p->xcd_remap};
+      SumGruArgs a{hin, hout, pre ? xb : sbases, pre ? mb.d_order : mb.d_order + first,
+                   pre ? mb.d_id_ptr : mb.d_msg_ptr + first, pre ? mb.d_id_src : mb.d_msg_src,
+                   p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count, p->xcd_remap};
       if (mp.aggr == IGN_AGGR_ATTENTION) a.msg_w = mb.d_msg_w;
       int sv = std::min(p->sum_variant, 7);
       if (mp.aggr == IGN_AGGR_SUM && cp.pk_wbf >= 0 && cp.pk_ubf >= 0 && mp.din == cp.din && !mp.feature_concat) {
@@ -1381,6 +1370,13 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       tm.begin(K_SUM, mb.flops * frac, mb.bytes * frac,
                bf ? tiles * (sv == 8 ? 3 : 6) * 3 * (cp.H / 16) * (mp.din / 32 + cp.H / 32) * kMfmaBf16Flops : 0,
                bf ? 0 : sum_mfma_f32(count, mp.din, cp.H));
+      if (pre && mb.sum_seg) {
+        SumSegArgs sa{sbases.base[0], mb.d_order, mb.d_msg_ptr, mb.d_msg_src, mb.d_xsum, mb.n_dst};
+        HIP_TRY(launch_sum_seg(sa, mp.din, st));
+      } else if (pre) {
+        SumWinArgs wa{sbases.base[0], mb.d_win_wg, mb.d_win_dst, mb.d_win_ptr, mb.d_win_src, mb.d_xsum, mb.n_win_wg};
+        HIP_TRY(launch_sum_win(wa, mp.din, st));
+      }
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, sv, st));
       tm.end();
       if (target >= 0) b->proj_ready[target] = 1;
