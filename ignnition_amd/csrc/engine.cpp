@@ -988,9 +988,14 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
       // windowed aggregation pays where each destination gathers many messages (one lane per
       // destination otherwise walks a long dependent chain): auto threshold 64 per destination
-      // IGN_SUM_WINDOW: -1 auto (segmented for MPs with >= 64 messages per destination, Q-size's
-      // path -> node update: 4.36-4.39 ms/step against 5.19 windowed and 5.51 lane-walk), 0 off (one
-      // lane group per destination walks its messages), 1 windowed, 2 segmented for every sum MP
+      // IGN_SUM_WINDOW: -1 auto, 0 off (one lane group per destination walks its messages in the
+      // GRU-step kernel), 1 windowed, 2 segmented for every sum MP.  Auto takes the segmented sum
+      // where the lane walk is latency-bound by long per-destination chains: >= 64 messages per
+      // destination (Q-size's path -> node update, ~144 per node: 4.36-4.39 ms/step against 5.19
+      // windowed and 5.51 lane-walk).  The rule reads the MP's mean in-degree, a property of the
+      // graphs rather than of the batch size, so a graph's predictions stay bitwise the same alone
+      // and in any batch (the two kernels add a destination's messages in different orders).
+      // RouteNet synth50's links (~36 per link) keep the lane walk: 2.755 against 2.838 ms/step.
       const bool high = ND > 0 && (double)mdst.size() >= 64.0 * (double)ND;
       const bool window = p->sum_window == 1;
       const bool seg = p->sum_window == 2 || (p->sum_window < 0 && high);
