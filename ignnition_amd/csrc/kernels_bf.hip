@@ -244,14 +244,6 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   __shared__ float sbias[H];
   __shared__ float sbn[4][H];                // per wave: the candidate's recurrent bias times SS
   __shared__ h8 su[NF * 64];
-#ifndef IGN_SEQ_NO_HPF
-  // inference: the wave's next tile's state rows, landed by LDS-DMA during the current tile
-  // (lane-ordered: lane l's 16 B of row tile t at [wave][t][l]); see the tile loop
-  constexpr bool HPF = !SAVE;
-  __shared__ f4 shn[HPF ? 4 : 1][HPF ? NT : 1][64];
-#else
-  constexpr bool HPF = false;
-#endif
   for (int i = threadIdx.x; i < H; i += blockDim.x) sbias[i] = a.bias[3 * H + i];
   {
     const u4v* src = reinterpret_cast<const u4v*>(a.Uh);
@@ -278,7 +270,6 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
   IGN_STAMP(t_0);
   const unsigned long long t_begin = t_0;
 #endif
-  bool h_landed = false;   // HPF: this tile's state rows are in shn (DMA'd during the previous tile)
   for (; tile < n_tiles; tile += tile_stride) {
 #ifdef IGN_SEQ_STAMP
     IGN_STAMP(t_0);
@@ -291,24 +282,10 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
     float* hsv = nullptr;
     if constexpr (SAVE) hsv = a.hs_save + ((int64_t)hd[2] + pos) * H + 4 * g;
     f4 h[NT];
-    if (HPF && h_landed) {
-#ifndef IGN_SEQ_NO_HPF
-      // the previous tile's epilogue issued its NT state stores after this tile's DMA: everything
-      // older than those stores (the DMA included) has completed at vmcnt(NT)
-      if constexpr (NT == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const f4 v = shn[wave][t][lane];
-        h[t] = valid ? v : f4{0, 0, 0, 0};
-      }
-#endif
-    } else {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const f4 v = ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g);
-        h[t] = valid ? v : f4{0, 0, 0, 0};
-      }
+    for (int t = 0; t < NT; ++t) {
+      const f4 v = ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g);
+      h[t] = valid ? v : f4{0, 0, 0, 0};
     }
     // the first step's projected rows (and the second step's code) are in flight with the state
     f4 x[3][NT];
@@ -448,26 +425,6 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
     IGN_STAMP(t_1);
     s_pro += t_1 - t_0;
 #endif
-    // HPF: the next tile's state rows go to shn by LDS-DMA after the first step (its header hd has
-    // long arrived; issued as asm so that the compiler, which cannot tell shn from su, puts no
-    // vmcnt(0) in front of the steps' fragment reads; the next tile start waits for it explicitly)
-    const bool issue_hpf = HPF && tile + tile_stride < n_tiles;
-    auto dma_next_h = [&]() __attribute__((always_inline)) {
-#ifndef IGN_SEQ_NO_HPF
-      if constexpr (HPF) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const float* src = a.h_in + (int64_t)hd[0] * H + 16 * t + 4 * g;
-          const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-              (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(&shn[wave][t][0]));
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-          asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
-#pragma clang diagnostic pop
-        }
-      }
-#endif
-    };
     for (int t = 0;;) {
 #ifdef IGN_SEQ_STAMP
       IGN_STAMP(t_1);
@@ -480,12 +437,10 @@ __global__ __launch_bounds__(256) void seq_gru_h16_kernel(SeqGruArgs a) {
       s_gate += t_3 - t_2;
       ++n_st;
 #endif
-      if (t == 0 && issue_hpf) dma_next_h();
       if (++t >= Lmax) break;
       load_x(code, x);
       code = codes[t + 1];
     }
-    h_landed = issue_hpf;
 #ifdef IGN_SEQ_STAMP
     IGN_STAMP(t_1);
 #endif
