@@ -1,6 +1,6 @@
 # round 4, call 3: the ordered update's next-tile state prefetch (LDS-DMA, hpf = default tree) against
-# (the HPF change was measured 1-2 % slower per launch, bitwise equal, and reverted: see DESIGN §3b'"'"')
 # the previous tile prologue (nohpf = -DIGN_SEQ_NO_HPF): bitwise check, parity tests, A/B
+# (reverted: bitwise equal, 1-2 % slower per launch; DESIGN.md round-4 notes)
 set -o pipefail
 O=gpurun_out/c3
 mkdir -p $O
