@@ -6,7 +6,9 @@
 set -o pipefail
 TAG=${1:-r01}
 ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu --no-edge-cut"}
-XX
+# the trace pass runs the bench command as given (default: bench.py's defaults without the edge-cut
+# leg, whose 1M-node kernels would otherwise mix into the kernel kinds of the workload profiled)
+TRACE_ARGS=${TRACE_ARGS-"--no-edge-cut"}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
