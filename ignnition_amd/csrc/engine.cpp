@@ -1225,11 +1225,13 @@ static double sum_mfma_f32(int64_t n, int din, int H) {
   return (double)((n + 15) / 16) * 3 * (H / 16) * ((din + H) / 4) * kMfmaF32Flops;
 }
 
-// The ordered MP whose input projection sum MP mi can produce in its epilogue (sum_gru_g32), or -1:
-// the next MP (cyclically, within this forward) that touches mi's destination entity reads it as
-// its only source, with the projection sum_gru_g32 forms (32 -> 3 x 32, no message network, no
-// feature concat), and every row of the entity is one of mi's destinations (no halo rows).
-static int fused_proj_target(const ign_plan* p, const ign_batch* b, int mi) {
+// The ordered MP whose input projection sum MP mi can produce in its epilogue (sum_gru_g32), or -1,
+// and in *slot the source of that MP whose table rows it fills: the next MP (cyclically, within this
+// forward) that touches mi's destination entity reads it as exactly one of its sources, with the
+// projection sum_gru_g32 forms (32 -> 3 x 32, no message network, no feature concat), and every row
+// of the entity is one of mi's destinations (no halo rows).  A multi-source reader (Q-size's
+// {link, node} -> path interleave) gets each source's rows from the sum update of that source.
+static int fused_proj_target(const ign_plan* p, const ign_batch* b, int mi, int* slot) {
   const MPP& mp = p->mps[mi];
   const int e = mp.dst, n = (int)p->mps.size();
   if (mp.sorted || mp.aggr != IGN_AGGR_SUM || mp.feature_concat || mp.din != 32 || p->cells[mp.cell].H != 32 ||
@@ -1241,13 +1243,18 @@ static int fused_proj_target(const ign_plan* p, const ign_batch* b, int mi) {
     const int m2 = (mi + k) % n;
     if (m2 <= mi && b->fuse_last_iter) return -1;   // the next reader runs in no later iteration
     const MPP& q = p->mps[m2];
-    bool reads = false;
-    for (const auto& sd : q.src) reads = reads || sd.entity == e;
+    int reads = 0, s_e = -1;
+    for (size_t s = 0; s < q.src.size(); ++s)
+      if (q.src[s].entity == e) {
+        ++reads;
+        s_e = (int)s;
+      }
     if (!reads && q.dst != e) continue;
     const CellP& qc = p->cells[q.cell];
-    if (m2 == mi || !reads || !q.sorted || q.src.size() != 1 || q.feature_concat || !q.nn[0].layers.empty() ||
+    if (m2 == mi || reads != 1 || !q.sorted || q.src.size() > 8 || q.feature_concat || !q.nn[s_e].layers.empty() ||
         q.din != 32 || qc.H != 32 || qc.pk_wbf < 0)
       return -1;
+    *slot = s_e;
     return m2;
   }
   return -1;
@@ -1283,9 +1290,11 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
   if (mp.sorted) {
     if (part != IGN_PART_ALL) return fail(IGN_ERR_UNSUPPORTED, "interior/boundary split is for sum MPs only");
     const int W3 = 3 * cp.H;
-    const bool projected = b->fuse_ok && b->proj_ready[mi];   // by the previous sum update's epilogue
-    if (projected) b->proj_ready[mi] = 0;
-    for (size_t s = 0; s < mp.src.size() && !projected; ++s) {
+    // sources whose table rows the previous sum updates' epilogues already formed (bit s)
+    const int projected = b->fuse_ok ? b->proj_ready[mi] : 0;
+    b->proj_ready[mi] = 0;
+    for (size_t s = 0; s < mp.src.size(); ++s) {
+      if (projected >> s & 1) continue;
       const int64_t rs = mb.src_rows[s];
       const int sdin_t = mp.feature_concat ? p->ents[mp.src[s].entity].hidden_dim : mp.din;
       tm.begin(K_PROJECT, 2.0 * rs * mp.din * W3, (double)rs * (4.0 * mp.din + 4.0 * W3), 0,
@@ -1356,13 +1365,13 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
         a.conv_act = mp.act;
       }
       // the next ordered MP's input projection in the epilogue (sum_gru_g32 only)
-      int target = -1;
+      int target = -1, tslot = 0;
       if (b->fuse_ok && part == IGN_PART_ALL && sv == 7 && a.Wbf && a.Ubf && mp.aggr == IGN_AGGR_SUM &&
           count == mb.n_dst && mb.n_dst == b->rows[dst])
-        target = fused_proj_target(p, b, mi);
+        target = fused_proj_target(p, b, mi, &tslot);
       if (target >= 0) {
         const CellP& tc = p->cells[p->mps[target].cell];
-        a.proj_out = b->mp[target].d_table + b->mp[target].src_off[0] * 3 * tc.H;
+        a.proj_out = b->mp[target].d_table + b->mp[target].src_off[tslot] * 3 * tc.H;
         a.proj_W = p->d_packed + tc.pk_wbf;
         a.proj_b = p->d_packed + tc.pk_b;
         a.proj_bias_row = b->mp[target].d_table + b->mp[target].zero_row * 3 * tc.H;
@@ -1384,7 +1393,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       }
       HIP_TRY(launch_sum_gru(a, mp.din, cp.H, sv, st));
       tm.end();
-      if (target >= 0) b->proj_ready[target] = 1;
+      if (target >= 0) b->proj_ready[target] |= (char)(1 << tslot);
     }
   }
   if (part != IGN_PART_INTERIOR) b->cur[dst] ^= 1;   // GM:602: the destination state is overwritten

@@ -342,7 +342,11 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
       }
       if (step > 0) load_rows(hbase + (step - 1 < L ? step - 1 : 0), code_next);
+#ifdef IGN_BWD_ABL_NOGA
+      if (act && !FUSE) {   // timing-only ablation: no ga stores (wrong gradients)
+#else
       if (act) {
+#endif
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           float* pa = a.ga + i * (3 * H) + 16 * t + 4 * g;
@@ -366,6 +370,7 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
             R[(H + 16 * t + 4 * g + q) * 16 + wofs] = gr[t][q];
             R[(2 * H + 16 * t + 4 * g + q) * 16 + wofs] = guh[t][q];
           }
+#ifndef IGN_BWD_ABL_NODU   // timing-only ablation: no dU contraction (wrong gradients)
 #pragma unroll
         for (int nt = 0; nt < 3 * NT; ++nt) {
           const f4 bf = ld4(R + nt * 256 + rofs);
@@ -374,6 +379,7 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
 #pragma unroll
             for (int mt = 0; mt < NT; ++mt) dU[mt][nt] = MFMA(af[mt][ks], bf[ks], dU[mt][nt]);
         }
+#endif
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           bsum[t] += guh[t];

@@ -357,7 +357,7 @@ def test_split_fp16_scaling(monkeypatch, hidden, scale):
         assert v <= max(4 * errs["2/1"], 1e-6), errs
 
 
-@pytest.mark.parametrize("order", ["routenet", "sum_first"])
+@pytest.mark.parametrize("order", ["routenet", "sum_first", "qsize"])
 def test_fused_projection_matches_oracle(monkeypatch, order):
     """The 32-wide sum update projects its new states for the next ordered MP that reads them
     (sum_gru_g32's epilogue, IGN_FUSE_PROJ, default on): in RouteNet the link states of
@@ -366,12 +366,16 @@ def test_fused_projection_matches_oracle(monkeypatch, order):
     writes the table's hole row).  Fused and unfused forwards both match the float64 oracle, are
     deterministic, and differ (the switch took effect: the projection runs on split-bf16 instead
     of f32 MFMA)."""
-    desc = model_examples.routenet(hidden=32, iterations=4)
+    kind = "qsize" if order == "qsize" else "routenet"
+    desc = model_examples.qsize(hidden=32, iterations=4) if kind == "qsize" else model_examples.routenet(hidden=32, iterations=4)
     if order == "sum_first":
         desc["message_passing"]["stages"] = desc["message_passing"]["stages"][::-1]
-    _, dims, _ = workloads.model("routenet")
+    _, dims, _ = workloads.model(kind)
     mi = Model_information(copy.deepcopy(desc), dims)
-    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", g) for g in range(3)])
+    # qsize: the {link, node} -> path interleave reads two sources, each projected by its own sum
+    # update's epilogue (path -> link on the lane walk, path -> node on the segmented sum)
+    graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", g, qsize=kind == "qsize")
+                                            for g in range(3)])
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(13, bias_scale=0.2)
     ref = DenseOracle(desc, dims, prm).forward(graphs)
