@@ -1800,257 +1800,6 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
   }  // row groups
 }
 
-// ---------------------------------------------------------------------------------------------
-// Readout variant 4, pipelined (default since round 4): readout_h16's arithmetic, bit for bit, as
-// one instruction stream per SIMD.  readout_h16 runs layer 1 (VALU-heavy: the selu of 256 units per
-// row and the fp16 splits beside 96 MFMAs) and layer 2 (MFMA-heavy: 768 MFMAs, a short epilogue per
-// 16-unit chunk) as phases, and its two co-resident waves per SIMD rarely sit in opposite phases
-// (VALU and MFMA co-executed 9.5 % of MFMA time, DESIGN.md §3b'').  Here one wave per SIMD (512
-// registers) keeps two row groups in flight: while the layer-2 MFMAs of group n run chunk by chunk,
-// layer 1 of group n + 1 runs in the same chunks, one 16-unit tile per chunk (its 6 MFMAs, its 8
-// selu values per lane, the fp16 split every second chunk), and the layer-2 epilogue of chunk v runs
-// inside chunk v + 1.  Every value sees the same operations in the same order as in readout_h16
-// (the epilogue's additions into y keep chunk order), so the outputs are bitwise equal.
-template <int DIN, int ACT, int WAVES, int RT>
-__global__ __launch_bounds__(64 * WAVES, WAVES / 4) void readout_h16p_kernel(Readout3Args a, const h8* __restrict__ W2f) {
-  constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
-  constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
-  constexpr int NTH = 64 * WAVES;
-  constexpr int CHF = KS2 * 2 * 64;              // h8 per W2 chunk of one 16-unit tile (16 KB)
-  constexpr int NCH = U2;
-  constexpr int W1F = U1 * KS1 * 2 * 64;
-  static_assert(CHF % NTH == 0, "chunk layout: whole 1 KB pieces per wave");
-  static_assert(U1 == 2 * KS2 && NCH == U1, "one layer-1 unit tile per layer-2 chunk");
-  constexpr float LAM = 1.0507009873554805f, LA = LAM * 1.6732632423543772f, LOG2E = 1.4426950408889634f;
-  __shared__ h8 sw2[2][CHF];
-  __shared__ h8 sw1[W1F];
-  __shared__ f4 sbias[3 * 64];   // b1 | b2 | w3
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int j = lane & 15, g = lane >> 4;
-  const u4v* W2v = reinterpret_cast<const u4v*>(W2f);
-  const h8* W1f = reinterpret_cast<const h8*>(reinterpret_cast<const float*>(W2f) + N1 * 256 + 64);
-  {
-    const u4v* W1v = reinterpret_cast<const u4v*>(W1f);
-    for (int i = tid; i < W1F; i += NTH) reinterpret_cast<u4v*>(sw1)[i] = W1v[i];
-  }
-  const int es1 = reinterpret_cast<const int*>(W1f + W1F)[0];
-  for (int i = tid; i < CHF; i += NTH) reinterpret_cast<u4v*>(sw2[0])[i] = W2v[i];
-  for (int i = tid; i < 3 * 64; i += NTH) sbias[i] = ld4((i < 64 ? a.b1 : i < 128 ? a.b2 : a.w3) + 4 * (i & 63));
-  const int* hdr = reinterpret_cast<const int*>(W2f + (int64_t)NCH * CHF);
-  const int es2 = hdr[0];
-  const float A1 = __int_as_float(hdr[1]), B1 = __int_as_float(hdr[2]);
-  const int64_t n_groups = (a.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
-  const int64_t stride = gridDim.x;
-
-  // ---- per row group: input rows, scales, layer-1 B fragments (as readout_h16) ----
-  f4 xl[RT][KS1][2];
-  auto load_x = [&](int64_t grp) __attribute__((always_inline)) {
-    const int64_t rr = (grp * WAVES + wave) * (16 * RT) + j;
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const int64_t r = rr + 16 * t;
-      const bool ok = grp < n_groups && r < a.n_rows;
-      const float* xr = a.x + (ok ? r : 0) * (int64_t)a.x_stride;
-#pragma unroll
-      for (int s = 0; s < KS1; ++s) {
-        xl[t][s][0] = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
-        xl[t][s][1] = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
-      }
-    }
-  };
-  struct Sc { float S[RT], S1S[RT], c1[RT], SS[RT], cSS[RT]; };
-  h8 xf[RT][KS1][2];
-  auto prepare = [&](Sc& sc) __attribute__((always_inline)) {   // scales and xf from xl
-    float mx[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      mx[t] = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS1; ++s)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) mx[t] = fmaxf(mx[t], fmaxf(fabsf(xl[t][s][0][q]), fabsf(xl[t][s][1][q])));
-    }
-#pragma unroll
-    for (int t = 0; t < RT; ++t) mx[t] = wave_max_nonneg(mx[t]);
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const float bnd = fmaf(fmaf(A1, mx[t], B1), 1.0508f, 1.7582f);
-      const int E = (__builtin_amdgcn_readfirstlane(__float_as_int(bnd)) >> 23) - 126;
-      const int eS = 15 - E;
-      sc.S[t] = __int_as_float((127 + eS) << 23);
-      sc.SS[t] = __int_as_float((127 + eS + es2) << 23);
-      sc.cSS[t] = __int_as_float((127 - eS - es2) << 23);
-      const int E1 = (__builtin_amdgcn_readfirstlane(__float_as_int(fmaxf(mx[t], 1e-18f))) >> 23) - 126;
-      const int eS1 = min(60, max(-60, 15 - E1));
-      const float S1 = __int_as_float((127 + eS1) << 23);
-      sc.S1S[t] = __int_as_float((127 + eS1 + es1) << 23);
-      sc.c1[t] = __int_as_float((127 - eS1 - es1) << 23);
-#pragma unroll
-      for (int s = 0; s < KS1; ++s) {
-        const f4 lo = xl[t][s][0] * S1, hi = xl[t][s][1] * S1;
-        const hpair p0 = split2h(lo[0], lo[1]), p1 = split2h(lo[2], lo[3]);
-        const hpair p2 = split2h(hi[0], hi[1]), p3 = split2h(hi[2], hi[3]);
-        const u4v w0 = {p0.hi, p1.hi, p2.hi, p3.hi}, w1 = {p0.lo, p1.lo, p2.lo, p3.lo};
-        xf[t][s][0] = __builtin_bit_cast(h8, w0);
-        xf[t][s][1] = __builtin_bit_cast(h8, w1);
-      }
-    }
-  };
-  // layer 1, unit tile u, in two parts: the MFMAs (into acc1), then the activations and their fp16
-  // split into the layer-2 B fragments hfn[.][u / 2] (tile u fills dwords 2 (u & 1), + 1: the split
-  // pairs never cross the two tiles of a pair)
-  f4 acc1[RT];
-  u4v hfc[RT][KS2][2], hfn[RT][KS2][2];   // layer-2 B fragments (fp16 pieces): current, next group
-  auto l1_mfma = [&](int u, const Sc& sc) __attribute__((always_inline)) {
-    const f4 bias = sbias[4 * u + g];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) acc1[t] = bias * sc.S1S[t];
-#pragma unroll
-    for (int s = 0; s < KS1; ++s) {
-      const h8 w1 = sw1[((u * KS1 + s) * 2 + 1) * 64 + lane];
-      const h8 w0 = sw1[((u * KS1 + s) * 2 + 0) * 64 + lane];
-#pragma unroll
-      for (int t = 0; t < RT; ++t) acc1[t] = MFMA_H(w1, xf[t][s][0], acc1[t]);
-#pragma unroll
-      for (int t = 0; t < RT; ++t) acc1[t] = MFMA_H(w0, xf[t][s][1], acc1[t]);
-#pragma unroll
-      for (int t = 0; t < RT; ++t) acc1[t] = MFMA_H(w0, xf[t][s][0], acc1[t]);
-    }
-  };
-  auto l1_act = [&](int u, const Sc& sc, int t) __attribute__((always_inline)) {
-    const int half = u & 1, s2 = u >> 1;
-    const float k = (ACT == IGN_K_ACT_SELU ? LAM : 1.0f) * sc.S[t] * sc.c1[t];
-    float vv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      vv[q] = act_scaled<ACT>(acc1[t][q], sc.c1[t], k, sc.c1[t] * LOG2E, LA * sc.S[t], sc.S[t]);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const hpair p = split2h(vv[2 * q], vv[2 * q + 1]);
-      hfn[t][s2][0][2 * half + q] = p.hi;
-      hfn[t][s2][1][2 * half + q] = p.lo;
-    }
-  };
-
-  int64_t grp = blockIdx.x;
-  Sc scc, scn;
-  load_x(grp);
-  prepare(scc);
-  __syncthreads();   // sw1, sw2[0], sbias staged
-  // the first group's layer 1, unpipelined
-#pragma unroll
-  for (int u = 0; u < U1; ++u) {
-    l1_mfma(u, scc);
-#pragma unroll
-    for (int t = 0; t < RT; ++t) l1_act(u, scc, t);
-  }
-#pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int s = 0; s < KS2; ++s) {
-      hfc[t][s][0] = hfn[t][s][0];
-      hfc[t][s][1] = hfn[t][s][1];
-    }
-  load_x(grp + stride);
-  for (; grp < n_groups; grp += stride) {
-    const int64_t r0 = (grp * WAVES + wave) * (16 * RT) + j;
-    // the next group's scales and layer-1 input fragments (its rows loaded during this wave's
-    // previous group); then the rows of the group after it start loading.  A wave past the last
-    // group computes layer 1 on zero rows (its results are never stored).
-    prepare(scn);
-    load_x(grp + 2 * stride);
-    float y[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) y[t] = 0.f;
-    f4 accp[RT];   // the previous chunk's layer-2 accumulators (epilogue deferred by one chunk)
-    auto epilogue = [&](int v) __attribute__((always_inline)) {
-      const f4 w3 = sbias[128 + 4 * v + g];
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          y[t] += w3[q] * act_scaled<ACT>(accp[t][q], scc.cSS[t], ACT == IGN_K_ACT_SELU ? LAM : 1.0f,
-                                          scc.cSS[t] * LOG2E, LA * scc.SS[t], scc.SS[t]);
-    };
-#pragma unroll
-    for (int v = 0; v < NCH; ++v) {
-      const int cur = v & 1;
-      const int nv = (v + 1) % NCH;
-      // chunk v+1 of W2 by LDS-DMA into the other buffer (readout_bf_kernel: why asm, and M0)
-#pragma unroll
-      for (int k = 0; k < CHF / NTH; ++k) {
-        const int piece = wave + WAVES * k;
-        const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(sw2[cur ^ 1] + piece * 64));
-        const u4v* src = W2v + (int64_t)nv * CHF + piece * 64 + lane;
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
-#pragma clang diagnostic pop
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      int lofs = lane;
-      asm volatile("" : "+v"(lofs));
-      const h8* wbase = sw2[cur] + lofs;
-      const f4 b = sbias[64 + 4 * v + g];
-      f4 acc[RT];
-#pragma unroll
-      for (int t = 0; t < RT; ++t) acc[t] = b * scc.SS[t];
-      h8 wn[2];
-#pragma unroll
-      for (int pu = 0; pu < 2; ++pu) wn[pu] = wbase[pu * 64];
-#pragma unroll
-      for (int s = 0; s < KS2; ++s) {
-        h8 w[2];
-#pragma unroll
-        for (int pu = 0; pu < 2; ++pu) w[pu] = wn[pu];
-        if (s + 1 < KS2) {
-#pragma unroll
-          for (int pu = 0; pu < 2; ++pu) wn[pu] = wbase[((s + 1) * 2 + pu) * 64];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // W2 lo x a hi, W2 hi x {a lo, a hi}
-#pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w[1], __builtin_bit_cast(h8, hfc[t][s][0]), acc[t]);
-#pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w[0], __builtin_bit_cast(h8, hfc[t][s][1]), acc[t]);
-#pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t] = MFMA_H(w[0], __builtin_bit_cast(h8, hfc[t][s][0]), acc[t]);
-        // beside them: the next group's layer-1 tile v, the previous chunk's epilogue
-        if (s == 0) l1_mfma(v, scn);
-        if (s == 2 && v > 0) epilogue(v - 1);
-        if (s >= 4 && s - 4 < RT) l1_act(v, scn, s - 4);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int t = 0; t < RT; ++t) accp[t] = acc[t];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed (for every wave: barrier)
-      __syncthreads();
-    }
-    epilogue(NCH - 1);
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      float yt = y[t];
-      yt += __shfl_xor(yt, 16);
-      yt += __shfl_xor(yt, 32);
-      const int64_t r = r0 + 16 * t;
-      if (g == 0 && r < a.n_rows) {
-        const float b3 = a.b3 ? a.b3[0] : 0.f;
-        a.y[r] = act_apply(fmaf(yt, scc.cSS[t], b3), a.act3);
-      }
-    }
-    // the next group becomes the current one
-    scc = scn;
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int s = 0; s < KS2; ++s) {
-        hfc[t][s][0] = hfn[t][s][0];
-        hfc[t][s][1] = hfn[t][s][1];
-      }
-  }  // row groups
-}
-
 __device__ __forceinline__ float act_grad_out(float a, int act) {   // act' through the output a
   switch (act) {
     case IGN_K_ACT_RELU: return a > 0.f ? 1.f : 0.f;
@@ -2274,21 +2023,6 @@ static void readout_h16_launch(const Readout3Args& args, const h8* w, hipStream_
 #define IGN_READOUT_WAVES 4
 #endif
   constexpr int WAVES = IGN_READOUT_WAVES, RT = 2;   // RT = 1 (8 or 4 waves) measured slower: 0.59 / 0.69 ms
-#ifndef IGN_RO_NOPIPE
-  {   // the pipelined form: two row groups in flight per wave
-#ifndef IGN_RO_PWAVES
-#define IGN_RO_PWAVES 8
-#endif
-#ifndef IGN_RO_PRT
-#define IGN_RO_PRT 1
-#endif
-    constexpr int PW = IGN_RO_PWAVES, PRT = IGN_RO_PRT;
-    auto kp = readout_h16p_kernel<DIN, ACT, PW, PRT>;
-    const int64_t groups = (args.n_rows + 16 * PRT * PW - 1) / (16 * PRT * PW);
-    hipLaunchKernelGGL(kp, dim3((unsigned)persistent_grid(kp, groups, 64 * PW)), dim3(64 * PW), 0, st, args, w);
-    return;
-  }
-#endif
   auto k = readout_h16_kernel<DIN, ACT, WAVES, RT>;
   const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
   hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w);
