@@ -546,7 +546,7 @@ def main():
         step()
     barrier_sync()
     warm = stats_all()
-    dom = max(("seq_gru", "sum_gru", "readout"), key=lambda k: warm[k]["ms"])
+    dom = max(("seq_gru", "sum_gru", "readout", "mp_resident"), key=lambda k: warm[k]["ms"])
     set_timing(not args.no_timing, kinds=[dom])
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -643,6 +643,8 @@ def main():
                    "sum_update": (H16 % 3 if plan.hidden[0] == 64 and sum_v == 8 else BF % 6)
                    if plan.hidden[0] in (32, 64) and sum_v in (7, 8) else "f32 MFMA",
                    "projection": "f32 MFMA"}
+    contraction["mp_resident"] = "ordered update %s; sum update %s" % (contraction["ordered_update_hU"],
+                                                                     contraction["sum_update"])
     if roof is not None and isolated and isolated["launches"]:
         il = isolated["launches"]
         iavg = isolated["ms"] / il / 1e3
@@ -656,8 +658,8 @@ def main():
                             "achieved": round(iach, 3), "frac": round(iach / roof["peak"], 4),
                             "mfma_pipe": pipe(isolated)}
     if roof is not None:
-        roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout"}.get(dom,
-                                                                                              "sum_update")]
+        roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout",
+                                           "mp_resident": "mp_resident"}.get(dom, "sum_update")]
     line = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,

@@ -80,7 +80,7 @@ class Stats(C.Structure):
                 ("bytes", C.c_double * 8), ("mfma_bf16", C.c_double * 8), ("mfma_f32", C.c_double * 8)]
 
 
-KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "project", "other"]
+KERNEL_KINDS = ["init_state", "seq_gru", "sum_gru", "readout", "project", "other", "mp_resident"]
 
 MSG_INPUT = {"hs_source": 0, "hs_dest": 1, "edge_params": 2}
 AGGR = {"sum": 0, "ordered": 1, "interleave": 2, "concat": 3, "attention": 4, "convolution": 5}

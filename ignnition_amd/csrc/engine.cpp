@@ -218,6 +218,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 || atoi(v) == 8 ? atoi(v) : 3;
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
+  if (const char* v = getenv("IGN_RESIDENT")) p->resident = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_H16")) p->train_dense_h16 = atoi(v) != 0;
@@ -562,6 +563,99 @@ int ign_plan_set_stream(ign_plan* p, void* s) {
   p->own_stream = false;
   p->external_stream = true;
   p->stream = static_cast<hipStream_t>(s);
+  return IGN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The graph-resident forward (resident.hip): a RouteNet-shaped model -- one ordered MP (src -> dst,
+// plain, single source) and one sum MP back (dst -> src), H = DIN = 32, the default split kernels --
+// on graphs whose states and projected table fit one workgroup's LDS.  Otherwise the batched path.
+static bool resident_plan_ok(const ign_plan* p) {
+  if (!p->resident || p->ents.size() != 2 || p->mps.size() != 2 || !p->fuse_proj) return false;
+  const MPP& a = p->mps[0];
+  const MPP& s = p->mps[1];
+  if (!a.sorted || a.aggr != IGN_AGGR_ORDERED || a.src.size() != 1 || s.sorted || s.aggr != IGN_AGGR_SUM ||
+      s.src.size() != 1 || a.feature_concat || s.feature_concat || !a.nn[0].layers.empty() || !s.nn[0].layers.empty())
+    return false;
+  const int link = a.src[0].entity, path = a.dst;
+  if (link == path || s.src[0].entity != path || s.dst != link) return false;
+  const CellP& ca = p->cells[a.cell];
+  const CellP& cs = p->cells[s.cell];
+  if (ca.H != 32 || cs.H != 32 || a.din != 32 || s.din != 32 || ca.pk_uh < 0 || ca.pk_wbf < 0 || cs.pk_wbf < 0 ||
+      cs.pk_ubf < 0 || p->seq_variant != 6 || p->sum_variant < 7)
+    return false;
+  return p->ents[path].feature_total <= 32 && p->ents[link].feature_total <= 32;
+}
+
+static size_t resident_lds_bytes(int64_t paths, int64_t links) {
+  return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
+         sizeof(float);
+}
+
+// per-graph tables of the resident forward; leaves b->resident false where it does not apply
+static int resident_batch(ign_plan* p, ign_batch* b) {
+  if (!resident_plan_ok(p)) return IGN_OK;
+  const MPP& a = p->mps[0];
+  const int link = a.src[0].entity, path = a.dst;
+  const MPB& ma = b->mp[0];
+  const MPB& ms = b->mp[1];
+  if (b->halo[link] || b->halo[path] || ma.n_multi || ma.src_off.size() != 1 || ma.src_off[0] != 0) return IGN_OK;
+  const int G = b->G;
+  const auto& po = b->row_off[path];
+  const auto& lo = b->row_off[link];
+  size_t lds = 0;
+  for (int g = 0; g < G; ++g) lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], lo[g + 1] - lo[g]));
+  if (lds > kResidentMaxDynLds) return IGN_OK;
+  // the graph of every row (rows are graph-contiguous)
+  auto graph_of = [&](const std::vector<int64_t>& off, int64_t r) {
+    return (int)(std::upper_bound(off.begin(), off.end(), r) - off.begin()) - 1;
+  };
+  // ordered MP: each graph's positions in the batch's length-sorted order (stable, so still sorted
+  // by length, descending), padded to whole tiles; sum MP: each graph's order positions
+  std::vector<std::vector<int32_t>> pp(G), lp(G);
+  const int64_t ND = (int64_t)ma.h_order.size();
+  for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
+  for (size_t i = 0; i < ms.h_order.size(); ++i) lp[graph_of(lo, ms.h_order[i])].push_back((int32_t)i);
+  hvec<int32_t> ptile_off(G + 1, 0), lpos_off(G + 1, 0), hdr, lpos;
+  const int64_t steps = ma.n_steps;
+  for (int g = 0; g < G; ++g) {
+    const int64_t n = (int64_t)pp[g].size(), np = (n + 15) / 16 * 16;
+    for (int64_t k = 0; k < np; ++k) {
+      if (k < n) {
+        const int64_t i = pp[g][k];
+        hdr.push_back(ma.h_order[i]);
+        hdr.push_back(ma.h_len[i]);
+        hdr.push_back(ma.h_step_ptr[i]);
+        hdr.push_back((int32_t)ma.h_step_code[ma.h_step_ptr[i]]);
+      } else {   // padding: length 0, codes of the hole row
+        hdr.push_back(0);
+        hdr.push_back(0);
+        hdr.push_back((int32_t)steps);
+        hdr.push_back((int32_t)ma.h_step_code[steps]);
+      }
+    }
+    ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
+    lpos.insert(lpos.end(), lp[g].begin(), lp[g].end());
+    lpos_off[g + 1] = (int32_t)lpos.size();
+  }
+  if (lpos.empty()) lpos.push_back(0);
+  std::vector<int64_t> pov(po.begin(), po.end()), lov(lo.begin(), lo.end());
+  int rc;
+  if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_link_off, lov)) ||
+      (rc = dev_upload(b, &b->d_res_ptile_off, ptile_off)) || (rc = dev_upload(b, &b->d_res_hdr, hdr)) ||
+      (rc = dev_upload(b, &b->d_res_lpos_off, lpos_off)) || (rc = dev_upload(b, &b->d_res_lpos, lpos)))
+    return rc;
+  b->res_lds = lds;
+  // one launch reads the features, the tile headers, the step codes (T times, from L2 after the
+  // first), the sum MP's CSR and positions and writes the final states once: the HBM floor
+  const int64_t P = b->rows[path], L = b->rows[link];
+  b->res_bytes = 4.0 * (P * p->ents[path].feature_total + L * p->ents[link].feature_total) + 4.0 * hdr.size() +
+                 4.0 * (double)ma.h_step_code.size() + 4.0 * (ms.h_msg_ptr.size() + ms.h_msg_src.size()) +
+                 8.0 * (double)lpos.size() + 4.0 * 32 * (P + L);
+  // the MPs' FLOPs per iteration (the sum update's aggregation and GRU step, the ordered update's
+  // h.U and gates) plus the ordered MP's input projection of every link state
+  b->res_flops = p->T * (ma.flops + ms.flops + 2.0 * L * 32 * 96);
+  b->resident = true;
   return IGN_OK;
 }
 
@@ -1070,6 +1164,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     b->mp.push_back(std::move(mb));
   }
 
+  if ((rc = resident_batch(p, b.get()))) return rc;
   // readout buffers
   if ((rc = readout_batch(p, b.get(), d))) return rc;
   const int64_t P = space_rows(p, b.get(), p->ro_t[p->ro_in[0]]);
@@ -1513,7 +1608,57 @@ int copy_out(ign_plan* p, ign_batch* b, float* pred_out) {
   return IGN_OK;
 }
 
+// the whole MP loop of a resident batch in one launch; the final states land in
+// buffer 0 of both entities
+static int resident_forward(ign_plan* p, ign_batch* b) {
+  const MPP& a = p->mps[0];
+  const MPP& s = p->mps[1];
+  const int link = a.src[0].entity, path = a.dst;
+  const MPB& ma = b->mp[0];
+  const MPB& ms = b->mp[1];
+  const CellP& ca = p->cells[a.cell];
+  const CellP& cs = p->cells[s.cell];
+  ResidentArgs r{};
+  r.path_off = b->d_res_path_off;
+  r.link_off = b->d_res_link_off;
+  r.ptile_off = b->d_res_ptile_off;
+  r.hdr = b->d_res_hdr;
+  r.step_code = ma.d_step_code;
+  r.lpos_off = b->d_res_lpos_off;
+  r.lpos = b->d_res_lpos;
+  r.l_order = ms.d_order;
+  r.msg_ptr = ms.d_msg_ptr;
+  r.msg_src = ms.d_msg_src;
+  r.path_feat = b->d_feat[path];
+  r.path_F = p->ents[path].feature_total;
+  r.link_feat = b->d_feat[link];
+  r.link_F = p->ents[link].feature_total;
+  r.path_state = b->d_state[0][path];
+  r.link_state = b->d_state[0][link];
+  r.Uh = p->d_packed + ca.pk_uh;
+  r.seq_bias = p->d_packed + ca.pk_b;
+  r.sWbf = p->d_packed + cs.pk_wbf;
+  r.sUbf = p->d_packed + cs.pk_ubf;
+  r.sum_bias = p->d_packed + cs.pk_b;
+  r.proj_W = p->d_packed + ca.pk_wbf;
+  r.proj_b = p->d_packed + ca.pk_b;
+  r.proj_Wf = p->d_packed + ca.pk_w;
+  r.T = p->T;
+  r.zero_row = ma.zero_row;
+  Timer tm{p};
+  tm.begin(K_RESIDENT, b->res_flops, b->res_bytes);
+  HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, p->stream));
+  tm.end();
+  b->cur[path] = 0;
+  b->cur[link] = 0;
+  return IGN_OK;
+}
+
 int forward_body(ign_plan* p, ign_batch* b) {
+  if (b->resident) {
+    const int rc = resident_forward(p, b);
+    return rc ? rc : readout(p, b);
+  }
   int rc = ign_forward_begin(p, b);
   if (rc) return rc;
   b->proj_ready.assign(p->mps.size(), 0);

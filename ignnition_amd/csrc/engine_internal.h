@@ -72,7 +72,7 @@ using hvec = std::vector<T, HostAlloc<T>>;
     if (_e != hipSuccess) return fail(IGN_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e));    \
   } while (0)
 
-enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_PROJECT = 4, K_OTHER = 5, K_KINDS = 6 };
+enum { K_INIT = 0, K_SEQ = 1, K_SUM = 2, K_READOUT = 3, K_PROJECT = 4, K_OTHER = 5, K_RESIDENT = 6, K_KINDS = 7 };
 
 // per timed launch: algorithmic FLOPs / bytes and the FLOPs its MFMAs execute (bf16 / f32 pipe)
 struct EvCost {
@@ -263,6 +263,7 @@ struct ign_plan {
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
   bool train_seq_h16 = true;      // training forward's ordered update on split-fp16 (IGN_TRAIN_SEQ_H16=0: bf16)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
+  bool resident = true;           // graph-resident forward for small RouteNet-shaped graphs (IGN_RESIDENT=0: off)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
                                   // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
                                   // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);
@@ -305,6 +306,17 @@ struct ign_batch {
   // forward_body only: a sum update may project its new states for the next ordered MP that reads
   // them (fused_proj_target); proj_ready[m'] tells m' that its table is already filled
   bool fuse_ok = false, fuse_last_iter = false;
+  // the graph-resident forward (resident.hip, plan->resident): per-graph offsets, the ordered MP's
+  // per-graph tile headers, the sum MP's per-graph order positions; dynamic LDS of the largest graph
+  bool resident = false;
+  size_t res_lds = 0;
+  double res_bytes = 0, res_flops = 0;   // per launch: HBM bytes it must move, FLOPs it executes
+  int64_t* d_res_path_off = nullptr;
+  int64_t* d_res_link_off = nullptr;
+  int32_t* d_res_ptile_off = nullptr;
+  int32_t* d_res_hdr = nullptr;
+  int32_t* d_res_lpos_off = nullptr;
+  int32_t* d_res_lpos = nullptr;
   std::vector<char> proj_ready;
   float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
   std::vector<float*> d_ro_tmp;                 // generic readout intermediates

@@ -157,6 +157,42 @@ struct SumSegArgs {
   int64_t n_dst;
 };
 hipError_t launch_sum_seg(const SumSegArgs& args, int din, hipStream_t st);
+
+// Graph-resident forward of a RouteNet-shaped model (resident.hip): one workgroup per graph runs the
+// T iterations of one ordered MP (src -> dst, single source) and one sum MP (dst -> src), H = DIN =
+// 32, with the graph's states and projected table in LDS; writes the final states of both entities.
+constexpr int kResidentWaves = 16;
+constexpr int kResidentStateStride = 36;    // LDS floats per 32-wide state row
+constexpr int kResidentTableStride = 100;   // LDS floats per 96-wide projected row
+constexpr size_t kResidentMaxDynLds = 144 * 1024;
+struct ResidentArgs {
+  const int64_t* path_off;    // [G + 1] rows of the ordered MP's destination entity ("paths") per graph
+  const int64_t* link_off;    // [G + 1] rows of its source entity ("links") per graph
+  const int32_t* ptile_off;   // [G + 1] first header of graph g (multiples of 16)
+  const int32_t* hdr;         // [headers][4] per graph, its paths by length descending, padded to whole
+                              // tiles: {path row, final_len (0: padding), step_ptr, first step's code}
+  const uint32_t* step_code;  // the ordered MP's step codes (global table rows; zero_row = hole)
+  const int32_t* lpos_off;    // [G + 1]
+  const int32_t* lpos;        // per graph, the sum MP's order positions of its links
+  const int32_t* l_order;     // the sum MP's order: position -> link row
+  const int32_t* msg_ptr;     // the sum MP's CSR over order positions
+  const uint32_t* msg_src;    // its message codes (slot 0 | path row)
+  const float* path_feat; int path_F;
+  const float* link_feat; int link_F;
+  float* path_state;          // [rows][32] final states
+  float* link_state;
+  const void* Uh;             // the ordered MP's U, scaled fp16 pieces (pack_u_f16) + exponent
+  const float* seq_bias;      // the ordered MP's combined biases [4][H]
+  const void* sWbf;           // the sum MP's W / U split-bf16 pieces, combined biases
+  const void* sUbf;
+  const float* sum_bias;
+  const void* proj_W;         // the ordered MP's input kernel as split-bf16 pieces, its biases
+  const float* proj_b;
+  const float* proj_Wf;       // ... and as project_kernel's f32 fragments (the iteration-0 projection)
+  int T;
+  int64_t zero_row;           // the ordered MP's hole row (= the source entity's rows)
+};
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

@@ -233,7 +233,9 @@ def test_synthetic_graph_h64_matches_oracle():
 
 def test_hip_graph_replay_matches_direct(monkeypatch):
     """The captured hipGraph replays the same launches: bitwise-equal predictions.  Timed
-    forwards launch directly, and the per-kernel event timing covers every launch."""
+    forwards launch directly, and the per-kernel event timing covers every launch (the batched
+    launches: the resident forward is off here, test_resident_forward_is_the_batched_forward)."""
+    monkeypatch.setenv("IGN_RESIDENT", "0")
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "geant2", 3)
     plan = MPPlan.from_model_info(mi)
     prm = plan.init_params(1, bias_scale=0.1)
@@ -444,6 +446,74 @@ def test_windowed_sum_matches_oracle(monkeypatch, window):
     out, ref, b, _ = _run(desc, dims, graphs, seed=3, bias=0.1)
     _close(out, ref)
     np.testing.assert_array_equal(out, b.forward())
+
+
+@pytest.mark.parametrize("topo,n", [("geant2", 3), ("nsfnet", 2), ("mixed", 4)])
+def test_resident_forward_is_the_batched_forward(monkeypatch, topo, n):
+    """The graph-resident forward (resident.hip: one workgroup per graph for all T iterations,
+    states and the projected table in LDS; the default for RouteNet-shaped models on graphs that
+    fit) computes each row with the batched kernels' arithmetic: predictions and final states
+    bitwise equal to the batched launches (IGN_RESIDENT=0), both within the parity tolerance of
+    the float64 oracle; one launch per forward (plus the readout), replayed bitwise from the
+    captured hipGraph."""
+    if topo == "mixed":
+        desc, dims, mi = workloads.model("routenet")
+        graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet" if g % 2 else "geant2", 40 + g)
+                                                for g in range(n)])
+    else:
+        desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", topo, n)
+    plan = MPPlan.from_model_info(mi)
+    prm = plan.init_params(5, bias_scale=0.1)
+    ref = DenseOracle(desc, dims, prm).forward(graphs)
+    outs, states = {}, {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("IGN_RESIDENT", v)
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        b = Batch(eng, graphs)
+        eng.set_timing(True)
+        out = b.forward().reshape(-1)
+        st = eng.stats()
+        eng.set_timing(False)
+        np.testing.assert_array_equal(out, b.forward().reshape(-1))   # graph capture + replay
+        if v == "1":
+            assert st["mp_resident"]["launches"] == 1 and st["seq_gru"]["launches"] == 0, st
+            assert st["sum_gru"]["launches"] == 0 and st["project"]["launches"] == 0, st
+        else:
+            assert st["mp_resident"]["launches"] == 0 and st["seq_gru"]["launches"] == plan.iterations, st
+        outs[v] = out
+        states[v] = {e: b.state(e) for e in ("path", "link")}
+        b.close()
+        eng.close()
+        _close(out, ref)
+    np.testing.assert_array_equal(outs["1"], outs["0"])
+    for e in ("path", "link"):
+        np.testing.assert_array_equal(states["1"][e], states["0"][e])
+
+
+def test_resident_forward_batch_invariance():
+    """A graph's predictions are the same bits alone, in a resident batch, and in a batch that
+    takes the batched path (a synth50 graph is too large for one workgroup's LDS)."""
+    desc, dims, mi = workloads.model("routenet")
+    small = [synthetic.routenet_sample("geant2", 60 + g) for g in range(3)]
+    big = synthetic.routenet_sample("synth50", 70)
+    graphs, _ = workloads.graph_inputs(mi, small + [big])
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(6, bias_scale=0.1))
+    eng.set_timing(True)
+    def launches():   # the stats accumulate over the engine's life
+        st = eng.stats()
+        return st["mp_resident"]["launches"], st["seq_gru"]["launches"]
+
+    alone = [Batch(eng, [g]).forward().reshape(-1) for g in graphs[:3]]
+    assert launches() == (3, 0)
+    res = Batch(eng, graphs[:3]).forward().reshape(-1)
+    assert launches() == (4, 0)
+    mixed = Batch(eng, graphs).forward().reshape(-1)
+    assert launches() == (4, plan.iterations)
+    np.testing.assert_array_equal(res, np.concatenate(alone))
+    np.testing.assert_array_equal(mixed[:res.size], res)
 
 
 def test_timing_kinds_mask():

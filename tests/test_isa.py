@@ -24,6 +24,18 @@ def asm(tmp_path_factory):
     return out.read_text()
 
 
+@pytest.fixture(scope="module")
+def asm_resident(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    src = os.path.join(os.path.dirname(SRC), "resident.hip")
+    out = tmp_path_factory.mktemp("isa") / "resident.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", "-amdgpu-mfma-vgpr-form",
+                    "--cuda-device-only", "-S", "-I", os.path.dirname(SRC), src, "-o", str(out)],
+                   check=True, capture_output=True, timeout=600)
+    return out.read_text()
+
+
 def _functions(asm, pattern):
     for name in re.findall(r"^(%s\w*):" % pattern, asm, re.M):
         i = asm.index("\n" + name + ":")
@@ -67,5 +79,19 @@ def test_default_ordered_update_keeps_four_waves(asm):
             assert vgpr and int(vgpr.group(1)) <= 128, (name, vgpr and vgpr.group(1))
         else:                # the training forward at H = 32 (138 VGPRs in round 3): keep its 3 waves per SIMD
             assert vgpr and int(vgpr.group(1)) <= 168, (name, vgpr and vgpr.group(1))
+        assert scratch and int(scratch.group(1)) == 0, name
+    assert found
+
+
+def test_resident_forward_fits_its_workgroup(asm_resident):
+    """resident_forward_kernel: 16 waves (one workgroup per graph) need <= 128 VGPRs; no scratch
+    (the per-lane fragment addresses stay inside the loops)."""
+    found = False
+    for name, body, meta in _functions(asm_resident, r"_Z23resident_forward_kernel"):
+        found = True
+        vgpr = re.search(r"NumVgprs: (\d+)", meta)
+        scratch = re.search(r"ScratchSize: (\d+)", meta)
+        print(name, vgpr.group(1), scratch.group(1))
+        assert vgpr and int(vgpr.group(1)) <= 128, name
         assert scratch and int(scratch.group(1)) == 0, name
     assert found
