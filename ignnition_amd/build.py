@@ -17,7 +17,7 @@ OUT = os.path.join(HERE, "libignmp.so")
 SOURCES = ["engine.cpp", "devpool.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "plan_json.cpp", "kernels.hip", "kernels_bf.hip",
            "train_kernels.hip", "readout_kernels.hip", "resident.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
-EXTRA = {"kernels_bf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+EXTRA = {"kernels_bf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "resident.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def needs_build() -> bool:

@@ -587,9 +587,10 @@ static bool resident_plan_ok(const ign_plan* p) {
   return p->ents[path].feature_total <= 32 && p->ents[link].feature_total <= 32;
 }
 
-static size_t resident_lds_bytes(int64_t paths, int64_t links) {
+static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs) {
   return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
-         sizeof(float);
+             sizeof(float) +
+         (size_t)(links + 1) * sizeof(int32_t) + (size_t)msgs * sizeof(uint16_t);
 }
 
 // per-graph tables of the resident forward; leaves b->resident false where it does not apply
@@ -603,20 +604,44 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   const int G = b->G;
   const auto& po = b->row_off[path];
   const auto& lo = b->row_off[link];
-  size_t lds = 0;
-  for (int g = 0; g < G; ++g) lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], lo[g + 1] - lo[g]));
-  if (lds > kResidentMaxDynLds) return IGN_OK;
   // the graph of every row (rows are graph-contiguous)
   auto graph_of = [&](const std::vector<int64_t>& off, int64_t r) {
     return (int)(std::upper_bound(off.begin(), off.end(), r) - off.begin()) - 1;
   };
+  // sum MP: each graph's CSR by local link row, its messages in the MP's order (local path rows)
+  const int64_t NL = (int64_t)ms.h_order.size();
+  hvec<int32_t> lmsg_ptr((size_t)(lo[G] + G), 0), lmsg_off(G + 1, 0);
+  std::vector<int64_t> nmsg(G, 0);
+  for (int64_t q = 0; q < NL; ++q) {
+    const int64_t row = ms.h_order[q];
+    const int g = graph_of(lo, row);
+    lmsg_ptr[row + g + 1] = ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];   // counts, prefix-summed below
+    nmsg[g] += ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];
+  }
+  size_t lds = 0;
+  for (int g = 0; g < G; ++g) {
+    const int64_t P = po[g + 1] - po[g], L = lo[g + 1] - lo[g];
+    if (P > 65535) return IGN_OK;   // local path rows are 16-bit
+    lds = std::max(lds, resident_lds_bytes(P, L, nmsg[g]));
+    lmsg_off[g + 1] = lmsg_off[g] + (int32_t)nmsg[g];
+    int32_t* cp = lmsg_ptr.data() + lo[g] + g;
+    for (int64_t r = 0; r < L; ++r) cp[r + 1] += cp[r];
+  }
+  if (lds > kResidentMaxDynLds) return IGN_OK;
+  hvec<uint16_t> lmsg_src(std::max<int32_t>(lmsg_off[G], 1));
+  for (int64_t q = 0; q < NL; ++q) {
+    const int64_t row = ms.h_order[q];
+    const int g = graph_of(lo, row);
+    int32_t pos = lmsg_off[g] + lmsg_ptr[row + g];
+    for (int32_t m = ms.h_msg_ptr[q]; m < ms.h_msg_ptr[q + 1]; ++m)
+      lmsg_src[pos++] = (uint16_t)((ms.h_msg_src[m] & IGN_ROW_MASK) - po[g]);
+  }
   // ordered MP: each graph's positions in the batch's length-sorted order (stable, so still sorted
-  // by length, descending), padded to whole tiles; sum MP: each graph's order positions
-  std::vector<std::vector<int32_t>> pp(G), lp(G);
+  // by length, descending), padded to whole tiles
+  std::vector<std::vector<int32_t>> pp(G);
   const int64_t ND = (int64_t)ma.h_order.size();
   for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
-  for (size_t i = 0; i < ms.h_order.size(); ++i) lp[graph_of(lo, ms.h_order[i])].push_back((int32_t)i);
-  hvec<int32_t> ptile_off(G + 1, 0), lpos_off(G + 1, 0), hdr, lpos;
+  hvec<int32_t> ptile_off(G + 1, 0), hdr;
   const int64_t steps = ma.n_steps;
   for (int g = 0; g < G; ++g) {
     const int64_t n = (int64_t)pp[g].size(), np = (n + 15) / 16 * 16;
@@ -635,23 +660,21 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       }
     }
     ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
-    lpos.insert(lpos.end(), lp[g].begin(), lp[g].end());
-    lpos_off[g + 1] = (int32_t)lpos.size();
   }
-  if (lpos.empty()) lpos.push_back(0);
   std::vector<int64_t> pov(po.begin(), po.end()), lov(lo.begin(), lo.end());
   int rc;
   if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_link_off, lov)) ||
       (rc = dev_upload(b, &b->d_res_ptile_off, ptile_off)) || (rc = dev_upload(b, &b->d_res_hdr, hdr)) ||
-      (rc = dev_upload(b, &b->d_res_lpos_off, lpos_off)) || (rc = dev_upload(b, &b->d_res_lpos, lpos)))
+      (rc = dev_upload(b, &b->d_res_lmsg_off, lmsg_off)) || (rc = dev_upload(b, &b->d_res_lmsg_ptr, lmsg_ptr)) ||
+      (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)))
     return rc;
   b->res_lds = lds;
   // one launch reads the features, the tile headers, the step codes (T times, from L2 after the
   // first), the sum MP's CSR and positions and writes the final states once: the HBM floor
   const int64_t P = b->rows[path], L = b->rows[link];
   b->res_bytes = 4.0 * (P * p->ents[path].feature_total + L * p->ents[link].feature_total) + 4.0 * hdr.size() +
-                 4.0 * (double)ma.h_step_code.size() + 4.0 * (ms.h_msg_ptr.size() + ms.h_msg_src.size()) +
-                 8.0 * (double)lpos.size() + 4.0 * 32 * (P + L);
+                 4.0 * (double)ma.h_step_code.size() + 4.0 * lmsg_ptr.size() + 2.0 * lmsg_src.size() +
+                 4.0 * 32 * (P + L);
   // the MPs' FLOPs per iteration (the sum update's aggregation and GRU step, the ordered update's
   // h.U and gates) plus the ordered MP's input projection of every link state
   b->res_flops = p->T * (ma.flops + ms.flops + 2.0 * L * 32 * 96);
@@ -1624,11 +1647,9 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.ptile_off = b->d_res_ptile_off;
   r.hdr = b->d_res_hdr;
   r.step_code = ma.d_step_code;
-  r.lpos_off = b->d_res_lpos_off;
-  r.lpos = b->d_res_lpos;
-  r.l_order = ms.d_order;
-  r.msg_ptr = ms.d_msg_ptr;
-  r.msg_src = ms.d_msg_src;
+  r.lmsg_off = b->d_res_lmsg_off;
+  r.lmsg_ptr = b->d_res_lmsg_ptr;
+  r.lmsg_src = b->d_res_lmsg_src;
   r.path_feat = b->d_feat[path];
   r.path_F = p->ents[path].feature_total;
   r.link_feat = b->d_feat[link];

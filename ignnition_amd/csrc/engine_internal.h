@@ -307,7 +307,7 @@ struct ign_batch {
   // them (fused_proj_target); proj_ready[m'] tells m' that its table is already filled
   bool fuse_ok = false, fuse_last_iter = false;
   // the graph-resident forward (resident.hip, plan->resident): per-graph offsets, the ordered MP's
-  // per-graph tile headers, the sum MP's per-graph order positions; dynamic LDS of the largest graph
+  // per-graph tile headers, the sum MP's per-graph CSR (local rows); dynamic LDS of the largest graph
   bool resident = false;
   size_t res_lds = 0;
   double res_bytes = 0, res_flops = 0;   // per launch: HBM bytes it must move, FLOPs it executes
@@ -315,8 +315,9 @@ struct ign_batch {
   int64_t* d_res_link_off = nullptr;
   int32_t* d_res_ptile_off = nullptr;
   int32_t* d_res_hdr = nullptr;
-  int32_t* d_res_lpos_off = nullptr;
-  int32_t* d_res_lpos = nullptr;
+  int32_t* d_res_lmsg_off = nullptr;
+  int32_t* d_res_lmsg_ptr = nullptr;
+  uint16_t* d_res_lmsg_src = nullptr;
   std::vector<char> proj_ready;
   float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
   std::vector<float*> d_ro_tmp;                 // generic readout intermediates

@@ -164,7 +164,7 @@ hipError_t launch_sum_seg(const SumSegArgs& args, int din, hipStream_t st);
 constexpr int kResidentWaves = 16;
 constexpr int kResidentStateStride = 36;    // LDS floats per 32-wide state row
 constexpr int kResidentTableStride = 100;   // LDS floats per 96-wide projected row
-constexpr size_t kResidentMaxDynLds = 144 * 1024;
+constexpr size_t kResidentMaxDynLds = 144 * 1024;   // + ~14.5 KB static (U pieces, biases)
 struct ResidentArgs {
   const int64_t* path_off;    // [G + 1] rows of the ordered MP's destination entity ("paths") per graph
   const int64_t* link_off;    // [G + 1] rows of its source entity ("links") per graph
@@ -172,11 +172,9 @@ struct ResidentArgs {
   const int32_t* hdr;         // [headers][4] per graph, its paths by length descending, padded to whole
                               // tiles: {path row, final_len (0: padding), step_ptr, first step's code}
   const uint32_t* step_code;  // the ordered MP's step codes (global table rows; zero_row = hole)
-  const int32_t* lpos_off;    // [G + 1]
-  const int32_t* lpos;        // per graph, the sum MP's order positions of its links
-  const int32_t* l_order;     // the sum MP's order: position -> link row
-  const int32_t* msg_ptr;     // the sum MP's CSR over order positions
-  const uint32_t* msg_src;    // its message codes (slot 0 | path row)
+  const int32_t* lmsg_off;    // [G + 1] graph g's sum-MP messages start here in lmsg_src; its CSR
+  const int32_t* lmsg_ptr;    //   [link_off[g] + g ...][L_g + 1] local offsets, by local link row
+  const uint16_t* lmsg_src;   //   local path rows, each link's messages in the sum MP's order
   const float* path_feat; int path_F;
   const float* link_feat; int link_F;
   float* path_state;          // [rows][32] final states

@@ -9,9 +9,11 @@
 //        (the hole row last), U's fp16 pieces;
 //   per iteration: phase A, the ordered update (link -> path, seq_gru_h16's tile loop over the
 //        graph's paths sorted by length; the projected rows and states come from LDS), barrier,
-//        phase B, the sum update (path -> link, sum_gru_g32's lane walk in message order over LDS
-//        path states, its split-bf16 GRU step, and the next iteration's projection of the new link
-//        states, as sum_gru_g32's fused projection), barrier.
+//        phase B, the sum update (path -> link) in three passes over all 16 waves: B1 the message
+//        sums (sum_gru_g32's adds in message order, one lane per (link, float4 column), the local
+//        CSR in LDS), B2 its split-bf16 GRU step (one wave per (link tile, column half)), B3 the
+//        next iteration's projection of the new link states (sum_gru_g32's fused projection, one
+//        wave per (link tile, gate)), barriers between.
 // The arithmetic per row is that of the batched kernels: the same message order, pieces, products
 // and gate formulas (iteration 0 projects with project_kernel's f32 MFMA, later iterations with
 // sum_gru_g32's fused split-bf16 projection), so the predictions are the batched forward's bits and
@@ -23,6 +25,21 @@
 #include <stdint.h>
 #include "kernels.h"
 #include "device_common.h"
+
+#ifdef IGN_RES_STAMP
+// Diagnostic build only (tools/build_ab.sh NAME -DIGN_RES_STAMP; tools/probes/res_stamps.py): per
+// wave of the first 256 workgroups, s_memtime sums of the phases (cdna_hip_programming.md §7).
+__device__ unsigned long long ign_res_stamps[256 * kResidentWaves * 8];
+#define IGN_STAMP(v)                                                          \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+extern "C" int ign_debug_res_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ign_res_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 namespace {
 
@@ -121,8 +138,15 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   float* hP = dyn;
   float* hL = hP + P * SP;
   float* tab = hL + L * SP;
+  int* smp = reinterpret_cast<int*>(tab + (L + 1) * ST);   // the sum MP's CSR by local link row
+  uint16_t* sms = reinterpret_cast<uint16_t*>(smp + L + 1);
+  float* xs = tab;   // phase B's message sums [L][SP] alias the (consumed) projected table
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
+#ifdef IGN_RES_STAMP
+  unsigned long long t_0, t_a, t_b, s_init = 0, s_aw = 0, s_ab = 0, s_bw = 0, s_bb = 0, n_at = 0, n_bt = 0;
+  IGN_STAMP(t_0);
+#endif
   for (int i = tid; i < H; i += 64 * kW) sbias[i] = a.seq_bias[3 * H + i];
   {
     const u4v* src = reinterpret_cast<const u4v*>(a.Uh);
@@ -142,6 +166,12 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     hL[r * SP + c] = c < a.link_F ? a.link_feat[(l0 + r) * a.link_F + c] : 0.f;
   }
   for (int i = tid; i < 3 * H; i += 64 * kW) tab[L * ST + i] = a.proj_b[i];   // the hole row: b' alone
+  {
+    const int* gp = a.lmsg_ptr + l0 + gph;
+    for (int64_t i = tid; i <= L; i += 64 * kW) smp[i] = gp[i];
+    const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
+    for (int64_t i = tid; i < M; i += 64 * kW) sms[i] = a.lmsg_src[ms0 + i];
+  }
   __syncthreads();
   const int64_t nlt = (L + 15) / 16;   // link tiles
   // the first iteration's projected table
@@ -155,9 +185,12 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     project_row_f32(a, h, tab, ll, valid, lane, g);
   }
   __syncthreads();
+#ifdef IGN_RES_STAMP
+  IGN_STAMP(t_a);
+  s_init = t_a - t_0;
+#endif
 
   const int64_t pt0 = a.ptile_off[gph], npt = (a.ptile_off[gph + 1] - pt0) / 16;
-  const int64_t q0 = a.lpos_off[gph];
   const uint32_t zero_row = (uint32_t)a.zero_row;
   // global table row -> LDS table row; the hole row (and, for the masked steps past a row's end,
   // codes of other graphs' links, whose rows are never used) -> L
@@ -167,8 +200,10 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   };
   for (int it = 0; it < a.T; ++it) {
     // ---- phase A: the ordered update (seq_gru_h16's tile loop over the graph's path tiles) ----
+    i4v hd_next = wave < npt ? *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * wave + j)) : i4v{0, 0, 0, 0};
     for (int64_t k = wave; k < npt; k += kW) {
-      const i4v hd = *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * k + j));
+      const i4v hd = hd_next;   // the next tile's header loads under this tile's steps
+      if (k + kW < npt) hd_next = *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * (k + kW) + j));
       const int Lr = hd[1];
       const bool valid = Lr > 0;   // tile padding: length 0
       const int64_t rl = valid ? hd[0] - p0 : 0;
@@ -274,61 +309,87 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #pragma unroll
         for (int t = 0; t < NT; ++t) lds4w(hP + rl * SP + 16 * t + 4 * g, h[t] * iS);
       }
+#ifdef IGN_RES_STAMP
+      ++n_at;
+#endif
+    }
+#ifdef IGN_RES_STAMP
+    IGN_STAMP(t_b);
+    s_aw += t_b - t_a;
+#endif
+    __syncthreads();
+#ifdef IGN_RES_STAMP
+    IGN_STAMP(t_a);
+    s_ab += t_a - t_b;
+#endif
+    // ---- phase B: the sum update, in three passes over all 16 waves ----
+    // B1: the message sums, one lane per (link, float4 column): the adds of sum_gru_g32's lane walk
+    // (message order from zero, per column), the codes from LDS
+    for (int64_t i = tid; i < L * (H / 4); i += 64 * kW) {
+      const int64_t ll = i >> 3;
+      const int c4 = (int)(i & 7);
+      const int m0 = smp[ll], m1 = smp[ll + 1];
+      const float* hp = hP + 4 * c4;
+      f4 x = {0, 0, 0, 0};
+      int m = m0;
+      for (; m + 8 <= m1; m += 8) {
+        int rr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rr[u] = sms[m + u];
+        f4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = lds4(hp + rr[u] * SP);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x = x + v[u];
+      }
+      for (; m < m1; ++m) x = x + lds4(hp + sms[m] * SP);
+      lds4w(xs + ll * SP + 4 * c4, x);
     }
     __syncthreads();
-    // ---- phase B: the sum update (sum_gru_g32: lane walk in message order, split-bf16 GRU step) ----
+    // B2: the split-bf16 GRU step (sum_gru_g32's), one wave per (link tile, 16-column half); the new
+    // states are written after a barrier (the other half's wave still reads the old ones)
     const bool last = it + 1 == a.T;
-    for (int64_t k = wave; k < nlt; k += kW) {
+    const int64_t nb2 = 2 * nlt, rounds2 = (nb2 + kW - 1) / kW;
+    for (int64_t rr = 0; rr < rounds2; ++rr) {
+      const int64_t item = rr * kW + wave;
+      const bool act = item < nb2;   // wave-uniform
+      const int64_t k = act ? item >> 1 : 0;
+      const int t = (int)(item & 1);
       const int64_t idx = 16 * k + j;
-      const bool valid = idx < L;
-      const int q = a.lpos[q0 + (valid ? idx : 0)];
-      const int ll = valid ? a.l_order[q] - (int)l0 : 0;
-      const int64_t m0 = valid ? a.msg_ptr[q] : 0, m1 = valid ? a.msg_ptr[q + 1] : 0;
-      f4 x[2] = {f4{0, 0, 0, 0}, f4{0, 0, 0, 0}};
-      const int64_t lastm = m1 > m0 ? m1 - 1 : m0;
-      for (int64_t mm = m0; mm < m1; mm += 8) {   // 8 codes per round trip, the adds in message order
-        uint32_t cc8[8];
+      const bool valid = act && idx < L;
+      const int ll = valid ? (int)idx : 0;
+      f4 hn = {0, 0, 0, 0};
+      if (act) {
+        f4 x[2], h[2];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) cc8[u] = a.msg_src[mm + u < lastm ? mm + u : lastm];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (mm + u < m1) {
-            const int64_t pr = (int64_t)(cc8[u] & IGN_ROW_MASK) - p0;
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) x[cc] = x[cc] + lds4(hP + pr * SP + 16 * cc + 4 * g);
-          }
+        for (int c = 0; c < 2; ++c) {
+          x[c] = lds4(xs + (int64_t)ll * SP + 16 * c + 4 * g);
+          h[c] = lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g);
         }
-      }
-      f4 h[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) h[t] = lds4(hL + (int64_t)ll * SP + 16 * t + 4 * g);
-      bf8 xf[3][1], hf[3][1];
-      split_frags1(x, xf);
-      split_frags1(h, hf);
-      const bf8* sW = static_cast<const bf8*>(a.sWbf);
-      const bf8* sU = static_cast<const bf8*>(a.sUbf);
-      int lofs = lane;   // opaque: the fragment addresses stay inside the loop (as project_row)
-      asm volatile("" : "+v"(lofs));
-      f4 hn[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
+        bf8 xf[3][1], hf[3][1];
+        split_frags1(x, xf);
+        split_frags1(h, hf);
+        const bf8* sW = static_cast<const bf8*>(a.sWbf);
+        const bf8* sU = static_cast<const bf8*>(a.sUbf);
+        int lofs = lane + 64 * t;   // opaque: the fragment addresses stay inside the loop (as project_row)
+        asm volatile("" : "+v"(lofs));
         const int u0 = 16 * t + 4 * g;
         f4 az = ld4(a.sum_bias + 0 * H + u0), ar = ld4(a.sum_bias + 1 * H + u0);
         f4 ax = ld4(a.sum_bias + 2 * H + u0), ah = ld4(a.sum_bias + 3 * H + u0);
 #pragma unroll
         for (int pu = 2; pu >= 0; --pu) {
-          const bf8 wz = sW[((pu * 3 + 0) * NT + t) * 64 + lofs];
-          const bf8 wr = sW[((pu * 3 + 1) * NT + t) * 64 + lofs];
-          const bf8 wh = sW[((pu * 3 + 2) * NT + t) * 64 + lofs];
+          const bf8 wz = sW[((pu * 3 + 0) * NT) * 64 + lofs];
+          const bf8 wr = sW[((pu * 3 + 1) * NT) * 64 + lofs];
+          const bf8 wh = sW[((pu * 3 + 2) * NT) * 64 + lofs];
 #pragma unroll
           for (int ph = 2 - pu; ph >= 0; --ph) {
             az = MFMA_BF(wz, xf[ph][0], az);
             ar = MFMA_BF(wr, xf[ph][0], ar);
             ax = MFMA_BF(wh, xf[ph][0], ax);
           }
-          const bf8 uz = sU[((pu * 3 + 0) * NT + t) * 64 + lofs];
-          const bf8 ur = sU[((pu * 3 + 1) * NT + t) * 64 + lofs];
-          const bf8 uh = sU[((pu * 3 + 2) * NT + t) * 64 + lofs];
+          const bf8 uz = sU[((pu * 3 + 0) * NT) * 64 + lofs];
+          const bf8 ur = sU[((pu * 3 + 1) * NT) * 64 + lofs];
+          const bf8 uh = sU[((pu * 3 + 2) * NT) * 64 + lofs];
 #pragma unroll
           for (int ph = 2 - pu; ph >= 0; --ph) {
             az = MFMA_BF(uz, hf[ph][0], az);
@@ -336,23 +397,70 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
             ah = MFMA_BF(uh, hf[ph][0], ah);
           }
         }
+        const f4 ho = t ? h[1] : h[0];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float z = sig2_(az[r]);
-          const float rr = sig2_(ar[r]);
-          const float cnd = tanh2_(ax[r] + rr * ah[r]);
-          hn[t][r] = cnd + z * (h[t][r] - cnd);
+          const float rg = sig2_(ar[r]);
+          const float cnd = tanh2_(ax[r] + rg * ah[r]);
+          hn[r] = cnd + z * (ho[r] - cnd);
         }
       }
-      static_assert(NFB == 18, "g32 piece layout");
-      if (valid) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn[t]);
-      }
-      if (!last) project_row(a, hn, tab, ll, valid, lane, g);
+      __syncthreads();
+      if (valid) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn);
     }
+    static_assert(NFB == 18, "g32 piece layout");
+    // B3: the next iteration's projected table (sum_gru_g32's fused projection), one wave per
+    // (link tile, gate)
+    if (!last) {
+      __syncthreads();
+      const bf8* pw = static_cast<const bf8*>(a.proj_W);
+      for (int64_t item = wave; item < 3 * nlt; item += kW) {
+        const int64_t k = item / 3;
+        const int G = (int)(item - 3 * k);
+        const int64_t idx = 16 * k + j;
+        const bool valid = idx < L;
+        const int ll = valid ? (int)idx : 0;
+        f4 h[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) h[c] = lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g);
+        bf8 pf[3][1];
+        split_frags1(h, pf);
+        int lofs = lane + 64 * NT * G;
+        asm volatile("" : "+v"(lofs));
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          f4 acc = ld4(a.proj_b + G * H + 16 * i + 4 * g);
+#pragma unroll
+          for (int pu = 2; pu >= 0; --pu) {
+            const bf8 w = pw[(pu * 3 * NT + i) * 64 + lofs];
+#pragma unroll
+            for (int ph = 2 - pu; ph >= 0; --ph) acc = MFMA_BF(w, pf[ph][0], acc);
+          }
+          if (valid) lds4w(tab + (int64_t)ll * ST + G * H + 16 * i + 4 * g, acc);
+        }
+#ifdef IGN_RES_STAMP
+        ++n_bt;
+#endif
+      }
+    }
+#ifdef IGN_RES_STAMP
+    IGN_STAMP(t_b);
+    s_bw += t_b - t_a;
+#endif
     __syncthreads();
+#ifdef IGN_RES_STAMP
+    IGN_STAMP(t_a);
+    s_bb += t_a - t_b;
+#endif
   }
+#ifdef IGN_RES_STAMP
+  if (lane == 0 && gph < 256) {
+    unsigned long long* o = ign_res_stamps + 8 * (gph * kW + wave);
+    o[0] = s_init; o[1] = s_aw; o[2] = s_ab; o[3] = s_bw; o[4] = s_bb; o[5] = n_at; o[6] = n_bt;
+    o[7] = t_a - t_0;
+  }
+#endif
   // the final states leave the workgroup (the readout and ign_batch_state read them)
   for (int64_t i = tid; i < P * (H / 4); i += 64 * kW) {
     const int64_t r = i / (H / 4);
