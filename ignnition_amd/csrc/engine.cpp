@@ -587,10 +587,10 @@ static bool resident_plan_ok(const ign_plan* p) {
   return p->ents[path].feature_total <= 32 && p->ents[link].feature_total <= 32;
 }
 
-static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs) {
+static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs, int64_t codes) {
   return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
              sizeof(float) +
-         (size_t)(links + 1) * sizeof(int32_t) + (size_t)msgs * sizeof(uint16_t);
+         (size_t)(links + 1) * sizeof(int32_t) + (size_t)(msgs + codes) * sizeof(uint16_t);
 }
 
 // per-graph tables of the resident forward; leaves b->resident false where it does not apply
@@ -618,16 +618,12 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     lmsg_ptr[row + g + 1] = ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];   // counts, prefix-summed below
     nmsg[g] += ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];
   }
-  size_t lds = 0;
   for (int g = 0; g < G; ++g) {
-    const int64_t P = po[g + 1] - po[g], L = lo[g + 1] - lo[g];
-    if (P > 65535) return IGN_OK;   // local path rows are 16-bit
-    lds = std::max(lds, resident_lds_bytes(P, L, nmsg[g]));
+    if (po[g + 1] - po[g] > 65535 || lo[g + 1] - lo[g] > 65535) return IGN_OK;   // local rows are 16-bit
     lmsg_off[g + 1] = lmsg_off[g] + (int32_t)nmsg[g];
     int32_t* cp = lmsg_ptr.data() + lo[g] + g;
-    for (int64_t r = 0; r < L; ++r) cp[r + 1] += cp[r];
+    for (int64_t r = 0; r < lo[g + 1] - lo[g]; ++r) cp[r + 1] += cp[r];
   }
-  if (lds > kResidentMaxDynLds) return IGN_OK;
   hvec<uint16_t> lmsg_src(std::max<int32_t>(lmsg_off[G], 1));
   for (int64_t q = 0; q < NL; ++q) {
     const int64_t row = ms.h_order[q];
@@ -637,43 +633,61 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       lmsg_src[pos++] = (uint16_t)((ms.h_msg_src[m] & IGN_ROW_MASK) - po[g]);
   }
   // ordered MP: each graph's positions in the batch's length-sorted order (stable, so still sorted
-  // by length, descending), padded to whole tiles
+  // by length, descending), padded to whole tiles; their step codes as local link rows (L_g: the
+  // hole), then max_len + 8 hole codes (the tile loop reads codes past a row's end)
   std::vector<std::vector<int32_t>> pp(G);
   const int64_t ND = (int64_t)ma.h_order.size();
   for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
-  hvec<int32_t> ptile_off(G + 1, 0), hdr;
-  const int64_t steps = ma.n_steps;
+  hvec<int32_t> ptile_off(G + 1, 0), hdr, lcode_off(G + 1, 0);
+  hvec<uint16_t> lcode;
+  size_t lds = 0;
   for (int g = 0; g < G; ++g) {
+    const int64_t L = lo[g + 1] - lo[g];
     const int64_t n = (int64_t)pp[g].size(), np = (n + 15) / 16 * 16;
-    for (int64_t k = 0; k < np; ++k) {
-      if (k < n) {
-        const int64_t i = pp[g][k];
-        hdr.push_back(ma.h_order[i]);
-        hdr.push_back(ma.h_len[i]);
-        hdr.push_back(ma.h_step_ptr[i]);
-        hdr.push_back((int32_t)ma.h_step_code[ma.h_step_ptr[i]]);
-      } else {   // padding: length 0, codes of the hole row
-        hdr.push_back(0);
-        hdr.push_back(0);
-        hdr.push_back((int32_t)steps);
-        hdr.push_back((int32_t)ma.h_step_code[steps]);
+    const size_t c0 = lcode.size();
+    int32_t maxl = 0;
+    for (int64_t k = 0; k < n; ++k) {
+      const int64_t i = pp[g][k];
+      const int32_t len = ma.h_len[i], sp = ma.h_step_ptr[i];
+      hdr.push_back((int32_t)(ma.h_order[i] - po[g]));
+      hdr.push_back(len);
+      hdr.push_back((int32_t)(lcode.size() - c0));
+      for (int32_t t = 0; t < len; ++t) {
+        const uint32_t c = ma.h_step_code[sp + t];
+        const int64_t lr = (int64_t)c - lo[g];
+        if (c < (uint32_t)ma.zero_row && (lr < 0 || lr >= L)) return IGN_OK;   // another graph's row: not resident
+        lcode.push_back((uint16_t)(c < (uint32_t)ma.zero_row ? lr : L));
       }
+      hdr.push_back(lcode[c0 + hdr[hdr.size() - 1]]);
+      maxl = std::max(maxl, len);
+    }
+    const int32_t pad = (int32_t)(lcode.size() - c0);
+    lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)L);
+    for (int64_t k = n; k < np; ++k) {   // padding: length 0, hole codes
+      hdr.push_back(0);
+      hdr.push_back(0);
+      hdr.push_back(pad);
+      hdr.push_back((int32_t)L);
     }
     ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
+    lcode_off[g + 1] = (int32_t)lcode.size();
+    lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], lcode_off[g + 1] - lcode_off[g]));
   }
+  if (lds > kResidentMaxDynLds) return IGN_OK;
   std::vector<int64_t> pov(po.begin(), po.end()), lov(lo.begin(), lo.end());
   int rc;
   if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_link_off, lov)) ||
       (rc = dev_upload(b, &b->d_res_ptile_off, ptile_off)) || (rc = dev_upload(b, &b->d_res_hdr, hdr)) ||
       (rc = dev_upload(b, &b->d_res_lmsg_off, lmsg_off)) || (rc = dev_upload(b, &b->d_res_lmsg_ptr, lmsg_ptr)) ||
-      (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)))
+      (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)) || (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
+      (rc = dev_upload(b, &b->d_res_lcode, lcode)))
     return rc;
   b->res_lds = lds;
-  // one launch reads the features, the tile headers, the step codes (T times, from L2 after the
-  // first), the sum MP's CSR and positions and writes the final states once: the HBM floor
+  // one launch reads the features, the tile headers (T times, from L2 after the first), the step
+  // codes, the sum MP's CSR and writes the final states once: the HBM floor
   const int64_t P = b->rows[path], L = b->rows[link];
   b->res_bytes = 4.0 * (P * p->ents[path].feature_total + L * p->ents[link].feature_total) + 4.0 * hdr.size() +
-                 4.0 * (double)ma.h_step_code.size() + 4.0 * lmsg_ptr.size() + 2.0 * lmsg_src.size() +
+                 2.0 * (double)lcode.size() + 4.0 * lmsg_ptr.size() + 2.0 * lmsg_src.size() +
                  4.0 * 32 * (P + L);
   // the MPs' FLOPs per iteration (the sum update's aggregation and GRU step, the ordered update's
   // h.U and gates) plus the ordered MP's input projection of every link state
@@ -1646,7 +1660,8 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.link_off = b->d_res_link_off;
   r.ptile_off = b->d_res_ptile_off;
   r.hdr = b->d_res_hdr;
-  r.step_code = ma.d_step_code;
+  r.lcode_off = b->d_res_lcode_off;
+  r.lcode = b->d_res_lcode;
   r.lmsg_off = b->d_res_lmsg_off;
   r.lmsg_ptr = b->d_res_lmsg_ptr;
   r.lmsg_src = b->d_res_lmsg_src;
@@ -1665,7 +1680,6 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.proj_b = p->d_packed + ca.pk_b;
   r.proj_Wf = p->d_packed + ca.pk_w;
   r.T = p->T;
-  r.zero_row = ma.zero_row;
   Timer tm{p};
   tm.begin(K_RESIDENT, b->res_flops, b->res_bytes);
   HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, p->stream));

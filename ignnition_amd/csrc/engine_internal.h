@@ -318,6 +318,8 @@ struct ign_batch {
   int32_t* d_res_lmsg_off = nullptr;
   int32_t* d_res_lmsg_ptr = nullptr;
   uint16_t* d_res_lmsg_src = nullptr;
+  int32_t* d_res_lcode_off = nullptr;
+  uint16_t* d_res_lcode = nullptr;
   std::vector<char> proj_ready;
   float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
   std::vector<float*> d_ro_tmp;                 // generic readout intermediates

@@ -170,8 +170,10 @@ struct ResidentArgs {
   const int64_t* link_off;    // [G + 1] rows of its source entity ("links") per graph
   const int32_t* ptile_off;   // [G + 1] first header of graph g (multiples of 16)
   const int32_t* hdr;         // [headers][4] per graph, its paths by length descending, padded to whole
-                              // tiles: {path row, final_len (0: padding), step_ptr, first step's code}
-  const uint32_t* step_code;  // the ordered MP's step codes (global table rows; zero_row = hole)
+                              // tiles: {local path row, final_len (0: padding), local step offset,
+                              // first step's local code}
+  const int32_t* lcode_off;   // [G + 1] graph g's ordered-MP step codes start here in lcode
+  const uint16_t* lcode;      //   local link rows (L_g = the hole), then max_len + 8 hole codes
   const int32_t* lmsg_off;    // [G + 1] graph g's sum-MP messages start here in lmsg_src; its CSR
   const int32_t* lmsg_ptr;    //   [link_off[g] + g ...][L_g + 1] local offsets, by local link row
   const uint16_t* lmsg_src;   //   local path rows, each link's messages in the sum MP's order
@@ -188,7 +190,6 @@ struct ResidentArgs {
   const float* proj_b;
   const float* proj_Wf;       // ... and as project_kernel's f32 fragments (the iteration-0 projection)
   int T;
-  int64_t zero_row;           // the ordered MP's hole row (= the source entity's rows)
 };
 hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);

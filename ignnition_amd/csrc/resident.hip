@@ -131,6 +131,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   __shared__ h8 su[NF * 64];
   __shared__ float sbn[kW][H];
   __shared__ float sbias[H];
+  __shared__ int sctr[2];   // phase A's tile counters (alternate iterations)
   extern __shared__ float dyn[];
   const int gph = blockIdx.x;
   const int64_t p0 = a.path_off[gph], P = a.path_off[gph + 1] - p0;
@@ -140,6 +141,9 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   float* tab = hL + L * SP;
   int* smp = reinterpret_cast<int*>(tab + (L + 1) * ST);   // the sum MP's CSR by local link row
   uint16_t* sms = reinterpret_cast<uint16_t*>(smp + L + 1);
+  const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
+  uint16_t* scd = sms + M;   // the ordered MP's local step codes
+  const int64_t cd0 = a.lcode_off[gph], NC = a.lcode_off[gph + 1] - cd0;
   float* xs = tab;   // phase B's message sums [L][SP] alias the (consumed) projected table
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -148,6 +152,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   IGN_STAMP(t_0);
 #endif
   for (int i = tid; i < H; i += 64 * kW) sbias[i] = a.seq_bias[3 * H + i];
+  if (tid < 2) sctr[tid] = 0;
   {
     const u4v* src = reinterpret_cast<const u4v*>(a.Uh);
     u4v* dst = reinterpret_cast<u4v*>(su);
@@ -169,8 +174,8 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   {
     const int* gp = a.lmsg_ptr + l0 + gph;
     for (int64_t i = tid; i <= L; i += 64 * kW) smp[i] = gp[i];
-    const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
     for (int64_t i = tid; i < M; i += 64 * kW) sms[i] = a.lmsg_src[ms0 + i];
+    for (int64_t i = tid; i < NC; i += 64 * kW) scd[i] = a.lcode[cd0 + i];
   }
   __syncthreads();
   const int64_t nlt = (L + 15) / 16;   // link tiles
@@ -191,23 +196,31 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #endif
 
   const int64_t pt0 = a.ptile_off[gph], npt = (a.ptile_off[gph + 1] - pt0) / 16;
-  const uint32_t zero_row = (uint32_t)a.zero_row;
-  // global table row -> LDS table row; the hole row (and, for the masked steps past a row's end,
-  // codes of other graphs' links, whose rows are never used) -> L
-  auto local_code = [&](uint32_t code) -> int64_t {
-    const int64_t r = (int64_t)code - l0;
-    return code < zero_row && r >= 0 && r < L ? r : L;
-  };
   for (int it = 0; it < a.T; ++it) {
     // ---- phase A: the ordered update (seq_gru_h16's tile loop over the graph's path tiles) ----
-    i4v hd_next = wave < npt ? *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * wave + j)) : i4v{0, 0, 0, 0};
-    for (int64_t k = wave; k < npt; k += kW) {
+#ifdef IGN_RES_STATIC
+    auto claim = [&](int k) -> int { return k < 0 ? wave : k + kW; };   // A/B: wave w takes tiles w, w + 16, ...
+#else
+    // the waves claim tiles from an LDS counter, longest tiles first (a greedy longest-first schedule:
+    // the SIMDs' arbitration decides which wave gets more of them; results do not depend on it)
+    int* ctr = &sctr[it & 1];
+    if (tid == 0) sctr[(it + 1) & 1] = 0;   // the next iteration's counter (its last user finished)
+    auto claim = [&](int) -> int {
+      int v = 0;
+      if (lane == 0) v = atomicAdd(ctr, 1);
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+#endif
+    int k = claim(-1);
+    i4v hd_next = k < npt ? *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * k + j)) : i4v{0, 0, 0, 0};
+    while (k < npt) {
       const i4v hd = hd_next;   // the next tile's header loads under this tile's steps
-      if (k + kW < npt) hd_next = *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * (k + kW) + j));
+      const int kn = claim(k);
+      if (kn < npt) hd_next = *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * kn + j));
       const int Lr = hd[1];
       const bool valid = Lr > 0;   // tile padding: length 0
-      const int64_t rl = valid ? hd[0] - p0 : 0;
-      const uint32_t* codes = a.step_code + hd[2];
+      const int64_t rl = valid ? hd[0] : 0;
+      const uint16_t* codes = scd + hd[2];
       f4 h[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -216,7 +229,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       }
       f4 x[3][NT];
       auto load_x = [&](uint32_t code, f4 (&xx)[3][NT]) __attribute__((always_inline)) {
-        const float* p = tab + local_code(code) * ST + 4 * g;
+        const float* p = tab + (int64_t)code * ST + 4 * g;
 #pragma unroll
         for (int G = 0; G < 3; ++G)
 #pragma unroll
@@ -312,6 +325,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #ifdef IGN_RES_STAMP
       ++n_at;
 #endif
+      k = kn;
     }
 #ifdef IGN_RES_STAMP
     IGN_STAMP(t_b);
