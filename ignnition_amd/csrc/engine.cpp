@@ -223,6 +223,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_H16")) p->train_dense_h16 = atoi(v) != 0;
   if (const char* v = getenv("IGN_TSGEMM_BF")) p->tsgemm_bf = atoi(v) != 0;
+  if (const char* v = getenv("IGN_FUSE_OUTER_BWD")) p->fuse_outer_bwd = atoi(v) != 0;
+  if (const char* v = getenv("IGN_TRAIN_FUSED_READOUT")) p->train_fused_readout = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_SEQ_H16")) p->train_seq_h16 = atoi(v) != 0;
   if (const char* v = getenv("IGN_READOUT_VARIANT")) {   // 4 (default), 2 or 1; anything else: 4

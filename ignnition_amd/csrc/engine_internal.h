@@ -260,6 +260,8 @@ struct ign_plan {
   bool train_dense_bf = true;     // training forward's Dense layers on dense_bf (IGN_TRAIN_DENSE_BF=0: f32)
   bool train_dense_h16 = true;    // ... on the split-fp16 form of dense_bf (IGN_TRAIN_DENSE_H16=0: split-bf16)
   bool tsgemm_bf = true;          // weight-gradient row contractions on tsgemm_bf (IGN_TSGEMM_BF=0: f32 MFMA)
+  bool train_fused_readout = true;   // training forward's readout on readout_h16 with saves (IGN_TRAIN_FUSED_READOUT=0: per layer)
+  bool fuse_outer_bwd = true;     // 1-unit output layer's backward formed on the fly (IGN_FUSE_OUTER_BWD=0: row_outer_t)
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
   bool train_seq_h16 = true;      // training forward's ordered update on split-fp16 (IGN_TRAIN_SEQ_H16=0: bf16)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)

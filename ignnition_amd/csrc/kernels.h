@@ -88,6 +88,8 @@ struct Readout3Args {
   const float* w3;  const float* b3;  // [N2] (output units == 1), [1]
   int act1, act2, act3;
   float* y;                // [n_rows]
+  float* save1 = nullptr;  // readout_h16 only: [n_rows][N1] layer-1 activations (training forward)
+  float* save2 = nullptr;  //   [n_rows][N2] layer-2 activations
 };
 
 hipError_t launch_init_state(float* state, const float* feats, int64_t n, int H, int F, hipStream_t st);
@@ -127,9 +129,19 @@ inline int64_t pack_w_bf16_floats(int K, int H) { return ((H == 32 || H == 64) &
 hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t st);
 // sum update at DIN = H = 32: code-prefetched gather (gu rows in flight per lane), split-bf16 GRU step
 hipError_t launch_sum_gru_g32(const SumGruArgs& args, int gu, hipStream_t st);
-// split-bf16 form of the training row contraction (train_kernels.hip tsgemm; same grid and partials)
+// Rows formed on the fly from the backward of a 1-unit output layer: row[r][k] = (0 + s[r] w[k]) *
+// act'(raw[r][k]), raw = the layer's input activations (row_outer_t's arithmetic); s == nullptr: off
+struct OuterRows {
+  const float* s = nullptr;   // [rows] the output layer's pre-activation gradient
+  const float* w = nullptr;   // [K] its weights
+  int act = 0;                // the activation of raw
+};
+// split-bf16 form of the training row contraction (train_kernels.hip tsgemm; same grid and partials);
+// bo: B formed on the fly (only where tsgemm_bf_lds_ok)
+bool tsgemm_bf_lds_ok(int M, int N);
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
-                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st);
+                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st,
+                            OuterRows bo = OuterRows{});
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 
 // Windowed sum (AUX:254-262 for single-source sum MPs of graph-local batches): one workgroup per
@@ -213,7 +225,7 @@ hipError_t launch_dense_bf(const float* x, int64_t n, int K, int x_stride, const
 // the backward row GEMM out[r][0..M) (+)= (dz[r] . W^T) * act'(aprev[r]) (act < 0: no act'), dz [n][K]
 // dense; W^T packed by launch_pack_dense_bf16_t(W [M][K])
 hipError_t launch_dense_bf_t(const float* dz, int64_t n, int K, const void* Wtbf, int M, float* out, int accumulate,
-                             int act, const float* aprev, hipStream_t st);
+                             int act, const float* aprev, hipStream_t st, OuterRows xo = OuterRows{});
 hipError_t launch_pack_dense_bf16_t(const float* W, void* out, int IN, int OUT, hipStream_t st);
 // the same two row GEMMs on scaled split-fp16 (x3; DESIGN.md §3b'): W pieces from
 // launch_pack_dense_f16 (IN x OUT natural k, trans = 1 for W^T: IN = OUT_orig, OUT = IN_orig);
@@ -221,7 +233,7 @@ hipError_t launch_pack_dense_bf16_t(const float* W, void* out, int IN, int OUT, 
 hipError_t launch_dense_h16(const float* x, int64_t n, int K, int x_stride, const void* Wh, const float* bias, int M,
                             int act, float* y, hipStream_t st);
 hipError_t launch_dense_h16_t(const float* dz, int64_t n, int K, const void* Wth, int M, float* out, int accumulate,
-                              int act, const float* aprev, hipStream_t st);
+                              int act, const float* aprev, hipStream_t st, OuterRows xo = OuterRows{});
 hipError_t launch_pack_dense_f16(const float* W, void* out, int IN, int OUT, int trans, hipStream_t st);
 hipError_t launch_dense_generic(const float* x, int64_t n, int in, int x_stride, const float* W, const float* b,
                                 int out, int act, float* y, hipStream_t st);

@@ -1120,6 +1120,19 @@ __global__ __launch_bounds__(256) void tsgemm_bf_kernel(const float* __restrict_
   }
 }
 
+__device__ __forceinline__ float act_grad_out(float a, int act) {   // act' through the output a
+  switch (act) {
+    case IGN_K_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case IGN_K_ACT_SELU: {
+      const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
+      return a > 0.f ? lam : a + la;
+    }
+    case IGN_K_ACT_SIGMOID: return a * (1.f - a);
+    case IGN_K_ACT_TANH: return 1.f - a * a;
+    default: return 1.f;
+  }
+}
+
 // tsgemm_bf_kernel for M % 64 == N % 64 == 0 with the pieces split once per block: a block of
 // mtb x tiles_n waves holds the tiles of mtb 64-column groups of A against all of B.  Per 32-row
 // step every (column, 8-row group) pair of the block's A columns and of B is loaded once (64 lanes =
@@ -1130,10 +1143,11 @@ __global__ __launch_bounds__(256) void tsgemm_bf_kernel(const float* __restrict_
 // old kernel split every value once per wave that used it (4 times at 256 x 256).  Same products in
 // the same order per accumulator and the same column-sum order: bitwise the old kernel's partials.
 constexpr int kTsLdsCols = 384;   // A columns of the block + N
+// bo (optional): B formed on the fly from the output layer's gradient, as dense_bf_kernel's xo
 __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restrict__ A, int lda,
                                                             const float* __restrict__ B, int ldb, int64_t n_rows,
                                                             int M, int N, int ones, int64_t chunk, int mtb,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part, OuterRows bo) {
   constexpr int NTH = 512, KP = (kTsLdsCols * 4 + NTH - 1) / NTH;
   __shared__ u4v sp[2 * 3 * kTsLdsCols * 4];   // two buffers of [piece][column][row group]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1160,6 +1174,12 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
     ld[k] = col < AC ? lda : ldb;
   }
   float v[KP][8];
+  float bw[KP];   // bo: the output layer's weight of the thread's B columns
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int col = (tid + NTH * k) % COLS;
+    bw[k] = bo.s && col >= AC ? bo.w[col - AC] : 0.f;
+  }
   auto load = [&](int64_t r) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < KP; ++k)
@@ -1168,6 +1188,20 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
         const int64_t rr = r + 8 * gp[k] + jj;
         v[k][jj] = (pok[k] && rr < r1) ? src[k][rr * ld[k]] : 0.f;
       }
+    if (bo.s) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const int col = (tid + NTH * k) % COLS;
+        if (col < AC) continue;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int64_t rr = r + 8 * gp[k] + jj;
+          float sq = 0.f;
+          sq += (pok[k] && rr < r1 ? bo.s[rr] : 0.f) * bw[k];
+          v[k][jj] = sq * act_grad_out(v[k][jj], bo.act);
+        }
+      }
+    }
   };
   float cs[KP] = {};
   f4 acc[4][4];
@@ -1589,7 +1623,9 @@ __device__ __forceinline__ float act_scaled(float zs, float c, float k, float cl
   else return So * act_t<ACT>(zs * c);
 }
 
-template <int DIN, int ACT, int WAVES, int RT>
+// SAVE (the training forward): the layer-1 and layer-2 activations are also written (a.save1,
+// a.save2; the unscaled values the layers used, 16 B per lane per 16-unit tile) for the backward
+template <int DIN, int ACT, int WAVES, int RT, bool SAVE = false>
 __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a, const h8* __restrict__ W2f) {
   constexpr int N1 = 256, U1 = N1 / 16, U2 = 256 / 16;
   constexpr int KS1 = DIN / 32, KS2 = N1 / 32;
@@ -1709,6 +1745,13 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           v[t][4 * half + q] = act_scaled<ACT>(acc[t][q], c1[t], k, c1[t] * LOG2E, LA * S[t], S[t]);
+        if constexpr (SAVE) {
+          const int64_t r = r0 + 16 * t;
+          const float iS = __int_as_float(254 - ((__float_as_int(S[t]) >> 23) & 255) << 23);   // 1 / S, exact
+          if (r < a.n_rows)
+            st4(a.save1 + r * N1 + 16 * u + 4 * g,
+                f4{v[t][4 * half], v[t][4 * half + 1], v[t][4 * half + 2], v[t][4 * half + 3]} * iS);
+        }
       }
     }
 #pragma unroll
@@ -1775,11 +1818,19 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
     }
     const f4 w3 = sbias[128 + 4 * v + g];
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+    for (int t = 0; t < RT; ++t) {
+      f4 av;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        y[t] += w3[q] * act_scaled<ACT>(acc[t][q], cSS[t], ACT == IGN_K_ACT_SELU ? LAM : 1.0f, cSS[t] * LOG2E,
-                                        LA * SS[t], SS[t]);
+      for (int q = 0; q < 4; ++q) {
+        av[q] = act_scaled<ACT>(acc[t][q], cSS[t], ACT == IGN_K_ACT_SELU ? LAM : 1.0f, cSS[t] * LOG2E, LA * SS[t],
+                                SS[t]);
+        y[t] += w3[q] * av[q];
+      }
+      if constexpr (SAVE) {
+        const int64_t r = r0 + 16 * t;
+        if (r < a.n_rows) st4(a.save2 + r * 256 + 16 * v + 4 * g, av * cSS[t]);
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed (for every wave: barrier)
     __syncthreads();
   }
@@ -1800,19 +1851,6 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
   }  // row groups
 }
 
-__device__ __forceinline__ float act_grad_out(float a, int act) {   // act' through the output a
-  switch (act) {
-    case IGN_K_ACT_RELU: return a > 0.f ? 1.f : 0.f;
-    case IGN_K_ACT_SELU: {
-      const float lam = 1.0507009873554805f, la = 1.0507009873554805f * 1.6732632423543772f;
-      return a > 0.f ? lam : a + la;
-    }
-    case IGN_K_ACT_SIGMOID: return a * (1.f - a);
-    case IGN_K_ACT_TANH: return 1.f - a * a;
-    default: return 1.f;
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // Row GEMM y[r] = act(x[r] . W + b) on the split-bf16 path (the training forward's Dense layers,
 // whose activations are kept for the backward).  readout_bf's layer-2 loop with the input read
@@ -1821,11 +1859,14 @@ __device__ __forceinline__ float act_grad_out(float a, int act) {   // act' thro
 // registers (K / 32 x 3 fragments per tile) and writes act(acc) as 16 B per lane.
 // BWD: the backward row GEMM instead, y[r] (+)= (x[r] . W^T) * act'(aprev[r]) with W^T packed
 // (row_gemm_t's contract; bias unused, ACT = the activation whose derivative is applied).
+// xo (BWD only, optional): the input rows are the backward of a 1-unit output layer, formed on the
+// fly: x[r][k] = (0 + xo.s[r] * xo.w[k]) * act'(x_raw[r][k]) with x_raw the layer's output
+// activations (row_outer_t's arithmetic, so the materialised dz rows are never written)
 template <int KS, int G, int ACT, bool BWD = false, int NP = 3>
 __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__ x, int64_t n, int x_stride,
                                                        const void* __restrict__ Wf, const float* __restrict__ bias,
                                                        int M, float* __restrict__ y, const float* __restrict__ aprev,
-                                                       int accumulate) {
+                                                       int accumulate, OuterRows xo) {
   constexpr int WAVES = 8, RT = 2, NTH = 64 * WAVES;
   // NP = 3: split-bf16 x6; NP = 2: scaled split-fp16 x3 (W pieces carry sigma = 2^es after the
   // fragments, each 16-row tile of x its own S = 2^(15 - E(max |x|)); DESIGN.md §3b')
@@ -1846,11 +1887,27 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
     const int64_t r = r0 + 16 * t;
     const bool ok = r < n;
     const float* xr = x + (ok ? r : 0) * (int64_t)x_stride;
+    const float xsr = BWD && xo.s && ok ? xo.s[r] : 0.f;
+    // the input's 4 values at column c0 (raw, or formed from the output layer's gradient)
+    auto ldx = [&](int c0) __attribute__((always_inline)) -> f4 {
+      if (!ok) return f4{0, 0, 0, 0};
+      const f4 v = ld4(xr + c0);
+      if (!BWD || !xo.s) return v;
+      const f4 w = ld4(xo.w + c0);
+      f4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float sq = 0.f;
+        sq += xsr * w[q];
+        o[q] = sq * act_grad_out(v[q], xo.act);
+      }
+      return o;
+    };
     if constexpr (NP == 3) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const f4 lo = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
-        const f4 hi = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+        const f4 lo = ldx(32 * s + 8 * g);
+        const f4 hi = ldx(32 * s + 8 * g + 4);
         const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         split_frag(v, xf[t][s]);
       }
@@ -1859,8 +1916,8 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
       float mx = 1e-18f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        xv[s][0] = ok ? ld4(xr + 32 * s + 8 * g) : f4{0, 0, 0, 0};
-        xv[s][1] = ok ? ld4(xr + 32 * s + 8 * g + 4) : f4{0, 0, 0, 0};
+        xv[s][0] = ldx(32 * s + 8 * g);
+        xv[s][1] = ldx(32 * s + 8 * g + 4);
 #pragma unroll
         for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fmaxf(fabsf(xv[s][0][q]), fabsf(xv[s][1][q])));
       }
@@ -2023,7 +2080,7 @@ static void readout_h16_launch(const Readout3Args& args, const h8* w, hipStream_
 #define IGN_READOUT_WAVES 4
 #endif
   constexpr int WAVES = IGN_READOUT_WAVES, RT = 2;   // RT = 1 (8 or 4 waves) measured slower: 0.59 / 0.69 ms
-  auto k = readout_h16_kernel<DIN, ACT, WAVES, RT>;
+  auto k = args.save1 ? readout_h16_kernel<DIN, ACT, WAVES, RT, true> : readout_h16_kernel<DIN, ACT, WAVES, RT>;
   const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
   hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w);
 }
@@ -2041,7 +2098,8 @@ static void readout_h16_din(const Readout3Args& args, const h8* w, hipStream_t s
 
 hipError_t launch_readout_h16(const Readout3Args& args, const void* Wh, int din, hipStream_t st) {
   if (args.n_rows == 0) return hipSuccess;
-  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !Wh || !args.b1 || !args.b2)
+  if (!readout_bf_supported(din, 256, 256, args.act1, args.act2) || !Wh || !args.b1 || !args.b2 ||
+      !args.save1 != !args.save2)
     return hipErrorInvalidValue;
   const h8* w = static_cast<const h8*>(Wh);
   if (din == 32) readout_h16_din<32>(args, w, st);
@@ -2065,9 +2123,9 @@ bool dense_bf_supported(int K, int M) {
 
 template <int KS, int G, bool BWD, int NP>
 static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const void* W, const float* bias, int M, int act,
-                              float* y, const float* aprev, int accumulate, hipStream_t st) {
+                              float* y, const float* aprev, int accumulate, OuterRows xo, hipStream_t st) {
   const dim3 grid((unsigned)((n + 255) / 256)), block(512);
-#define DBF(A) hipLaunchKernelGGL((dense_bf_kernel<KS, G, A, BWD, NP>), grid, block, 0, st, x, n, x_stride, W, bias, M, y, aprev, accumulate)
+#define DBF(A) hipLaunchKernelGGL((dense_bf_kernel<KS, G, A, BWD, NP>), grid, block, 0, st, x, n, x_stride, W, bias, M, y, aprev, accumulate, xo)
   switch (act) {
     case IGN_K_ACT_SELU: DBF(IGN_K_ACT_SELU); break;
     case IGN_K_ACT_RELU: DBF(IGN_K_ACT_RELU); break;
@@ -2081,23 +2139,24 @@ static hipError_t dense_bf_ks(const float* x, int64_t n, int x_stride, const voi
 
 template <bool BWD, int NP = 3>
 static hipError_t dense_bf_any(const float* x, int64_t n, int K, int x_stride, const void* W, const float* bias, int M,
-                               int act, float* y, const float* aprev, int accumulate, hipStream_t st) {
+                               int act, float* y, const float* aprev, int accumulate, hipStream_t st,
+                               OuterRows xo = OuterRows{}) {
   // G 16-unit tiles of K x 16 x NP pieces per stage (M % 128 == 0: G divides M / 16).  NP = 2: 32 KB
   // stages, so each pass writes >= 128 B (whole lines) of every row: 0.949 -> 0.877 ms for the
   // 256-wide training readout layer, 19.9 -> 19.8 ms per step; NP = 3: <= 24 KB
   if constexpr (NP == 2) {
     switch (K) {
-      case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-      case 64: return dense_bf_ks<2, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-      case 128: return dense_bf_ks<4, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-      default: return dense_bf_ks<8, 2, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+      case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
+      case 64: return dense_bf_ks<2, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
+      case 128: return dense_bf_ks<4, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
+      default: return dense_bf_ks<8, 2, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
     }
   }
   switch (K) {
-    case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-    case 64: return dense_bf_ks<2, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-    case 128: return dense_bf_ks<4, 2, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
-    default: return dense_bf_ks<8, 1, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, st);
+    case 32: return dense_bf_ks<1, 8, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
+    case 64: return dense_bf_ks<2, 4, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
+    case 128: return dense_bf_ks<4, 2, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
+    default: return dense_bf_ks<8, 1, BWD, NP>(x, n, x_stride, W, bias, M, act, y, aprev, accumulate, xo, st);
   }
 }
 
@@ -2116,11 +2175,11 @@ hipError_t launch_dense_h16(const float* x, int64_t n, int K, int x_stride, cons
 }
 
 hipError_t launch_dense_h16_t(const float* dz, int64_t n, int K, const void* Wth, int M, float* out, int accumulate,
-                              int act, const float* aprev, hipStream_t st) {
+                              int act, const float* aprev, hipStream_t st, OuterRows xo) {
   if (n == 0) return hipSuccess;
   if (!dense_bf_supported(K, M) || !Wth) return hipErrorInvalidValue;
   return dense_bf_any<true, 2>(dz, n, K, K, Wth, nullptr, M, act < 0 ? IGN_K_ACT_LINEAR : act, out,
-                               act < 0 ? nullptr : aprev, accumulate, st);
+                               act < 0 ? nullptr : aprev, accumulate, st, xo);
 }
 
 // Scaled fp16 pieces of a Dense kernel for dense_bf_kernel<.., NP = 2> (natural k; trans: of W^T),
@@ -2172,11 +2231,11 @@ hipError_t launch_pack_dense_f16(const float* W, void* out, int IN, int OUT, int
 }
 
 hipError_t launch_dense_bf_t(const float* dz, int64_t n, int K, const void* Wtbf, int M, float* out, int accumulate,
-                             int act, const float* aprev, hipStream_t st) {
+                             int act, const float* aprev, hipStream_t st, OuterRows xo) {
   if (n == 0) return hipSuccess;
   if (!dense_bf_supported(K, M) || !Wtbf) return hipErrorInvalidValue;
   return dense_bf_any<true>(dz, n, K, K, Wtbf, nullptr, M, act < 0 ? IGN_K_ACT_LINEAR : act,
-                            out, act < 0 ? nullptr : aprev, accumulate, st);
+                            out, act < 0 ? nullptr : aprev, accumulate, st, xo);
 }
 
 hipError_t launch_pack_dense_bf16_t(const float* W, void* out, int IN, int OUT, hipStream_t st) {
@@ -2301,18 +2360,23 @@ hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t
   return hipGetLastError();
 }
 
+bool tsgemm_bf_lds_ok(int M, int N) {
+  return M > 0 && N > 0 && M % 64 == 0 && N % 64 == 0 && N <= 256 && (M / 64) * (N / 64) >= 4;
+}
+
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
-                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st) {
+                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st, OuterRows bo) {
   // tsgemm_bf_lds where the pieces are shared by >= 4 tiles: 1.78 -> 1.51 ms for the readout's 256 x 256
   // weight gradient, bitwise the same partials
-  if (M > 0 && N > 0 && M % 64 == 0 && N % 64 == 0 && N <= 256 && (M / 64) * (N / 64) >= 4) {
+  if (tsgemm_bf_lds_ok(M, N)) {
     const int tiles_m = M / 64, tiles_n = N / 64;
     const int mtb = std::min(std::min(tiles_m, 8 / tiles_n), (kTsLdsCols - N) / 64);
     const dim3 g2((unsigned)chunks, (unsigned)((tiles_m + mtb - 1) / mtb));
     hipLaunchKernelGGL(tsgemm_bf_lds_kernel, g2, dim3(512), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, mtb,
-                       part);
+                       part, bo);
     return hipGetLastError();
   }
+  if (bo.s) return hipErrorInvalidValue;   // the on-the-fly B is the LDS kernel's only
   if (ones && M > 0 && M % 64 == 0) tiles = (M / 64) * ((N + 63) / 64);   // the ones row folded (kernel)
   dim3 grid((unsigned)chunks, (unsigned)((tiles + wpb - 1) / wpb));
   hipLaunchKernelGGL(tsgemm_bf_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, part);

@@ -321,6 +321,43 @@ def test_split_bf16_backward_matches_f32(monkeypatch, switch):
 
 
 @pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_output_layer_gradient_formed_on_the_fly(monkeypatch, kind):
+    """The 1-unit output layer's backward rows (dz[r][k] = dz_out[r] w3[k] selu'(a2[r][k])) formed
+    inside the layer below's weight-gradient and input-gradient kernels (default) instead of
+    materialised by row_outer_t (IGN_FUSE_OUTER_BWD=0): the same arithmetic, bitwise-equal
+    gradients, and within the tolerance of float64 autograd."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, "nsfnet", 6)
+    prm = MPPlan.from_model_info(mi).init_params(17, bias_scale=0.1)
+    eng, _, _, _, _, g1 = _engine_grads(desc, dims, graphs, labels, prm)
+    g1 = g1.cpu().numpy()
+    monkeypatch.setenv("IGN_FUSE_OUTER_BWD", "0")
+    g0 = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    np.testing.assert_array_equal(g1, g0)
+    assert _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g1, eng.layout) <= GTOL
+
+
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_training_forward_fused_readout(monkeypatch, kind):
+    """The training forward's readout on the inference kernel (readout_h16 writing both layers'
+    activations, IGN_TRAIN_FUSED_READOUT, default on) against the per-layer row GEMMs: bitwise
+    deterministic, the switch takes effect, and both within the tolerance of float64 autograd."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, "nsfnet", 4)
+    prm = MPPlan.from_model_info(mi).init_params(19, bias_scale=0.1)
+    eng, _, p1, _, _, g1 = _engine_grads(desc, dims, graphs, labels, prm)
+    g1 = g1.cpu().numpy()
+    np.testing.assert_array_equal(g1, _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy())
+    monkeypatch.setenv("IGN_TRAIN_FUSED_READOUT", "0")
+    _, _, p0, _, _, g0 = _engine_grads(desc, dims, graphs, labels, prm)
+    g0 = g0.cpu().numpy()
+    assert not np.array_equal(g0, g1)
+    np.testing.assert_allclose(p1, p0, rtol=1e-5, atol=1e-5)
+    e1 = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g1, eng.layout)
+    e0 = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, g0, eng.layout)
+    print("vs float64 autograd: fused readout %.3g, per layer %.3g" % (e1, e0))
+    assert e1 <= GTOL and e0 <= GTOL
+
+
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
 def test_pooled_buffers_reused_and_poisoned(monkeypatch, kind):
     """Batch and training buffers come from the plan's device-memory cache (devpool.cpp): a batch
     built after another was destroyed reuses its blocks.  With IGN_POOL_POISON=1 every scratch
