@@ -632,7 +632,20 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
     f4 acc = accumulate ? ld4(out + r * cols + c) : f4{0, 0, 0, 0};
     const int k1 = ptr[r + 1];
     int k = ptr[r];
-    // four rows in flight; the additions keep the CSR order (bitwise the same as one at a time)
+    // eight (then four) rows in flight; the additions keep the CSR order (bitwise the same as one
+    // at a time)
+#ifndef IGN_GATHER4   // A/B: four rows in flight only
+    for (; k + 8 <= k1; k += 8) {
+      int i8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) i8[u] = idx[k + u];
+      f4 v8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v8[u] = ld4(in + (int64_t)i8[u] * cols + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v8[u];
+    }
+#endif
     for (; k + 4 <= k1; k += 4) {
       const int i0 = idx[k], i1 = idx[k + 1], i2 = idx[k + 2], i3 = idx[k + 3];
       const f4 v0 = ld4(in + (int64_t)i0 * cols + c), v1 = ld4(in + (int64_t)i1 * cols + c);

@@ -197,7 +197,8 @@ typedef struct {
  * over every timed launch since the last ign_plan_set_timing / ign_plan_set_timing_kinds.  The
  * event pairs are resolved lazily: ign_stats waits for the plan's stream and then reads them, so
  * it blocks, and like every call on a plan it must come from the plan's one host thread.
- * kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 project, 5 other */
+ * kind: 0 init_state, 1 seq_gru, 2 sum_gru, 3 readout, 4 project, 5 other, 6 mp_resident (round 4:
+ * the graph-resident forward, every MP of every iteration in one launch) */
 typedef struct {
   int32_t kinds;
   int64_t launches[8];

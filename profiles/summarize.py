@@ -12,7 +12,8 @@ from collections import defaultdict
 import re
 
 # first match wins: the training kernels before the forward ones whose names they extend
-KINDS = {"seq_gru_bwd": r"seq_gru_bwd_kernel", "sum_gru_bwd": r"sum_gru_bwd_kernel",
+KINDS = {"mp_resident": r"resident_forward_kernel",
+         "seq_gru_bwd": r"seq_gru_bwd_kernel", "sum_gru_bwd": r"sum_gru_bwd_kernel",
          "csr_gather_add": r"csr_gather_add_kernel", "dense_bf": r"dense_bf_kernel", "tsgemm_bf": r"tsgemm_bf_kernel",
          "seq_gru": r"seq_gru\w*_kernel", "sum_gru": r"sum_gru\w*_kernel", "readout": r"readout\w*_kernel",
          "project": r"project_kernel", "init_state": r"init_state_kernel"}

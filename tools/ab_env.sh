@@ -10,7 +10,7 @@ for r in $(seq $REPS); do
     python - "$VAR=$v" $f.json <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
-wk = d["roofline"]["warmup_kernels"]
+wk = (d.get("roofline") or {}).get("warmup_kernels", {})
 print(sys.argv[1], "ms/step %.4f" % d["ms_per_step"], " ".join("%s %.4f" % (k, v["ms_total"] / max(1, v["launches"])) for k, v in wk.items()))
 PY
   done

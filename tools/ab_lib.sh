@@ -10,8 +10,8 @@ for r in $(seq $REPS); do
     python - "$n" $f.json <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
-wk = d["roofline"]["warmup_kernels"]
-print("%-10s" % sys.argv[1], "ms/step %.4f" % d["ms_per_step"], "dom %.4f" % d["roofline"]["avg_launch_ms"],
+wk = (d.get("roofline") or {}).get("warmup_kernels", {})
+print("%-10s" % sys.argv[1], "ms/step %.4f" % d["ms_per_step"], "dom %.4f" % (d.get("roofline") or {}).get("avg_launch_ms", 0),
       " ".join("%s %.4f" % (k, v["ms_total"] / max(1, v["launches"])) for k, v in wk.items()), flush=True)
 PY
   done
