@@ -135,13 +135,11 @@ struct OuterRows {
   const float* s = nullptr;   // [rows] the output layer's pre-activation gradient
   const float* w = nullptr;   // [K] its weights
   int act = 0;                // the activation of raw
+  float* out = nullptr;       // where the formed rows are also written (may be raw: in place)
 };
-// split-bf16 form of the training row contraction (train_kernels.hip tsgemm; same grid and partials);
-// bo: B formed on the fly (only where tsgemm_bf_lds_ok)
-bool tsgemm_bf_lds_ok(int M, int N);
+// split-bf16 form of the training row contraction (train_kernels.hip tsgemm; same grid and partials)
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
-                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st,
-                            OuterRows bo = OuterRows{});
+                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st);
 hipError_t launch_sum_gru(const SumGruArgs& args, int din, int h, int variant, hipStream_t st);
 
 // Windowed sum (AUX:254-262 for single-source sum MPs of graph-local batches): one workgroup per

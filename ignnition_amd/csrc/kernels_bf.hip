@@ -1143,11 +1143,10 @@ __device__ __forceinline__ float act_grad_out(float a, int act) {   // act' thro
 // old kernel split every value once per wave that used it (4 times at 256 x 256).  Same products in
 // the same order per accumulator and the same column-sum order: bitwise the old kernel's partials.
 constexpr int kTsLdsCols = 384;   // A columns of the block + N
-// bo (optional): B formed on the fly from the output layer's gradient, as dense_bf_kernel's xo
 __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restrict__ A, int lda,
                                                             const float* __restrict__ B, int ldb, int64_t n_rows,
                                                             int M, int N, int ones, int64_t chunk, int mtb,
-                                                            float* __restrict__ part, OuterRows bo) {
+                                                            float* __restrict__ part) {
   constexpr int NTH = 512, KP = (kTsLdsCols * 4 + NTH - 1) / NTH;
   __shared__ u4v sp[2 * 3 * kTsLdsCols * 4];   // two buffers of [piece][column][row group]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1174,12 +1173,6 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
     ld[k] = col < AC ? lda : ldb;
   }
   float v[KP][8];
-  float bw[KP];   // bo: the output layer's weight of the thread's B columns
-#pragma unroll
-  for (int k = 0; k < KP; ++k) {
-    const int col = (tid + NTH * k) % COLS;
-    bw[k] = bo.s && col >= AC ? bo.w[col - AC] : 0.f;
-  }
   auto load = [&](int64_t r) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < KP; ++k)
@@ -1188,20 +1181,6 @@ __global__ __launch_bounds__(512) void tsgemm_bf_lds_kernel(const float* __restr
         const int64_t rr = r + 8 * gp[k] + jj;
         v[k][jj] = (pok[k] && rr < r1) ? src[k][rr * ld[k]] : 0.f;
       }
-    if (bo.s) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        const int col = (tid + NTH * k) % COLS;
-        if (col < AC) continue;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const int64_t rr = r + 8 * gp[k] + jj;
-          float sq = 0.f;
-          sq += (pok[k] && rr < r1 ? bo.s[rr] : 0.f) * bw[k];
-          v[k][jj] = sq * act_grad_out(v[k][jj], bo.act);
-        }
-      }
-    }
   };
   float cs[KP] = {};
   f4 acc[4][4];
@@ -1861,9 +1840,10 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
 // (row_gemm_t's contract; bias unused, ACT = the activation whose derivative is applied).
 // xo (BWD only, optional): the input rows are the backward of a 1-unit output layer, formed on the
 // fly: x[r][k] = (0 + xo.s[r] * xo.w[k]) * act'(x_raw[r][k]) with x_raw the layer's output
-// activations (row_outer_t's arithmetic, so the materialised dz rows are never written)
+// activations (row_outer_t's arithmetic), and written to xo.out for the layer's weight gradient
+// (xo.out may be x_raw itself: each element is read and then written by the same lane, once)
 template <int KS, int G, int ACT, bool BWD = false, int NP = 3>
-__global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__ x, int64_t n, int x_stride,
+__global__ __launch_bounds__(512) void dense_bf_kernel(const float* x, int64_t n, int x_stride,
                                                        const void* __restrict__ Wf, const float* __restrict__ bias,
                                                        int M, float* __restrict__ y, const float* __restrict__ aprev,
                                                        int accumulate, OuterRows xo) {
@@ -1901,6 +1881,7 @@ __global__ __launch_bounds__(512) void dense_bf_kernel(const float* __restrict__
         sq += xsr * w[q];
         o[q] = sq * act_grad_out(v[q], xo.act);
       }
+      if (xo.out) st4(xo.out + r * (int64_t)x_stride + c0, o);   // for the weight gradient (may be x itself)
       return o;
     };
     if constexpr (NP == 3) {
@@ -2360,23 +2341,18 @@ hipError_t launch_sum_gru_bf(const SumGruArgs& args, int din, int h, hipStream_t
   return hipGetLastError();
 }
 
-bool tsgemm_bf_lds_ok(int M, int N) {
-  return M > 0 && N > 0 && M % 64 == 0 && N % 64 == 0 && N <= 256 && (M / 64) * (N / 64) >= 4;
-}
-
 hipError_t launch_tsgemm_bf(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N, int ones,
-                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st, OuterRows bo) {
+                            int64_t chunk, int64_t chunks, int tiles, int wpb, float* part, hipStream_t st) {
   // tsgemm_bf_lds where the pieces are shared by >= 4 tiles: 1.78 -> 1.51 ms for the readout's 256 x 256
   // weight gradient, bitwise the same partials
-  if (tsgemm_bf_lds_ok(M, N)) {
+  if (M > 0 && N > 0 && M % 64 == 0 && N % 64 == 0 && N <= 256 && (M / 64) * (N / 64) >= 4) {
     const int tiles_m = M / 64, tiles_n = N / 64;
     const int mtb = std::min(std::min(tiles_m, 8 / tiles_n), (kTsLdsCols - N) / 64);
     const dim3 g2((unsigned)chunks, (unsigned)((tiles_m + mtb - 1) / mtb));
     hipLaunchKernelGGL(tsgemm_bf_lds_kernel, g2, dim3(512), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, mtb,
-                       part, bo);
+                       part);
     return hipGetLastError();
   }
-  if (bo.s) return hipErrorInvalidValue;   // the on-the-fly B is the LDS kernel's only
   if (ones && M > 0 && M % 64 == 0) tiles = (M / 64) * ((N + 63) / 64);   // the ones row folded (kernel)
   dim3 grid((unsigned)chunks, (unsigned)((tiles + wpb - 1) / wpb));
   hipLaunchKernelGGL(tsgemm_bf_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, chunk, part);

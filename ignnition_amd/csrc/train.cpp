@@ -674,26 +674,25 @@ int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* gra
   const float* X = p->ro_in.size() > 1 ? t->ro_x : tensor(p->ro_in[0]);
   int zi = 0;
   HIP_TRY(launch_act_bwd(dpred, b->d_pred, P * p->dense[L - 1].out, p->dense[L - 1].act, t->dz[0], st));
-  // a 1-unit output layer's backward, dz[r][k] = dz_out[r] w[k] act'(a[r][k]), is not materialised
-  // when the layer below can form it on the fly in both of its contractions (its weight gradient on
-  // tsgemm_bf_lds, its input gradient on dense_bf): 2.56 GB of row_outer_t traffic less per step
+  // a 1-unit output layer's backward rows, dz[r][k] = dz_out[r] w[k] act'(a[r][k]), are formed by
+  // the layer below's input-gradient kernel (dense_bf) as it loads a, and written over a in place
+  // for that layer's weight gradient: row_outer_t's separate read of a is gone
   OuterRows xo{};
-  const float* xo_raw = nullptr;
   auto dense_t_bf = [&](const DenseP& d) { return p->train_dense_bf && (p->train_dense_h16 ? d.pk_ht >= 0 : d.pk_bft >= 0); };
   for (int l = L - 1; l >= 0; --l) {
     const DenseP& d = p->dense[l];
     const float* A = l == 0 ? X : t->act[l - 1];
-    const bool outer = xo.s != nullptr;   // this layer's dz is formed on the fly
-    HIP_TRY(launch_tsgemm_add(A, d.in, outer ? xo_raw : t->dz[zi], d.out, P, d.in, d.out, t->part, grads + d.off_w,
-                              d.use_bias ? grads + d.off_b : nullptr, st, xo));
-    if (l > 0 && d.out == 1 && d.in % 4 == 0 && p->fuse_outer_bwd && p->tsgemm_bf &&
-        tsgemm_bf_lds_ok(p->dense[l - 1].in, p->dense[l - 1].out) && dense_t_bf(p->dense[l - 1])) {
+    const bool outer = xo.s != nullptr;   // this layer's dz is formed by its dense_t from act[l]
+    if (!outer)
+      HIP_TRY(launch_tsgemm_add(A, d.in, t->dz[zi], d.out, P, d.in, d.out, t->part, grads + d.off_w,
+                                d.use_bias ? grads + d.off_b : nullptr, st));
+    if (l > 0 && d.out == 1 && d.in % 4 == 0 && p->fuse_outer_bwd && dense_t_bf(p->dense[l - 1])) {
       if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * l2_scale, (int64_t)d.in * d.out, st));
-      xo = OuterRows{t->dz[zi], p->d_params + d.off_w, p->dense[l - 1].act};
-      xo_raw = t->act[l - 1];
+      xo = OuterRows{t->dz[zi], p->d_params + d.off_w, p->dense[l - 1].act, t->act[l - 1]};
       continue;   // zi stays: dz[zi] holds dz_out for the layer below
     }
-    if (d.l2 != 0.f) HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * l2_scale, (int64_t)d.in * d.out, st));
+    if (!outer && d.l2 != 0.f)
+      HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * l2_scale, (int64_t)d.in * d.out, st));
     float* out;
     int act = -1, acc = 0;
     const float* aprev = nullptr;
@@ -707,18 +706,23 @@ int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* gra
       out = grad_of(p->ro_in[0]);
       acc = 1;
     }
+    const float* dzin = outer ? xo.out : t->dz[zi];
     if (p->train_dense_bf && p->train_dense_h16 && d.pk_ht >= 0)   // split-fp16 (x3)
-      HIP_TRY(launch_dense_h16_t(outer ? xo_raw : t->dz[zi], P, d.out, p->d_packed + d.pk_ht, d.in, out, acc, act, aprev,
-                                 st, xo));
+      HIP_TRY(launch_dense_h16_t(dzin, P, d.out, p->d_packed + d.pk_ht, d.in, out, acc, act, aprev, st, xo));
     else if (p->train_dense_bf && d.pk_bft >= 0)   // split-bf16, fp32-exact operands
-      HIP_TRY(launch_dense_bf_t(outer ? xo_raw : t->dz[zi], P, d.out, p->d_packed + d.pk_bft, d.in, out, acc, act, aprev,
-                                st, xo));
+      HIP_TRY(launch_dense_bf_t(dzin, P, d.out, p->d_packed + d.pk_bft, d.in, out, acc, act, aprev, st, xo));
     else if (outer)
       return fail(IGN_ERR_RUNTIME, "on-the-fly output-layer gradient without a dense_bf backward");
     else if (d.pk_wt >= 0)
       HIP_TRY(launch_row_gemm_t(t->dz[zi], P, d.out, p->d_packed + d.pk_wt, d.in, out, acc, act, aprev, st));
     else
       HIP_TRY(launch_row_gemm_t_generic(t->dz[zi], P, d.out, p->d_params + d.off_w, d.in, out, acc, act, aprev, st));
+    if (outer) {   // the weight gradient on the rows dense_t just wrote over act[l], then its l2 term
+      HIP_TRY(launch_tsgemm_add(A, d.in, xo.out, d.out, P, d.in, d.out, t->part, grads + d.off_w,
+                                d.use_bias ? grads + d.off_b : nullptr, st));
+      if (d.l2 != 0.f)
+        HIP_TRY(launch_axpy(grads + d.off_w, p->d_params + d.off_w, 2.f * d.l2 * l2_scale, (int64_t)d.in * d.out, st));
+    }
     xo = OuterRows{};
     zi = 1 - zi;
   }

@@ -2,7 +2,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include "kernels.h"   // OuterRows
 
 // Backward of the ordered update (reverse-time GRU, AUX:767-796).
 struct SeqBwdArgs {
@@ -107,7 +106,7 @@ void set_tsgemm_bf(bool on);
 hipError_t launch_partials_reduce_add(float* part, int64_t nchunks, int M, int N, int ones, float* C, float* Cb,
                                       hipStream_t st);
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
-                             float* part, float* C, float* Cb, hipStream_t st, OuterRows bo = OuterRows{});
+                             float* part, float* C, float* Cb, hipStream_t st);
 // forward Dense layer for the training readout: y = act(x W + b), MFMA when packed fragments exist
 bool dense_fwd_supported(int K, int M);
 hipError_t launch_dense_fwd(const float* x, int64_t n, int K, int x_stride, const float* Wp, const float* W,

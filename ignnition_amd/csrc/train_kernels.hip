@@ -1332,7 +1332,7 @@ int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N) {
 }
 
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
-                             float* part, float* C, float* Cb, hipStream_t st, OuterRows bo) {
+                             float* part, float* C, float* Cb, hipStream_t st) {
   if (n_rows == 0) return hipSuccess;
   const int ones = Cb != nullptr;
   const TsPlan p = ts_plan(n_rows, M, N, ones);
@@ -1342,9 +1342,7 @@ hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, i
   // split-bf16 contraction (kernels_bf.hip) when A is present; the plan's IGN_TSGEMM_BF=0 keeps f32 MFMA
   hipError_t e;
   if (g_tsgemm_bf && A) {
-    e = launch_tsgemm_bf(A, lda, B, ldb, n_rows, M, N, ones, p.chunk, p.chunks, p.tiles, wpb, part, st, bo);
-  } else if (bo.s) {
-    return hipErrorInvalidValue;   // the on-the-fly B is the split-bf16 LDS kernel's only
+    e = launch_tsgemm_bf(A, lda, B, ldb, n_rows, M, N, ones, p.chunk, p.chunks, p.tiles, wpb, part, st);
   } else {
     hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
     e = hipGetLastError();

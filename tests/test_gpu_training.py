@@ -323,9 +323,9 @@ def test_split_bf16_backward_matches_f32(monkeypatch, switch):
 @pytest.mark.parametrize("kind", ["routenet", "qsize"])
 def test_output_layer_gradient_formed_on_the_fly(monkeypatch, kind):
     """The 1-unit output layer's backward rows (dz[r][k] = dz_out[r] w3[k] selu'(a2[r][k])) formed
-    inside the layer below's weight-gradient and input-gradient kernels (default) instead of
-    materialised by row_outer_t (IGN_FUSE_OUTER_BWD=0): the same arithmetic, bitwise-equal
-    gradients, and within the tolerance of float64 autograd."""
+    by the layer below's input-gradient kernel as it loads a2, and written over a2 for that layer's
+    weight gradient (default), instead of by row_outer_t (IGN_FUSE_OUTER_BWD=0): the same
+    arithmetic, bitwise-equal gradients, and within the tolerance of float64 autograd."""
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, "nsfnet", 6)
     prm = MPPlan.from_model_info(mi).init_params(17, bias_scale=0.1)
     eng, _, _, _, _, g1 = _engine_grads(desc, dims, graphs, labels, prm)
