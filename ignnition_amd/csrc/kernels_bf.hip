@@ -1651,11 +1651,14 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
   load_x(blockIdx.x);
   for (int64_t grp = blockIdx.x; grp < n_groups; grp += (int64_t)gridDim.x) {
   const int64_t r0 = (grp * WAVES + wave) * (16 * RT) + j;
-  // per row tile: its max |x| and the scales derived from it (xl: loaded during the previous group)
+  // per row tile: its max |x| and the scales derived from it (xl: loaded during the previous group).
+  // The max is floored at 1 (as the ordered update's tile scale): every tile whose inputs lie in
+  // [-1, 1] gets the same scales, so a row's bits do not depend on which rows share its tile (the
+  // batch composition, an edge-cut partition's first row)
   float mx[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
-    mx[t] = 0.f;
+    mx[t] = 1.f;
 #pragma unroll
     for (int s = 0; s < KS1; ++s)
 #pragma unroll
@@ -1724,7 +1727,11 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           v[t][4 * half + q] = act_scaled<ACT>(acc[t][q], c1[t], k, c1[t] * LOG2E, LA * S[t], S[t]);
+#ifndef IGN_RO_SAVE1_OFF
         if constexpr (SAVE) {
+#else
+        if constexpr (false) {
+#endif
           const int64_t r = r0 + 16 * t;
           const float iS = __int_as_float(254 - ((__float_as_int(S[t]) >> 23) & 255) << 23);   // 1 / S, exact
           if (r < a.n_rows)
@@ -1803,9 +1810,15 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
       for (int q = 0; q < 4; ++q) {
         av[q] = act_scaled<ACT>(acc[t][q], cSS[t], ACT == IGN_K_ACT_SELU ? LAM : 1.0f, cSS[t] * LOG2E, LA * SS[t],
                                 SS[t]);
-        y[t] += w3[q] * av[q];
+        // an explicit fma: a contractable multiply-add may be lowered fused for one row tile and
+        // unfused for the other (it was, in the SAVE form), which made a row's bits depend on its tile
+        y[t] = fmaf(w3[q], av[q], y[t]);
       }
+#ifndef IGN_RO_SAVE2_OFF
       if constexpr (SAVE) {
+#else
+      if constexpr (false) {
+#endif
         const int64_t r = r0 + 16 * t;
         if (r < a.n_rows) st4(a.save2 + r * 256 + 16 * v + 4 * g, av * cSS[t]);
       }

@@ -357,6 +357,28 @@ def test_training_forward_fused_readout(monkeypatch, kind):
     assert e1 <= GTOL and e0 <= GTOL
 
 
+def test_readout_bits_do_not_depend_on_the_row_tile():
+    """A row's prediction is the same bits whichever rows share its 16-row tile: the synthetic graph
+    alone and after an 8-node graph in the same batch (every row shifted by 8), for the training
+    forward (readout_h16 with activation saves) and the inference forward.  (The SAVE form once
+    lowered one tile's layer-2 multiply-add fused and the other's unfused; tools/probes/ro_save_probe.py.)"""
+    desc, dims, _, graphs, _ = workloads.make_synthetic_inputs(n_nodes=2000, hidden=32, iterations=2, window=96)
+    small = synthetic.synthetic_graph_arrays(n_nodes=8, window=4, graph_id=7)
+    small.pop("target")
+    plan = MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims))
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(21, bias_scale=0.1))
+    for train in (True, False):
+        outs = []
+        for gs in (graphs, [small] + graphs):
+            b = Batch(eng, gs)
+            if train:
+                b.enable_training()
+            outs.append((b.forward_train() if train else b.forward()).reshape(-1).copy())
+            b.close()
+        np.testing.assert_array_equal(outs[0], outs[1][8:])
+
+
 @pytest.mark.parametrize("kind", ["routenet", "qsize"])
 def test_pooled_buffers_reused_and_poisoned(monkeypatch, kind):
     """Batch and training buffers come from the plan's device-memory cache (devpool.cpp): a batch
