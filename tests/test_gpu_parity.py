@@ -516,7 +516,8 @@ def test_resident_forward_batch_invariance():
     np.testing.assert_array_equal(mixed[:res.size], res)
 
 
-def test_timing_kinds_mask():
+def test_timing_kinds_mask(monkeypatch):
+    monkeypatch.setenv("IGN_RESIDENT", "0")   # the batched launches (the resident forward is one kind)
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
     plan = MPPlan.from_model_info(mi)
     eng = Engine(plan, 0)
