@@ -478,11 +478,11 @@ def main():
 
         import torch
         from ignnition_amd import generate_model as gm
-        from ignnition_amd import synthetic
+        from ignnition_amd import synthetic as synth_data   # (the name `synthetic` is the --model flag here)
         from ignnition_amd.training import Trainer
         torch.cuda.set_device(device if world > 1 else 0)
         tmp = tempfile.mkdtemp(prefix="ign_bench_")
-        synthetic.write_tar_dataset(synthetic.dataset(args.topology, len(ids), first_id=ids[0]), os.path.join(tmp, "train"))
+        synth_data.write_tar_dataset(synth_data.dataset(args.topology, len(ids), first_id=ids[0]), os.path.join(tmp, "train"))
         gm.register_user_functions(workloads.USER_FUNCTIONS)
         gm.set_model_info(mi)
         trainer = Trainer(mi, params=prm, device=device if world > 1 else 0, dist=dist)
