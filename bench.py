@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=0,
                     help="forward: the rank's graphs as this many sub-batches, one engine / HIP stream each, "
                          "launched back to back in every step (their kernels co-run); 0 = auto: 4 for graphs "
-                         "of fewer than 1000 paths (GEANT2: 0.872 against 0.906 ms/step with 2), else 2")
+                         "of fewer than 1000 paths or models of 3+ MPs per iteration (Q-size), else 2")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -437,9 +437,12 @@ def main():
     engines.append(eng)
     t_build = time.perf_counter()
     halo_rows = 0
-    if args.streams <= 0:   # auto: more, smaller sub-batches for small graphs, whose kernels are short
+    if args.streams <= 0:
+        # auto: more, smaller sub-batches where the kernels are short -- small graphs (GEANT2, NSFNET)
+        # or a step of three or more MPs per iteration (Q-size: 4.15-4.18 ms/step with 4 streams
+        # against 4.39-4.41 with 2; RouteNet synth50 is flat from 2 to 4: profiles/r04/streams/)
         sizes = [int(np.asarray(g[k]).reshape(())) for g in graphs[:1] for k in g if k.startswith("num_")]
-        args.streams = 4 if sizes and max(sizes) < 1000 else 2
+        args.streams = 4 if (sizes and max(sizes) < 1000) or len(plan.mps) >= 3 else 2
     if synthetic and world > 1:
         import torch
         from ignnition_amd import partition
