@@ -218,7 +218,11 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_HIP_GRAPH")) p->use_graph = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_VARIANT")) p->sum_variant = atoi(v) == 7 || atoi(v) == 8 ? atoi(v) : 3;
   if (const char* v = getenv("IGN_SUM_WINDOW")) p->sum_window = atoi(v);
-  if (const char* v = getenv("IGN_RESIDENT")) p->resident = atoi(v) != 0;
+  if (const char* v = getenv("IGN_RESIDENT")) {   // 0 off; 1 default; 2 also force the global-path form
+    p->resident = atoi(v) != 0;
+    p->resident_path_global = atoi(v) == 2;
+  }
+  if (const char* v = getenv("IGN_RESIDENT_PG")) p->resident_pg = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_H16")) p->train_dense_h16 = atoi(v) != 0;
@@ -589,7 +593,12 @@ static bool resident_plan_ok(const ign_plan* p) {
   return p->ents[path].feature_total <= 32 && p->ents[link].feature_total <= 32;
 }
 
-static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs, int64_t codes) {
+// dynamic LDS of one graph: path_global keeps the path states, codes and message rows in global
+// memory (resident_forward_kernel<true>)
+static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs, int64_t codes, bool path_global) {
+  if (path_global)
+    return (size_t)(links * kResidentStateStride + (links + 1) * kResidentTableStride) * sizeof(float) +
+           (size_t)(links + 1) * sizeof(int32_t);
   return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
              sizeof(float) +
          (size_t)(links + 1) * sizeof(int32_t) + (size_t)(msgs + codes) * sizeof(uint16_t);
@@ -642,7 +651,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
   hvec<int32_t> ptile_off(G + 1, 0), hdr, lcode_off(G + 1, 0);
   hvec<uint16_t> lcode;
-  size_t lds = 0;
+  size_t lds = 0, lds_pg = 0;
   for (int g = 0; g < G; ++g) {
     const int64_t L = lo[g + 1] - lo[g];
     const int64_t n = (int64_t)pp[g].size(), np = (n + 15) / 16 * 16;
@@ -673,9 +682,15 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     }
     ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
     lcode_off[g + 1] = (int32_t)lcode.size();
-    lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], lcode_off[g + 1] - lcode_off[g]));
+    lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], lcode_off[g + 1] - lcode_off[g], false));
+    lds_pg = std::max(lds_pg, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], 0, true));
   }
-  if (lds > kResidentMaxDynLds) return IGN_OK;
+  // every state in LDS where the largest graph's fit, else the path states in global memory
+  const bool pg = lds > kResidentMaxDynLds || p->resident_path_global;
+  if (pg) {
+    if (lds_pg > kResidentMaxDynLds || !p->resident_pg) return IGN_OK;
+    lds = lds_pg;
+  }
   std::vector<int64_t> pov(po.begin(), po.end()), lov(lo.begin(), lo.end());
   int rc;
   if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_link_off, lov)) ||
@@ -685,6 +700,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       (rc = dev_upload(b, &b->d_res_lcode, lcode)))
     return rc;
   b->res_lds = lds;
+  b->res_pg = pg;
   // one launch reads the features, the tile headers (T times, from L2 after the first), the step
   // codes, the sum MP's CSR and writes the final states once: the HBM floor
   const int64_t P = b->rows[path], L = b->rows[link];
@@ -1684,7 +1700,7 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.T = p->T;
   Timer tm{p};
   tm.begin(K_RESIDENT, b->res_flops, b->res_bytes);
-  HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, p->stream));
+  HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, b->res_pg, p->stream));
   tm.end();
   b->cur[path] = 0;
   b->cur[link] = 0;

@@ -266,6 +266,8 @@ struct ign_plan {
   bool train_seq_h16 = true;      // training forward's ordered update on split-fp16 (IGN_TRAIN_SEQ_H16=0: bf16)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
   bool resident = true;           // graph-resident forward for small RouteNet-shaped graphs (IGN_RESIDENT=0: off)
+  bool resident_pg = true;        // ... with the path states in global memory where they do not fit LDS (IGN_RESIDENT_PG)
+  bool resident_path_global = false;   // IGN_RESIDENT=2: that form for every eligible batch (tests)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
                                   // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
                                   // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);
@@ -312,6 +314,7 @@ struct ign_batch {
   // per-graph tile headers, the sum MP's per-graph CSR (local rows); dynamic LDS of the largest graph
   bool resident = false;
   size_t res_lds = 0;
+  bool res_pg = false;            // resident_forward_kernel<true>: path states in the state buffer
   double res_bytes = 0, res_flops = 0;   // per launch: HBM bytes it must move, FLOPs it executes
   int64_t* d_res_path_off = nullptr;
   int64_t* d_res_link_off = nullptr;

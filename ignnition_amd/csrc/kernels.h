@@ -201,7 +201,8 @@ struct ResidentArgs {
   const float* proj_Wf;       // ... and as project_kernel's f32 fragments (the iteration-0 projection)
   int T;
 };
-hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, hipStream_t st);
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, bool path_global,
+                                   hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

@@ -125,6 +125,10 @@ __device__ __forceinline__ void project_row_f32(const ResidentArgs& a, const f4 
 
 }  // namespace
 
+// PG: the path states stay in the batch's state buffer in HBM / L2 (rows of 32 floats) and the
+// codes and message rows are read from global memory: the form for graphs whose path states do
+// not fit (synth50: 2 450 paths); LDS then holds the link states, the projected table and the CSR
+template <bool PG>
 __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs a) {
   constexpr int H = 32, NT = 2, KS = 1, NF = 6 * NT * KS;   // U's fp16 pieces: 2 pieces x 3 gates x NT
   constexpr int NFB = 18;                                     // bf16 pieces of W / U per matrix (g32)
@@ -136,14 +140,17 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   const int gph = blockIdx.x;
   const int64_t p0 = a.path_off[gph], P = a.path_off[gph + 1] - p0;
   const int64_t l0 = a.link_off[gph], L = a.link_off[gph + 1] - l0;
-  float* hP = dyn;
-  float* hL = hP + P * SP;
+  constexpr int SPP = PG ? H : SP;   // row stride of the path states
+  float* hP = PG ? a.path_state + p0 * H : dyn;
+  float* hL = PG ? dyn : hP + P * SP;
   float* tab = hL + L * SP;
   int* smp = reinterpret_cast<int*>(tab + (L + 1) * ST);   // the sum MP's CSR by local link row
-  uint16_t* sms = reinterpret_cast<uint16_t*>(smp + L + 1);
+  uint16_t* sms_l = reinterpret_cast<uint16_t*>(smp + L + 1);
   const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
-  uint16_t* scd = sms + M;   // the ordered MP's local step codes
+  uint16_t* scd_l = sms_l + M;   // the ordered MP's local step codes
   const int64_t cd0 = a.lcode_off[gph], NC = a.lcode_off[gph + 1] - cd0;
+  const uint16_t* sms = PG ? a.lmsg_src + ms0 : sms_l;
+  const uint16_t* scd = PG ? a.lcode + cd0 : scd_l;
   float* xs = tab;   // phase B's message sums [L][SP] alias the (consumed) projected table
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -163,7 +170,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   for (int64_t i = tid; i < P * H; i += 64 * kW) {
     const int64_t r = i / H;
     const int c = (int)(i - r * H);
-    hP[r * SP + c] = c < a.path_F ? a.path_feat[(p0 + r) * a.path_F + c] : 0.f;
+    hP[r * SPP + c] = c < a.path_F ? a.path_feat[(p0 + r) * a.path_F + c] : 0.f;
   }
   for (int64_t i = tid; i < L * H; i += 64 * kW) {
     const int64_t r = i / H;
@@ -174,8 +181,10 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   {
     const int* gp = a.lmsg_ptr + l0 + gph;
     for (int64_t i = tid; i <= L; i += 64 * kW) smp[i] = gp[i];
-    for (int64_t i = tid; i < M; i += 64 * kW) sms[i] = a.lmsg_src[ms0 + i];
-    for (int64_t i = tid; i < NC; i += 64 * kW) scd[i] = a.lcode[cd0 + i];
+    if constexpr (!PG) {
+      for (int64_t i = tid; i < M; i += 64 * kW) sms_l[i] = a.lmsg_src[ms0 + i];
+      for (int64_t i = tid; i < NC; i += 64 * kW) scd_l[i] = a.lcode[cd0 + i];
+    }
   }
   __syncthreads();
   const int64_t nlt = (L + 15) / 16;   // link tiles
@@ -220,11 +229,11 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       const int Lr = hd[1];
       const bool valid = Lr > 0;   // tile padding: length 0
       const int64_t rl = valid ? hd[0] : 0;
-      const uint16_t* codes = scd + hd[2];
+      const int cbase = hd[2];   // (an index, not a pointer: one VGPR live through the tile)
       f4 h[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const f4 v = lds4(hP + rl * SP + 16 * t + 4 * g);
+        const f4 v = lds4(hP + rl * SPP + 16 * t + 4 * g);
         h[t] = valid ? v : f4{0, 0, 0, 0};
       }
       f4 x[3][NT];
@@ -236,7 +245,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
           for (int i = 0; i < NT; ++i) xx[G][i] = lds4(p + G * H + 16 * i);
       };
       load_x((uint32_t)hd[3], x);
-      uint32_t code = codes[1];
+      uint32_t code = scd[cbase + 1];
       // positions are sorted by length, descending, within the graph: lane 0 is the longest
       const int Lmax = __builtin_amdgcn_readfirstlane(Lr);
       float m = 1.0f;
@@ -316,11 +325,11 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         else step(t, x, std::true_type{});
         if (++t >= Lmax) break;
         load_x(code, x);
-        code = codes[t + 1];
+        code = scd[cbase + t + 1];
       }
       if (valid) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) lds4w(hP + rl * SP + 16 * t + 4 * g, h[t] * iS);
+        for (int t = 0; t < NT; ++t) lds4w(hP + rl * SPP + 16 * t + 4 * g, h[t] * iS);
       }
 #ifdef IGN_RES_STAMP
       ++n_at;
@@ -352,11 +361,11 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         for (int u = 0; u < 8; ++u) rr[u] = sms[m + u];
         f4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds4(hp + rr[u] * SP);
+        for (int u = 0; u < 8; ++u) v[u] = lds4(hp + rr[u] * SPP);
 #pragma unroll
         for (int u = 0; u < 8; ++u) x = x + v[u];
       }
-      for (; m < m1; ++m) x = x + lds4(hp + sms[m] * SP);
+      for (; m < m1; ++m) x = x + lds4(hp + sms[m] * SPP);
       lds4w(xs + ll * SP + 4 * c4, x);
     }
     __syncthreads();
@@ -476,11 +485,12 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   }
 #endif
   // the final states leave the workgroup (the readout and ign_batch_state read them)
-  for (int64_t i = tid; i < P * (H / 4); i += 64 * kW) {
-    const int64_t r = i / (H / 4);
-    const int c4 = (int)(i - r * (H / 4));
-    st4(a.path_state + (p0 + r) * H + 4 * c4, lds4(hP + r * SP + 4 * c4));
-  }
+  if constexpr (!PG)   // PG: the path states are already there
+    for (int64_t i = tid; i < P * (H / 4); i += 64 * kW) {
+      const int64_t r = i / (H / 4);
+      const int c4 = (int)(i - r * (H / 4));
+      st4(a.path_state + (p0 + r) * H + 4 * c4, lds4(hP + r * SP + 4 * c4));
+    }
   for (int64_t i = tid; i < L * (H / 4); i += 64 * kW) {
     const int64_t r = i / (H / 4);
     const int c4 = (int)(i - r * (H / 4));
@@ -488,16 +498,22 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   }
 }
 
-hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, hipStream_t st) {
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, bool path_global,
+                                   hipStream_t st) {
   if (n_graphs == 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(resident_forward_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResidentMaxDynLds);
-    if (e != hipSuccess) return e;
+    for (const void* k : {reinterpret_cast<const void*>(resident_forward_kernel<false>),
+                          reinterpret_cast<const void*>(resident_forward_kernel<true>)}) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResidentMaxDynLds);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
   if (lds_bytes > kResidentMaxDynLds) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(resident_forward_kernel, dim3((unsigned)n_graphs), dim3(64 * kW), lds_bytes, st, a);
+  if (path_global)
+    hipLaunchKernelGGL(resident_forward_kernel<true>, dim3((unsigned)n_graphs), dim3(64 * kW), lds_bytes, st, a);
+  else
+    hipLaunchKernelGGL(resident_forward_kernel<false>, dim3((unsigned)n_graphs), dim3(64 * kW), lds_bytes, st, a);
   return hipGetLastError();
 }

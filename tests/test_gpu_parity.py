@@ -448,14 +448,16 @@ def test_windowed_sum_matches_oracle(monkeypatch, window):
     np.testing.assert_array_equal(out, b.forward())
 
 
-@pytest.mark.parametrize("topo,n", [("geant2", 3), ("nsfnet", 2), ("mixed", 4)])
-def test_resident_forward_is_the_batched_forward(monkeypatch, topo, n):
+@pytest.mark.parametrize("topo,n,mode", [("geant2", 3, "1"), ("nsfnet", 2, "1"), ("mixed", 4, "1"),
+                                         ("synth50", 2, "1"), ("geant2", 2, "2")])
+def test_resident_forward_is_the_batched_forward(monkeypatch, topo, n, mode):
     """The graph-resident forward (resident.hip: one workgroup per graph for all T iterations,
-    states and the projected table in LDS; the default for RouteNet-shaped models on graphs that
-    fit) computes each row with the batched kernels' arithmetic: predictions and final states
-    bitwise equal to the batched launches (IGN_RESIDENT=0), both within the parity tolerance of
-    the float64 oracle; one launch per forward (plus the readout), replayed bitwise from the
-    captured hipGraph."""
+    states and the projected table in LDS; the default for RouteNet-shaped models; synth50-size
+    graphs, and every graph under IGN_RESIDENT=2, keep their path states in global memory)
+    computes each row with the batched kernels' arithmetic: predictions and final states bitwise
+    equal to the batched launches (IGN_RESIDENT=0), both within the parity tolerance of the
+    float64 oracle; one launch per forward (plus the readout), replayed bitwise from the captured
+    hipGraph."""
     if topo == "mixed":
         desc, dims, mi = workloads.model("routenet")
         graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet" if g % 2 else "geant2", 40 + g)
@@ -466,7 +468,7 @@ def test_resident_forward_is_the_batched_forward(monkeypatch, topo, n):
     prm = plan.init_params(5, bias_scale=0.1)
     ref = DenseOracle(desc, dims, prm).forward(graphs)
     outs, states = {}, {}
-    for v in ("1", "0"):
+    for v in (mode, "0"):
         monkeypatch.setenv("IGN_RESIDENT", v)
         eng = Engine(plan, 0)
         eng.set_params(prm)
@@ -476,7 +478,7 @@ def test_resident_forward_is_the_batched_forward(monkeypatch, topo, n):
         st = eng.stats()
         eng.set_timing(False)
         np.testing.assert_array_equal(out, b.forward().reshape(-1))   # graph capture + replay
-        if v == "1":
+        if v != "0":
             assert st["mp_resident"]["launches"] == 1 and st["seq_gru"]["launches"] == 0, st
             assert st["sum_gru"]["launches"] == 0 and st["project"]["launches"] == 0, st
         else:
@@ -486,14 +488,17 @@ def test_resident_forward_is_the_batched_forward(monkeypatch, topo, n):
         b.close()
         eng.close()
         _close(out, ref)
-    np.testing.assert_array_equal(outs["1"], outs["0"])
+    np.testing.assert_array_equal(outs[mode], outs["0"])
     for e in ("path", "link"):
-        np.testing.assert_array_equal(states["1"][e], states["0"][e])
+        np.testing.assert_array_equal(states[mode][e], states["0"][e])
 
 
-def test_resident_forward_batch_invariance():
-    """A graph's predictions are the same bits alone, in a resident batch, and in a batch that
-    takes the batched path (a synth50 graph is too large for one workgroup's LDS)."""
+@pytest.mark.parametrize("pg", ["0", "1"])
+def test_resident_forward_batch_invariance(monkeypatch, pg):
+    """A graph's predictions are the same bits alone, in a resident batch, and in a batch with a
+    synth50 graph, too large for one workgroup's LDS: that batch runs the global-path form
+    (IGN_RESIDENT_PG=1, default) or falls back to the batched launches (0)."""
+    monkeypatch.setenv("IGN_RESIDENT_PG", pg)
     desc, dims, mi = workloads.model("routenet")
     small = [synthetic.routenet_sample("geant2", 60 + g) for g in range(3)]
     big = synthetic.routenet_sample("synth50", 70)
@@ -511,7 +516,7 @@ def test_resident_forward_batch_invariance():
     res = Batch(eng, graphs[:3]).forward().reshape(-1)
     assert launches() == (4, 0)
     mixed = Batch(eng, graphs).forward().reshape(-1)
-    assert launches() == (4, plan.iterations)
+    assert launches() == ((5, 0) if pg == "1" else (4, plan.iterations))
     np.testing.assert_array_equal(res, np.concatenate(alone))
     np.testing.assert_array_equal(mixed[:res.size], res)
 
