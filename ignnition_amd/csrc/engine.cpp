@@ -593,12 +593,12 @@ static bool resident_plan_ok(const ign_plan* p) {
   return p->ents[path].feature_total <= 32 && p->ents[link].feature_total <= 32;
 }
 
-// dynamic LDS of one graph: path_global keeps the path states, codes and message rows in global
-// memory (resident_forward_kernel<true>)
+// dynamic LDS of one graph: path_global keeps the path states and the ordered MP's step codes in
+// global memory (resident_forward_kernel<true>)
 static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs, int64_t codes, bool path_global) {
   if (path_global)
     return (size_t)(links * kResidentStateStride + (links + 1) * kResidentTableStride) * sizeof(float) +
-           (size_t)(links + 1) * sizeof(int32_t);
+           (size_t)(links + 1) * sizeof(int32_t) + (size_t)msgs * sizeof(uint16_t);
   return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
              sizeof(float) +
          (size_t)(links + 1) * sizeof(int32_t) + (size_t)(msgs + codes) * sizeof(uint16_t);

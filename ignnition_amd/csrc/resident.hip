@@ -126,8 +126,9 @@ __device__ __forceinline__ void project_row_f32(const ResidentArgs& a, const f4 
 }  // namespace
 
 // PG: the path states stay in the batch's state buffer in HBM / L2 (rows of 32 floats) and the
-// codes and message rows are read from global memory: the form for graphs whose path states do
-// not fit (synth50: 2 450 paths); LDS then holds the link states, the projected table and the CSR
+// ordered MP's step codes are read from global memory: the form for graphs whose path states do
+// not fit (synth50: 2 450 paths); LDS then holds the link states, the projected table and the
+// sum MP's CSR
 template <bool PG>
 __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs a) {
   constexpr int H = 32, NT = 2, KS = 1, NF = 6 * NT * KS;   // U's fp16 pieces: 2 pieces x 3 gates x NT
@@ -149,8 +150,8 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
   uint16_t* scd_l = sms_l + M;   // the ordered MP's local step codes
   const int64_t cd0 = a.lcode_off[gph], NC = a.lcode_off[gph + 1] - cd0;
-  const uint16_t* sms = PG ? a.lmsg_src + ms0 : sms_l;
-  const uint16_t* scd = PG ? a.lcode + cd0 : scd_l;
+  const uint16_t* sms = sms_l;                      // in LDS in both forms
+  const uint16_t* scd = PG ? a.lcode + cd0 : scd_l;   // PG: read from global memory
   float* xs = tab;   // phase B's message sums [L][SP] alias the (consumed) projected table
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -181,10 +182,9 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   {
     const int* gp = a.lmsg_ptr + l0 + gph;
     for (int64_t i = tid; i <= L; i += 64 * kW) smp[i] = gp[i];
-    if constexpr (!PG) {
-      for (int64_t i = tid; i < M; i += 64 * kW) sms_l[i] = a.lmsg_src[ms0 + i];
+    for (int64_t i = tid; i < M; i += 64 * kW) sms_l[i] = a.lmsg_src[ms0 + i];
+    if constexpr (!PG)
       for (int64_t i = tid; i < NC; i += 64 * kW) scd_l[i] = a.lcode[cd0 + i];
-    }
   }
   __syncthreads();
   const int64_t nlt = (L + 15) / 16;   // link tiles
@@ -331,9 +331,6 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #pragma unroll
         for (int t = 0; t < NT; ++t) lds4w(hP + rl * SPP + 16 * t + 4 * g, h[t] * iS);
       }
-#ifdef IGN_RES_STAMP
-      ++n_at;
-#endif
       k = kn;
     }
 #ifdef IGN_RES_STAMP
@@ -355,6 +352,19 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       const float* hp = hP + 4 * c4;
       f4 x = {0, 0, 0, 0};
       int m = m0;
+      if constexpr (PG) {   // rows from L2: sixteen in flight (two groups of eight double-buffered
+                            // spilled 276 B per lane and ran 40 % slower)
+        for (; m + 16 <= m1; m += 16) {
+          int rr[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) rr[u] = sms[m + u];
+          f4 v[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) v[u] = lds4(hp + rr[u] * SPP);
+#pragma unroll
+          for (int u = 0; u < 16; ++u) x = x + v[u];
+        }
+      }
       for (; m + 8 <= m1; m += 8) {
         int rr[8];
 #pragma unroll
@@ -369,6 +379,13 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       lds4w(xs + ll * SP + 4 * c4, x);
     }
     __syncthreads();
+#ifdef IGN_RES_STAMP
+    {   // B1's end (after its barrier): n_at accumulates B1, n_bt B1 + B2 (diagnostic fields)
+      unsigned long long t_c;
+      IGN_STAMP(t_c);
+      n_at += t_c - t_a;
+    }
+#endif
     // B2: the split-bf16 GRU step (sum_gru_g32's), one wave per (link tile, 16-column half); the new
     // states are written after a barrier (the other half's wave still reads the old ones)
     const bool last = it + 1 == a.T;
@@ -433,6 +450,13 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       if (valid) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn);
     }
     static_assert(NFB == 18, "g32 piece layout");
+#ifdef IGN_RES_STAMP
+    {
+      unsigned long long t_c;
+      IGN_STAMP(t_c);
+      n_bt += t_c - t_a;
+    }
+#endif
     // B3: the next iteration's projected table (sum_gru_g32's fused projection), one wave per
     // (link tile, gate)
     if (!last) {
@@ -462,9 +486,6 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
           }
           if (valid) lds4w(tab + (int64_t)ll * ST + G * H + 16 * i + 4 * g, acc);
         }
-#ifdef IGN_RES_STAMP
-        ++n_bt;
-#endif
       }
     }
 #ifdef IGN_RES_STAMP
