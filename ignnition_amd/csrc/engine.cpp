@@ -596,12 +596,13 @@ static bool resident_plan_ok(const ign_plan* p) {
 // dynamic LDS of one graph: path_global keeps the path states and the ordered MP's step codes in
 // global memory (resident_forward_kernel<true>)
 static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs, int64_t codes, bool path_global) {
+  const size_t order = (size_t)((links + 1) & ~int64_t(1)) * sizeof(uint16_t);   // the link order, padded
   if (path_global)
     return (size_t)(links * kResidentStateStride + (links + 1) * kResidentTableStride) * sizeof(float) +
-           (size_t)(links + 1) * sizeof(int32_t) + (size_t)msgs * sizeof(uint16_t);
+           (size_t)(links + 1) * sizeof(int32_t) + order + (size_t)msgs * sizeof(uint16_t);
   return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
              sizeof(float) +
-         (size_t)(links + 1) * sizeof(int32_t) + (size_t)(msgs + codes) * sizeof(uint16_t);
+         (size_t)(links + 1) * sizeof(int32_t) + order + (size_t)(msgs + codes) * sizeof(uint16_t);
 }
 
 // per-graph tables of the resident forward; leaves b->resident false where it does not apply
@@ -634,6 +635,17 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     lmsg_off[g + 1] = lmsg_off[g] + (int32_t)nmsg[g];
     int32_t* cp = lmsg_ptr.data() + lo[g] + g;
     for (int64_t r = 0; r < lo[g + 1] - lo[g]; ++r) cp[r + 1] += cp[r];
+  }
+  // per graph, its local links by message count, descending (stable): the message sums start the
+  // long chains first
+  hvec<uint16_t> lorder(std::max<int64_t>(lo[G], 1));
+  for (int g = 0; g < G; ++g) {
+    const int64_t L = lo[g + 1] - lo[g];
+    const int32_t* cp = lmsg_ptr.data() + lo[g] + g;
+    std::vector<int32_t> ord(L);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cp[x + 1] - cp[x] > cp[y + 1] - cp[y]; });
+    for (int64_t r = 0; r < L; ++r) lorder[lo[g] + r] = (uint16_t)ord[r];
   }
   hvec<uint16_t> lmsg_src(std::max<int32_t>(lmsg_off[G], 1));
   for (int64_t q = 0; q < NL; ++q) {
@@ -696,7 +708,8 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_link_off, lov)) ||
       (rc = dev_upload(b, &b->d_res_ptile_off, ptile_off)) || (rc = dev_upload(b, &b->d_res_hdr, hdr)) ||
       (rc = dev_upload(b, &b->d_res_lmsg_off, lmsg_off)) || (rc = dev_upload(b, &b->d_res_lmsg_ptr, lmsg_ptr)) ||
-      (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)) || (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
+      (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)) || (rc = dev_upload(b, &b->d_res_lorder, lorder)) ||
+      (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
       (rc = dev_upload(b, &b->d_res_lcode, lcode)))
     return rc;
   b->res_lds = lds;
@@ -1683,6 +1696,7 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.lmsg_off = b->d_res_lmsg_off;
   r.lmsg_ptr = b->d_res_lmsg_ptr;
   r.lmsg_src = b->d_res_lmsg_src;
+  r.lorder = b->d_res_lorder;
   r.path_feat = b->d_feat[path];
   r.path_F = p->ents[path].feature_total;
   r.link_feat = b->d_feat[link];

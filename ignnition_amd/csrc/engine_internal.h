@@ -323,6 +323,7 @@ struct ign_batch {
   int32_t* d_res_lmsg_off = nullptr;
   int32_t* d_res_lmsg_ptr = nullptr;
   uint16_t* d_res_lmsg_src = nullptr;
+  uint16_t* d_res_lorder = nullptr;
   int32_t* d_res_lcode_off = nullptr;
   uint16_t* d_res_lcode = nullptr;
   std::vector<char> proj_ready;

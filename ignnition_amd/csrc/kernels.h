@@ -187,6 +187,7 @@ struct ResidentArgs {
   const int32_t* lmsg_off;    // [G + 1] graph g's sum-MP messages start here in lmsg_src; its CSR
   const int32_t* lmsg_ptr;    //   [link_off[g] + g ...][L_g + 1] local offsets, by local link row
   const uint16_t* lmsg_src;   //   local path rows, each link's messages in the sum MP's order
+  const uint16_t* lorder;     // [link rows] per graph, its local links by message count, descending
   const float* path_feat; int path_F;
   const float* link_feat; int link_F;
   float* path_state;          // [rows][32] final states

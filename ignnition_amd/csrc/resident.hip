@@ -146,7 +146,8 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   float* hL = PG ? dyn : hP + P * SP;
   float* tab = hL + L * SP;
   int* smp = reinterpret_cast<int*>(tab + (L + 1) * ST);   // the sum MP's CSR by local link row
-  uint16_t* sms_l = reinterpret_cast<uint16_t*>(smp + L + 1);
+  uint16_t* slo = reinterpret_cast<uint16_t*>(smp + L + 1);   // link order for the message sums
+  uint16_t* sms_l = slo + ((L + 1) & ~1);
   const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
   uint16_t* scd_l = sms_l + M;   // the ordered MP's local step codes
   const int64_t cd0 = a.lcode_off[gph], NC = a.lcode_off[gph + 1] - cd0;
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     const int* gp = a.lmsg_ptr + l0 + gph;
     for (int64_t i = tid; i <= L; i += 64 * kW) smp[i] = gp[i];
     for (int64_t i = tid; i < M; i += 64 * kW) sms_l[i] = a.lmsg_src[ms0 + i];
+    for (int64_t i = tid; i < L; i += 64 * kW) slo[i] = a.lorder[l0 + i];
     if constexpr (!PG)
       for (int64_t i = tid; i < NC; i += 64 * kW) scd_l[i] = a.lcode[cd0 + i];
   }
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     // B1: the message sums, one lane per (link, float4 column): the adds of sum_gru_g32's lane walk
     // (message order from zero, per column), the codes from LDS
     for (int64_t i = tid; i < L * (H / 4); i += 64 * kW) {
-      const int64_t ll = i >> 3;
+      const int64_t ll = slo[i >> 3];   // links by message count, descending: the long chains first
       const int c4 = (int)(i & 7);
       const int m0 = smp[ll], m1 = smp[ll + 1];
       const float* hp = hP + 4 * c4;
