@@ -1232,8 +1232,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     b->mp.push_back(std::move(mb));
   }
 
-  if ((rc = resident_batch(p, b.get()))) return rc;
-  // readout buffers
+  // readout buffers (the resident forward's tables are built by the first ign_forward: a batch that
+  // only trains or steps MP by MP never pays for them)
   if ((rc = readout_batch(p, b.get(), d))) return rc;
   const int64_t P = space_rows(p, b.get(), p->ro_t[p->ro_in[0]]);
   b->n_pred = P;
@@ -1782,6 +1782,10 @@ int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
 int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
   int rc = check_pb(p, b);
   if (rc) return rc;
+  if (!b->res_tried) {   // before any capture: the tables are uploaded here
+    b->res_tried = true;
+    if ((rc = resident_batch(p, b))) return rc;
+  }
   // HIP event records captured into a graph report 0 ms on this runtime, so timed forwards
   // launch directly; untimed ones replay the captured graph
   if (p->use_graph && p->stream && !p->timing) {

@@ -313,6 +313,7 @@ struct ign_batch {
   // the graph-resident forward (resident.hip, plan->resident): per-graph offsets, the ordered MP's
   // per-graph tile headers, the sum MP's per-graph CSR (local rows); dynamic LDS of the largest graph
   bool resident = false;
+  bool res_tried = false;         // resident_batch ran (lazily, at the first ign_forward)
   size_t res_lds = 0;
   bool res_pg = false;            // resident_forward_kernel<true>: path states in the state buffer
   double res_bytes = 0, res_flops = 0;   // per launch: HBM bytes it must move, FLOPs it executes
