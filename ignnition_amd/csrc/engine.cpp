@@ -720,6 +720,11 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   b->res_bytes = 4.0 * (P * p->ents[path].feature_total + L * p->ents[link].feature_total) + 4.0 * hdr.size() +
                  2.0 * (double)lcode.size() + 4.0 * lmsg_ptr.size() + 2.0 * lmsg_src.size() +
                  4.0 * 32 * (P + L);
+  // global-path form: the path states live in global memory, so every iteration moves them once
+  // in and out of the ordered update and once per message into the sum (rows of 128 B), and the
+  // ordered update reads its step codes again
+  if (pg)
+    b->res_bytes += p->T * (128.0 * (2.0 * P + (double)lmsg_src.size()) + 2.0 * (double)lcode.size());
   // the MPs' FLOPs per iteration (the sum update's aggregation and GRU step, the ordered update's
   // h.U and gates) plus the ordered MP's input projection of every link state
   b->res_flops = p->T * (ma.flops + ms.flops + 2.0 * L * 32 * 96);
