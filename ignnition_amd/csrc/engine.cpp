@@ -662,6 +662,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   const int64_t ND = (int64_t)ma.h_order.size();
   for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
   hvec<int32_t> ptile_off(G + 1, 0), hdr, lcode_off(G + 1, 0);
+  double res_wave_steps = 0;
   hvec<uint16_t> lcode;
   size_t lds = 0, lds_pg = 0;
   for (int g = 0; g < G; ++g) {
@@ -693,6 +694,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       hdr.push_back((int32_t)L);
     }
     ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
+    for (int64_t k = 0; k < n; k += 16) res_wave_steps += ma.h_len[pp[g][k]];   // a tile's first row is its longest
     lcode_off[g + 1] = (int32_t)lcode.size();
     lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], lcode_off[g + 1] - lcode_off[g], false));
     lds_pg = std::max(lds_pg, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], 0, true));
@@ -728,6 +730,13 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   // the MPs' FLOPs per iteration (the sum update's aggregation and GRU step, the ordered update's
   // h.U and gates) plus the ordered MP's input projection of every link state
   b->res_flops = p->T * (ma.flops + ms.flops + 2.0 * L * 32 * 96);
+  // the matrix pipe: phase A's split-fp16 h.U (3 products x 3 gates x 2 tiles per wave step), B2's
+  // split-bf16 GRU step (2 x 18 per half tile), B3's projection (3 gates x 2 x 6, T - 1 times), all
+  // 16x16x32; iteration 0's projection on f32 MFMA (3 gates x 2 tiles x 8 k-steps per link tile)
+  double link_tiles = 0;
+  for (int g = 0; g < G; ++g) link_tiles += (double)((lo[g + 1] - lo[g] + 15) / 16);
+  b->res_mfma_bf16 = (p->T * (res_wave_steps * 18.0 + link_tiles * 72.0) + (p->T - 1) * link_tiles * 36.0) * kMfmaBf16Flops;
+  b->res_mfma_f32 = link_tiles * 48.0 * kMfmaF32Flops;
   b->resident = true;
   return IGN_OK;
 }
@@ -1718,7 +1727,7 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.proj_Wf = p->d_packed + ca.pk_w;
   r.T = p->T;
   Timer tm{p};
-  tm.begin(K_RESIDENT, b->res_flops, b->res_bytes);
+  tm.begin(K_RESIDENT, b->res_flops, b->res_bytes, b->res_mfma_bf16, b->res_mfma_f32);
   HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, b->res_pg, p->stream));
   tm.end();
   b->cur[path] = 0;

@@ -317,6 +317,7 @@ struct ign_batch {
   size_t res_lds = 0;
   bool res_pg = false;            // resident_forward_kernel<true>: path states in the state buffer
   double res_bytes = 0, res_flops = 0;   // per launch: HBM bytes it must move, FLOPs it executes
+  double res_mfma_bf16 = 0, res_mfma_f32 = 0;   // ... and what its MFMAs execute (16-bit / f32 pipes)
   int64_t* d_res_path_off = nullptr;
   int64_t* d_res_link_off = nullptr;
   int32_t* d_res_ptile_off = nullptr;
