@@ -1727,11 +1727,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           v[t][4 * half + q] = act_scaled<ACT>(acc[t][q], c1[t], k, c1[t] * LOG2E, LA * S[t], S[t]);
-#ifndef IGN_RO_SAVE1_OFF
         if constexpr (SAVE) {
-#else
-        if constexpr (false) {
-#endif
           const int64_t r = r0 + 16 * t;
           const float iS = __int_as_float(254 - ((__float_as_int(S[t]) >> 23) & 255) << 23);   // 1 / S, exact
           if (r < a.n_rows)
@@ -1814,11 +1810,7 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
         // unfused for the other (it was, in the SAVE form), which made a row's bits depend on its tile
         y[t] = fmaf(w3[q], av[q], y[t]);
       }
-#ifndef IGN_RO_SAVE2_OFF
       if constexpr (SAVE) {
-#else
-      if constexpr (false) {
-#endif
         const int64_t r = r0 + 16 * t;
         if (r < a.n_rows) st4(a.save2 + r * 256 + 16 * v + 4 * g, av * cSS[t]);
       }

@@ -388,9 +388,84 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       n_at += t_c - t_a;
     }
 #endif
-    // B2: the split-bf16 GRU step (sum_gru_g32's), one wave per (link tile, 16-column half); the new
-    // states are written after a barrier (the other half's wave still reads the old ones)
+    // B2: the split-bf16 GRU step (sum_gru_g32's): one output half (16 columns) of a link tile
     const bool last = it + 1 == a.T;
+    const bf8* sW = static_cast<const bf8*>(a.sWbf);
+    const bf8* sU = static_cast<const bf8*>(a.sUbf);
+    auto gru_half = [&](const bf8 (&xf)[3][1], const bf8 (&hf)[3][1], const f4 ho, int t) __attribute__((always_inline)) {
+      int lofs = lane + 64 * t;   // opaque: the fragment addresses stay inside the loop (as project_row)
+      asm volatile("" : "+v"(lofs));
+      const int u0 = 16 * t + 4 * g;
+      f4 az = ld4(a.sum_bias + 0 * H + u0), ar = ld4(a.sum_bias + 1 * H + u0);
+      f4 ax = ld4(a.sum_bias + 2 * H + u0), ah = ld4(a.sum_bias + 3 * H + u0);
+#pragma unroll
+      for (int pu = 2; pu >= 0; --pu) {
+        const bf8 wz = sW[((pu * 3 + 0) * NT) * 64 + lofs];
+        const bf8 wr = sW[((pu * 3 + 1) * NT) * 64 + lofs];
+        const bf8 wh = sW[((pu * 3 + 2) * NT) * 64 + lofs];
+#pragma unroll
+        for (int ph = 2 - pu; ph >= 0; --ph) {
+          az = MFMA_BF(wz, xf[ph][0], az);
+          ar = MFMA_BF(wr, xf[ph][0], ar);
+          ax = MFMA_BF(wh, xf[ph][0], ax);
+        }
+        const bf8 uz = sU[((pu * 3 + 0) * NT) * 64 + lofs];
+        const bf8 ur = sU[((pu * 3 + 1) * NT) * 64 + lofs];
+        const bf8 uh = sU[((pu * 3 + 2) * NT) * 64 + lofs];
+#pragma unroll
+        for (int ph = 2 - pu; ph >= 0; --ph) {
+          az = MFMA_BF(uz, hf[ph][0], az);
+          ar = MFMA_BF(ur, hf[ph][0], ar);
+          ah = MFMA_BF(uh, hf[ph][0], ah);
+        }
+      }
+      f4 hn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[r]);
+        const float rg = sig2_(ar[r]);
+        const float cnd = tanh2_(ax[r] + rg * ah[r]);
+        hn[r] = cnd + z * (ho[r] - cnd);
+      }
+      return hn;
+    };
+#ifdef IGN_RES_B23_SPLIT   // A/B: B2 and B3 as separate passes whatever the link count
+    const bool fused23 = false;
+#else
+    const bool fused23 = nlt <= kW;   // block-uniform
+#endif
+    if (fused23) {
+      // B2 + B3 in one pass, one wave per link tile: the GRU step of both halves, the new states,
+      // then the next iteration's projected rows of the tile.  The message sums are read into
+      // registers before a barrier: they alias table rows that other waves' projections overwrite
+      const int64_t k = wave;
+      const bool act = k < nlt;   // wave-uniform
+      const int64_t idx = 16 * k + j;
+      const bool valid = act && idx < L;
+      const int ll = valid ? (int)idx : 0;
+      f4 x[2], h[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        x[c] = act ? lds4(xs + (int64_t)ll * SP + 16 * c + 4 * g) : f4{0, 0, 0, 0};
+        h[c] = act ? lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g) : f4{0, 0, 0, 0};
+      }
+      __syncthreads();
+      if (act) {
+        bf8 xf[3][1], hf[3][1];
+        split_frags1(x, xf);
+        split_frags1(h, hf);
+        f4 hn[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) hn[t] = gru_half(xf, hf, h[t], t);
+        if (valid) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn[t]);
+        }
+        if (!last) project_row(a, hn, tab, ll, valid, lane, g);
+      }
+    } else {
+    // B2 as its own pass: one wave per (link tile, half); the new states are written after a
+    // barrier (the other half's wave still reads the old ones)
     const int64_t nb2 = 2 * nlt, rounds2 = (nb2 + kW - 1) / kW;
     for (int64_t rr = 0; rr < rounds2; ++rr) {
       const int64_t item = rr * kW + wave;
@@ -411,42 +486,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         bf8 xf[3][1], hf[3][1];
         split_frags1(x, xf);
         split_frags1(h, hf);
-        const bf8* sW = static_cast<const bf8*>(a.sWbf);
-        const bf8* sU = static_cast<const bf8*>(a.sUbf);
-        int lofs = lane + 64 * t;   // opaque: the fragment addresses stay inside the loop (as project_row)
-        asm volatile("" : "+v"(lofs));
-        const int u0 = 16 * t + 4 * g;
-        f4 az = ld4(a.sum_bias + 0 * H + u0), ar = ld4(a.sum_bias + 1 * H + u0);
-        f4 ax = ld4(a.sum_bias + 2 * H + u0), ah = ld4(a.sum_bias + 3 * H + u0);
-#pragma unroll
-        for (int pu = 2; pu >= 0; --pu) {
-          const bf8 wz = sW[((pu * 3 + 0) * NT) * 64 + lofs];
-          const bf8 wr = sW[((pu * 3 + 1) * NT) * 64 + lofs];
-          const bf8 wh = sW[((pu * 3 + 2) * NT) * 64 + lofs];
-#pragma unroll
-          for (int ph = 2 - pu; ph >= 0; --ph) {
-            az = MFMA_BF(wz, xf[ph][0], az);
-            ar = MFMA_BF(wr, xf[ph][0], ar);
-            ax = MFMA_BF(wh, xf[ph][0], ax);
-          }
-          const bf8 uz = sU[((pu * 3 + 0) * NT) * 64 + lofs];
-          const bf8 ur = sU[((pu * 3 + 1) * NT) * 64 + lofs];
-          const bf8 uh = sU[((pu * 3 + 2) * NT) * 64 + lofs];
-#pragma unroll
-          for (int ph = 2 - pu; ph >= 0; --ph) {
-            az = MFMA_BF(uz, hf[ph][0], az);
-            ar = MFMA_BF(ur, hf[ph][0], ar);
-            ah = MFMA_BF(uh, hf[ph][0], ah);
-          }
-        }
-        const f4 ho = t ? h[1] : h[0];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float z = sig2_(az[r]);
-          const float rg = sig2_(ar[r]);
-          const float cnd = tanh2_(ax[r] + rg * ah[r]);
-          hn[r] = cnd + z * (ho[r] - cnd);
-        }
+        hn = gru_half(xf, hf, t ? h[1] : h[0], t);
       }
       __syncthreads();
       if (valid) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn);
@@ -490,6 +530,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         }
       }
     }
+    }   // B2, B3 as separate passes
 #ifdef IGN_RES_STAMP
     IGN_STAMP(t_b);
     s_bw += t_b - t_a;

@@ -85,9 +85,7 @@ def test_default_ordered_update_keeps_four_waves(asm):
 
 def test_resident_forward_fits_its_workgroup(asm_resident):
     """resident_forward_kernel: 16 waves (one workgroup per graph) need <= 128 VGPRs; no scratch in
-    the all-LDS form (the per-lane fragment addresses stay inside the loops); the
-    global-path form (64-bit addresses of the path rows) spills one dword, reloaded once per
-    iteration outside the tile loops."""
+    either form (the per-lane fragment addresses stay inside the loops)."""
     found = 0
     for name, body, meta in _functions(asm_resident, r"_Z23resident_forward_kernel"):
         found += 1
@@ -95,5 +93,5 @@ def test_resident_forward_fits_its_workgroup(asm_resident):
         scratch = re.search(r"ScratchSize: (\d+)", meta)
         print(name, vgpr.group(1), scratch.group(1))
         assert vgpr and int(vgpr.group(1)) <= 128, name
-        assert scratch and int(scratch.group(1)) <= (0 if "ILb0E" in name else 8), name
+        assert scratch and int(scratch.group(1)) == 0, name
     assert found == 2
