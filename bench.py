@@ -35,6 +35,11 @@ METRIC = "message-passing edges/sec, RouteNet synth50 batched, 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md), the split-bf16 kernels' pipe
+CLOCK_GHZ = 2.4                  # MI355X peak engine clock (spec), the issue roof's clock
+N_CU = 256
+RES_KERNEL = {0: "_Z23resident_forward_kernelILb0ELb1EEv12ResidentArgs",   # form -> instance (resident.hip)
+              1: "_Z23resident_forward_kernelILb1ELb1EEv12ResidentArgs",
+              2: "_Z23resident_forward_kernelILb1ELb0EEv12ResidentArgs"}
 
 
 def parse():
@@ -380,6 +385,7 @@ def main():
 
     engines = []   # every engine of the step (--streams: one per sub-batch)
     subs = []      # --streams: the sub-batches
+    batches = []   # the forward's batches (resident_info)
 
     def barrier_sync(_eng=None):
         for e in engines:
@@ -515,8 +521,10 @@ def main():
         step = lambda: sb.forward(to_host=False)
         edges = sb.edges_per_forward
         gru_steps = sb.gru_steps_per_forward
+        batches += sb.parts
     else:
         batch = Batch(eng, graphs)
+        batches.append(batch)
         step = lambda: batch.forward(to_host=False)
         edges = batch.edges_per_forward
         gru_steps = batch.gru_steps_per_forward
@@ -660,6 +668,8 @@ def main():
                             "alg_flops_per_launch": isolated["flops"] / il, "alg_bytes_per_launch": isolated["bytes"] / il,
                             "achieved": round(iach, 3), "frac": round(iach / roof["peak"], 4),
                             "mfma_pipe": pipe(isolated)}
+    if roof is not None and dom == "mp_resident":
+        roof.update(resident_roof(batches, roof, isolated))
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout",
                                            "mp_resident": "mp_resident"}.get(dom, "sum_update")]
@@ -689,6 +699,49 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def resident_roof(batches, roof, isolated):
+    """The graph-resident forward's per-launch cost model (ign_batch_resident_info) and its issue
+    roof: phase A's tile-steps x the cycles one tile-step's instructions hold a SIMD's vector issue
+    (tools/isa_mix.py over the built kernel: VALU 2, packed f32 4, transcendental 8, an MFMA's hold 8
+    cycles; MI355X_MICROARCH.md constants table), over the launch's SIMDs at the 2.4 GHz clock.  Phase
+    B (the message sums, the GRU step of the union rows, the projection) is not in it: the roof is a
+    floor for phase A's share of the launch (68 % of the cycles in round 4's stamps)."""
+    infos = [b.resident_info() for b in batches]
+    infos = [i for i in infos if i["active"]]
+    if not infos:
+        return {}
+    n = len(infos)
+    avg = {k: sum(i[k] for i in infos) / n for k in ("tile_steps", "union_tiles", "seg_rows", "messages",
+                                                     "bytes_compulsory", "bytes_roundtrip", "bytes_stage", "lds_bytes")}
+    out = {"resident": {"form": {0: "all states in LDS", 1: "path states in HBM/L2",
+                                 2: "path states and sum CSR in HBM/L2"}[infos[0]["form"]],
+                        "launches_per_step": n, "lds_bytes": int(avg["lds_bytes"]),
+                        "tile_steps_per_launch": avg["tile_steps"], "union_tiles_per_iteration": avg["union_tiles"],
+                        "segmented_rows": avg["seg_rows"], "sum_messages_per_iteration": avg["messages"]},
+           # SURVEY §8(d): alg bytes = B_stage over the launch's T x MPs (the line's alg_bytes_per_launch);
+           # the compulsory bytes (inputs once, final states once) and the design's L2 round trips beside it
+           "bytes_per_launch": {"b_stage": avg["bytes_stage"], "compulsory": avg["bytes_compulsory"],
+                                "roundtrip_l2": avg["bytes_roundtrip"]}}
+    path = os.path.join(REPO, "ignnition_amd", "isa_mix.json")
+    if not os.path.exists(path):
+        return out
+    with open(path) as f:
+        mix = json.load(f)["kernels"].get(RES_KERNEL[infos[0]["form"]])
+    if not mix:
+        return out
+    graphs = max(b.num_graphs for b in batches)
+    simds = 4 * min(graphs, N_CU)
+    issue_ms = avg["tile_steps"] * mix["cycles_per_tile_step"] / (simds * CLOCK_GHZ * 1e9) * 1e3
+    iso_ms = isolated["ms"] / isolated["launches"] if isolated and isolated["launches"] else None
+    out["issue"] = {"what": "phase A's VALU/MFMA issue floor: tile_steps x cycles_per_tile_step / (SIMDs x clock)",
+                    "cycles_per_tile_step": mix["cycles_per_tile_step"],
+                    "tile_step_mix": {k: mix[k] for k in ("valu", "valu_pk", "trans", "mfma16", "lds", "vmem", "salu")},
+                    "simds": simds, "clock_ghz": CLOCK_GHZ, "issue_floor_ms": round(issue_ms, 4),
+                    "frac": round(issue_ms / roof["avg_launch_ms"], 4),
+                    "frac_isolated": round(issue_ms / iso_ms, 4) if iso_ms else None}
+    return out
 
 
 def dry_run(args, dist, rank, world, mi, graphs, synthetic):

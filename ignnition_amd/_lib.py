@@ -75,6 +75,13 @@ class BatchInfo(C.Structure):
                 ("gru_steps_per_forward", i64), ("rows", i64 * 8)]
 
 
+class ResidentInfo(C.Structure):
+    _fields_ = [("active", i32), ("form", i32), ("lds_bytes", i64), ("tile_steps", i64), ("union_tiles", i64),
+                ("seg_rows", i64), ("messages", i64), ("bytes_compulsory", C.c_double),
+                ("bytes_roundtrip", C.c_double), ("bytes_stage", C.c_double), ("flops", C.c_double),
+                ("mfma_bf16", C.c_double), ("mfma_f32", C.c_double)]
+
+
 class Stats(C.Structure):
     _fields_ = [("kinds", i32), ("launches", i64 * 8), ("ms", C.c_double * 8), ("flops", C.c_double * 8),
                 ("bytes", C.c_double * 8), ("mfma_bf16", C.c_double * 8), ("mfma_f32", C.c_double * 8)]
@@ -101,9 +108,9 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get", "ign_dataset_batch_create",
            "ign_dataset_batch_get", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json", "ign_forward_train_begin", "ign_forward_train_mp",
            "ign_forward_train_end", "ign_backward_begin", "ign_backward_mp", "ign_backward_end",
-           "ign_batch_train_buffers", "ign_batch_read_predictions"]
+           "ign_batch_train_buffers", "ign_batch_read_predictions", "ign_batch_resident_info"]
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -175,6 +182,7 @@ def _load():
         "ign_backward_end": (C.c_int, [VP, VP]),
         "ign_batch_train_buffers": (C.c_int, [VP, i32, P(VP), P(VP)]),
         "ign_batch_read_predictions": (C.c_int, [VP, VP, VP]),
+        "ign_batch_resident_info": (C.c_int, [VP, P(ResidentInfo)]),
     }
     # an A/B build of an older tree may lack newer entry points: only the A/B tools, which set
     # IGN_AB_LIB=1 next to IGN_LIB_PATH, skip them; any other library must export every symbol
@@ -189,7 +197,7 @@ def _load():
 
 
 lib = _load()
-if lib.ign_abi_version() != ABI_VERSION:
+if lib.ign_abi_version() != ABI_VERSION and os.environ.get("IGN_AB_LIB") != "1":   # (A/B: an older build)
     raise ImportError("libignmp.so ABI %d, bindings expect %d: rebuild (python -m ignnition_amd.build)"
                       % (lib.ign_abi_version(), ABI_VERSION))
 

@@ -14,6 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "libignmp.so")
+# the resident kernel's phase-A instruction mix (tools/isa_mix.py), read by bench.py's roofline.issue
+ISA_MIX = os.path.join(HERE, "isa_mix.json")
 SOURCES = ["engine.cpp", "devpool.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "plan_json.cpp", "kernels.hip", "kernels_bf.hip",
            "train_kernels.hip", "readout_kernels.hip", "resident.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
@@ -51,7 +53,21 @@ def build(force: bool = False, verbose: bool = True) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, OUT)
+    write_isa_mix(hipcc)
     return OUT
+
+
+def write_isa_mix(hipcc: str) -> None:
+    tool = os.path.join(HERE, "..", "tools", "isa_mix.py")
+    if not os.path.exists(tool):
+        return
+    asm = os.path.join(OBJ, "resident.s")
+    subprocess.run([hipcc] + FLAGS + EXTRA["resident.hip"] + ["--cuda-device-only", "-S", "-I", CSRC,
+                                                               os.path.join(CSRC, "resident.hip"), "-o", asm], check=True)
+    out = subprocess.run([sys.executable, tool, asm], check=True, capture_output=True, text=True).stdout
+    with open(ISA_MIX + ".tmp", "w") as f:
+        f.write(out)
+    os.replace(ISA_MIX + ".tmp", ISA_MIX)
 
 
 if __name__ == "__main__":

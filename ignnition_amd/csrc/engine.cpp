@@ -573,100 +573,158 @@ int ign_plan_set_stream(ign_plan* p, void* s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// The graph-resident forward (resident.hip): a RouteNet-shaped model -- one ordered MP (src -> dst,
-// plain, single source) and one sum MP back (dst -> src), H = DIN = 32, the default split kernels --
-// on graphs whose states and projected table fit one workgroup's LDS.  Otherwise the batched path.
-static bool resident_plan_ok(const ign_plan* p) {
-  if (!p->resident || p->ents.size() != 2 || p->mps.size() != 2 || !p->fuse_proj) return false;
+// The graph-resident forward (resident.hip): one ordered MP into the "path" entity from S <= 2
+// source entities (plain, one message per position) and, for each source entity, one sum MP from
+// the paths back to it, every MP at H = DIN = 32 on the default split kernels (RouteNet: S = 1;
+// Q-size: links and nodes interleaved, S = 2), on graphs whose states and projected table fit one
+// workgroup's LDS.  Otherwise the batched path.
+struct ResShape {
+  int path = -1, n_src = 0;
+  int src_ent[kResidentMaxSrc] = {-1, -1};
+  int sum_mp[kResidentMaxSrc] = {-1, -1};
+};
+
+static bool resident_plan_shape(const ign_plan* p, ResShape* sh) {
+  // the windowed sum (IGN_SUM_WINDOW=1) adds in another order: not restated here
+  if (!p->resident || !p->fuse_proj || p->seq_variant != 6 || p->sum_variant < 7 || p->sum_window == 1) return false;
+  const int n = (int)p->mps.size();
+  if (n < 2 || n > kResidentMaxSrc + 1 || (int)p->ents.size() != n) return false;
   const MPP& a = p->mps[0];
-  const MPP& s = p->mps[1];
-  if (!a.sorted || a.aggr != IGN_AGGR_ORDERED || a.src.size() != 1 || s.sorted || s.aggr != IGN_AGGR_SUM ||
-      s.src.size() != 1 || a.feature_concat || s.feature_concat || !a.nn[0].layers.empty() || !s.nn[0].layers.empty())
-    return false;
-  const int link = a.src[0].entity, path = a.dst;
-  if (link == path || s.src[0].entity != path || s.dst != link) return false;
+  const int S = (int)a.src.size();
+  if (!a.sorted || S + 1 != n || a.feature_concat || a.din != 32) return false;
   const CellP& ca = p->cells[a.cell];
-  const CellP& cs = p->cells[s.cell];
-  if (ca.H != 32 || cs.H != 32 || a.din != 32 || s.din != 32 || ca.pk_uh < 0 || ca.pk_wbf < 0 || cs.pk_wbf < 0 ||
-      cs.pk_ubf < 0 || p->seq_variant != 6 || p->sum_variant < 7)
-    return false;
-  return p->ents[path].feature_total <= 32 && p->ents[link].feature_total <= 32;
+  if (ca.H != 32 || ca.pk_uh < 0 || ca.pk_wbf < 0 || ca.pk_w < 0) return false;
+  sh->path = a.dst;
+  sh->n_src = S;
+  for (int s = 0; s < S; ++s) {
+    const int e = a.src[s].entity;
+    if (e == a.dst || !a.nn[s].layers.empty()) return false;
+    for (int t = 0; t < s; ++t)
+      if (sh->src_ent[t] == e) return false;
+    sh->src_ent[s] = e;
+  }
+  // MPs 1 .. S: one sum MP path -> each source entity, in any order (they read only the paths)
+  for (int m = 1; m < n; ++m) {
+    const MPP& q = p->mps[m];
+    int s = -1;
+    for (int t = 0; t < S; ++t)
+      if (sh->src_ent[t] == q.dst) s = t;
+    if (s < 0 || sh->sum_mp[s] >= 0) return false;
+    if (q.sorted || q.aggr != IGN_AGGR_SUM || q.src.size() != 1 || q.src[0].entity != a.dst || q.feature_concat ||
+        !q.nn[0].layers.empty() || q.din != 32)
+      return false;
+    const CellP& cq = p->cells[q.cell];
+    if (cq.H != 32 || cq.pk_wbf < 0 || cq.pk_ubf < 0) return false;
+    sh->sum_mp[s] = m;
+  }
+  for (int e = 0; e < n; ++e)
+    if (p->ents[e].feature_total > 32 || p->ents[e].hidden_dim != 32) return false;
+  return true;
 }
 
-// dynamic LDS of one graph: path_global keeps the path states and the ordered MP's step codes in
-// global memory (resident_forward_kernel<true>)
-static size_t resident_lds_bytes(int64_t paths, int64_t links, int64_t msgs, int64_t codes, bool path_global) {
-  const size_t order = (size_t)((links + 1) & ~int64_t(1)) * sizeof(uint16_t);   // the link order, padded
-  if (path_global)
-    return (size_t)(links * kResidentStateStride + (links + 1) * kResidentTableStride) * sizeof(float) +
-           (size_t)(links + 1) * sizeof(int32_t) + order + (size_t)msgs * sizeof(uint16_t);
-  return (size_t)(paths * kResidentStateStride + links * kResidentStateStride + (links + 1) * kResidentTableStride) *
-             sizeof(float) +
-         (size_t)(links + 1) * sizeof(int32_t) + order + (size_t)(msgs + codes) * sizeof(uint16_t);
+// dynamic LDS of one graph in a form: union-row states and projected table always; the sum MPs' CSR
+// rows unless CL is off; the path states and step codes in the all-LDS form
+static size_t resident_lds_bytes(int64_t paths, int64_t urows, int64_t msgs, int64_t codes, int form) {
+  const size_t order = (size_t)((urows + 1) & ~int64_t(1)) * sizeof(uint16_t);   // the row order, padded
+  size_t b = (size_t)(urows * kResidentStateStride + (urows + 1) * kResidentTableStride) * sizeof(float) +
+             (size_t)(urows + 1) * sizeof(int32_t) + order;
+  if (form != IGN_RES_PATH_CSR_GLOBAL) b += (size_t)msgs * sizeof(uint16_t);
+  if (form == IGN_RES_ALL_LDS) b += (size_t)paths * kResidentStateStride * sizeof(float) + (size_t)codes * sizeof(uint16_t);
+  return b;
+}
+
+// a sum MP's destinations with at least this many messages take the segmented sum (sum_seg_kernel,
+// one wave per destination); the others the lane walk of the GRU-step kernel (IGN_SUM_WINDOW: 0 never,
+// 2 always).  Per destination, so a graph's rows take the same order alone and in any batch.
+static int64_t seg_min_messages(const ign_plan* p) {
+  return p->sum_window == 0 ? INT64_MAX : p->sum_window == 2 ? 0 : 64;
 }
 
 // per-graph tables of the resident forward; leaves b->resident false where it does not apply
 static int resident_batch(ign_plan* p, ign_batch* b) {
-  if (!resident_plan_ok(p)) return IGN_OK;
-  const MPP& a = p->mps[0];
-  const int link = a.src[0].entity, path = a.dst;
+  ResShape sh;
+  if (!resident_plan_shape(p, &sh)) return IGN_OK;
+  const int path = sh.path, S = sh.n_src;
   const MPB& ma = b->mp[0];
-  const MPB& ms = b->mp[1];
-  if (b->halo[link] || b->halo[path] || ma.n_multi || ma.src_off.size() != 1 || ma.src_off[0] != 0) return IGN_OK;
+  if (b->halo[path] || ma.n_multi || (int)ma.src_off.size() != S) return IGN_OK;
+  for (int s = 0; s < S; ++s)
+    if (b->halo[sh.src_ent[s]]) return IGN_OK;
   const int G = b->G;
   const auto& po = b->row_off[path];
-  const auto& lo = b->row_off[link];
+  const std::vector<int64_t>* so[kResidentMaxSrc] = {&b->row_off[sh.src_ent[0]],
+                                                    S > 1 ? &b->row_off[sh.src_ent[1]] : nullptr};
+  auto Ls = [&](int s, int g) -> int64_t { return s < S ? (*so[s])[g + 1] - (*so[s])[g] : 0; };
+  // union rows: per graph, source entity 0's rows, then entity 1's
+  std::vector<int64_t> uo(G + 1, 0);
+  for (int g = 0; g < G; ++g) {
+    uo[g + 1] = uo[g] + Ls(0, g) + Ls(1, g);
+    if (po[g + 1] - po[g] > 65535 || uo[g + 1] - uo[g] > 65535) return IGN_OK;   // local rows are 16-bit
+    if ((Ls(0, g) + 15) / 16 + (Ls(1, g) + 15) / 16 > kResidentMaxTiles) return IGN_OK;   // B2/B3: two tiles per wave
+  }
   // the graph of every row (rows are graph-contiguous)
   auto graph_of = [&](const std::vector<int64_t>& off, int64_t r) {
     return (int)(std::upper_bound(off.begin(), off.end(), r) - off.begin()) - 1;
   };
-  // sum MP: each graph's CSR by local link row, its messages in the MP's order (local path rows)
-  const int64_t NL = (int64_t)ms.h_order.size();
-  hvec<int32_t> lmsg_ptr((size_t)(lo[G] + G), 0), lmsg_off(G + 1, 0);
+  auto urow = [&](int s, int g, int64_t row) { return uo[g] + (s ? Ls(0, g) : 0) + (row - (*so[s])[g]); };
+  // the sum MPs: each graph's CSR by local union row, its messages in the MP's order (local path rows)
+  hvec<int32_t> lmsg_ptr((size_t)(uo[G] + G), 0), lmsg_off(G + 1, 0);
   std::vector<int64_t> nmsg(G, 0);
-  for (int64_t q = 0; q < NL; ++q) {
-    const int64_t row = ms.h_order[q];
-    const int g = graph_of(lo, row);
-    lmsg_ptr[row + g + 1] = ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];   // counts, prefix-summed below
-    nmsg[g] += ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];
+  for (int s = 0; s < S; ++s) {
+    const MPB& ms = b->mp[sh.sum_mp[s]];
+    for (int64_t q = 0; q < (int64_t)ms.h_order.size(); ++q) {
+      const int64_t row = ms.h_order[q];
+      const int g = graph_of(*so[s], row);
+      const int32_t cnt = ms.h_msg_ptr[q + 1] - ms.h_msg_ptr[q];
+      lmsg_ptr[urow(s, g, row) + g + 1] = cnt;   // counts, prefix-summed below
+      nmsg[g] += cnt;
+    }
   }
+  const int64_t seg_min = seg_min_messages(p);
+  hvec<uint16_t> lorder(std::max<int64_t>(uo[G], 1));
+  hvec<int32_t> lnseg(G, 0);
+  int64_t seg_rows = 0;
   for (int g = 0; g < G; ++g) {
-    if (po[g + 1] - po[g] > 65535 || lo[g + 1] - lo[g] > 65535) return IGN_OK;   // local rows are 16-bit
     lmsg_off[g + 1] = lmsg_off[g] + (int32_t)nmsg[g];
-    int32_t* cp = lmsg_ptr.data() + lo[g] + g;
-    for (int64_t r = 0; r < lo[g + 1] - lo[g]; ++r) cp[r + 1] += cp[r];
-  }
-  // per graph, its local links by message count, descending (stable): the message sums start the
-  // long chains first
-  hvec<uint16_t> lorder(std::max<int64_t>(lo[G], 1));
-  for (int g = 0; g < G; ++g) {
-    const int64_t L = lo[g + 1] - lo[g];
-    const int32_t* cp = lmsg_ptr.data() + lo[g] + g;
-    std::vector<int32_t> ord(L);
+    int32_t* cp = lmsg_ptr.data() + uo[g] + g;
+    const int64_t U = uo[g + 1] - uo[g];
+    // its local rows by message count, descending (stable): the rows of >= seg_min messages first
+    // (the segmented sums), then the lane walks, long chains first
+    std::vector<int32_t> ord(U);
     std::iota(ord.begin(), ord.end(), 0);
-    std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cp[x + 1] - cp[x] > cp[y + 1] - cp[y]; });
-    for (int64_t r = 0; r < L; ++r) lorder[lo[g] + r] = (uint16_t)ord[r];
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cp[x + 1] > cp[y + 1]; });
+    for (int64_t r = 0; r < U; ++r) {
+      lorder[uo[g] + r] = (uint16_t)ord[r];
+      if (cp[ord[r] + 1] >= seg_min) lnseg[g]++;
+    }
+    seg_rows += lnseg[g];
+    for (int64_t r = 0; r < U; ++r) cp[r + 1] += cp[r];
   }
   hvec<uint16_t> lmsg_src(std::max<int32_t>(lmsg_off[G], 1));
-  for (int64_t q = 0; q < NL; ++q) {
-    const int64_t row = ms.h_order[q];
-    const int g = graph_of(lo, row);
-    int32_t pos = lmsg_off[g] + lmsg_ptr[row + g];
-    for (int32_t m = ms.h_msg_ptr[q]; m < ms.h_msg_ptr[q + 1]; ++m)
-      lmsg_src[pos++] = (uint16_t)((ms.h_msg_src[m] & IGN_ROW_MASK) - po[g]);
+  for (int s = 0; s < S; ++s) {
+    const MPB& ms = b->mp[sh.sum_mp[s]];
+    for (int64_t q = 0; q < (int64_t)ms.h_order.size(); ++q) {
+      const int64_t row = ms.h_order[q];
+      const int g = graph_of(*so[s], row);
+      int32_t pos = lmsg_off[g] + lmsg_ptr[urow(s, g, row) + g];
+      for (int32_t m = ms.h_msg_ptr[q]; m < ms.h_msg_ptr[q + 1]; ++m) {
+        const int64_t pr = (int64_t)(ms.h_msg_src[m] & IGN_ROW_MASK) - po[g];
+        if ((ms.h_msg_src[m] >> IGN_SLOT_SHIFT) != 0 || pr < 0 || pr >= po[g + 1] - po[g]) return IGN_OK;
+        lmsg_src[pos++] = (uint16_t)pr;
+      }
+    }
   }
   // ordered MP: each graph's positions in the batch's length-sorted order (stable, so still sorted
-  // by length, descending), padded to whole tiles; their step codes as local link rows (L_g: the
+  // by length, descending), padded to whole tiles; their step codes as local union rows (U_g: the
   // hole), then max_len + 8 hole codes (the tile loop reads codes past a row's end)
   std::vector<std::vector<int32_t>> pp(G);
   const int64_t ND = (int64_t)ma.h_order.size();
   for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
   hvec<int32_t> ptile_off(G + 1, 0), hdr, lcode_off(G + 1, 0);
-  double res_wave_steps = 0;
+  double tile_steps = 0;
   hvec<uint16_t> lcode;
-  size_t lds = 0, lds_pg = 0;
+  size_t lds[3] = {0, 0, 0};
   for (int g = 0; g < G; ++g) {
-    const int64_t L = lo[g + 1] - lo[g];
+    const int64_t U = uo[g + 1] - uo[g];
     const int64_t n = (int64_t)pp[g].size(), np = (n + 15) / 16 * 16;
     const size_t c0 = lcode.size();
     int32_t maxl = 0;
@@ -678,65 +736,100 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       hdr.push_back((int32_t)(lcode.size() - c0));
       for (int32_t t = 0; t < len; ++t) {
         const uint32_t c = ma.h_step_code[sp + t];
-        const int64_t lr = (int64_t)c - lo[g];
-        if (c < (uint32_t)ma.zero_row && (lr < 0 || lr >= L)) return IGN_OK;   // another graph's row: not resident
-        lcode.push_back((uint16_t)(c < (uint32_t)ma.zero_row ? lr : L));
+        uint16_t code = (uint16_t)U;   // the zero row: a hole
+        if (c < (uint32_t)ma.zero_row) {
+          const int s = S > 1 && (int64_t)c >= ma.src_off[1] ? 1 : 0;
+          const int64_t lr = (int64_t)c - ma.src_off[s] - (*so[s])[g];
+          if (lr < 0 || lr >= Ls(s, g)) return IGN_OK;   // another graph's row: not resident
+          code = (uint16_t)((s ? Ls(0, g) : 0) + lr);
+        } else if (c != (uint32_t)ma.zero_row) {
+          return IGN_OK;   // a multi-message row (n_multi == 0: unreachable)
+        }
+        lcode.push_back(code);
       }
-      hdr.push_back(lcode[c0 + hdr[hdr.size() - 1]]);
+      hdr.push_back(len > 0 ? lcode[c0 + hdr[hdr.size() - 1]] : (int32_t)U);
       maxl = std::max(maxl, len);
     }
     const int32_t pad = (int32_t)(lcode.size() - c0);
-    lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)L);
+    lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)U);
     for (int64_t k = n; k < np; ++k) {   // padding: length 0, hole codes
       hdr.push_back(0);
       hdr.push_back(0);
       hdr.push_back(pad);
-      hdr.push_back((int32_t)L);
+      hdr.push_back((int32_t)U);
     }
     ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
-    for (int64_t k = 0; k < n; k += 16) res_wave_steps += ma.h_len[pp[g][k]];   // a tile's first row is its longest
+    for (int64_t k = 0; k < n; k += 16) tile_steps += ma.h_len[pp[g][k]];   // a tile's first row is its longest
     lcode_off[g + 1] = (int32_t)lcode.size();
-    lds = std::max(lds, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], lcode_off[g + 1] - lcode_off[g], false));
-    lds_pg = std::max(lds_pg, resident_lds_bytes(po[g + 1] - po[g], L, nmsg[g], 0, true));
+    for (int f = 0; f < 3; ++f)
+      lds[f] = std::max(lds[f], resident_lds_bytes(po[g + 1] - po[g], U, nmsg[g], lcode_off[g + 1] - lcode_off[g], f));
   }
-  // every state in LDS where the largest graph's fit, else the path states in global memory
-  const bool pg = lds > kResidentMaxDynLds || p->resident_path_global;
-  if (pg) {
-    if (lds_pg > kResidentMaxDynLds || !p->resident_pg) return IGN_OK;
-    lds = lds_pg;
+  // every state in LDS where the largest graph's fit, else the path states in global memory, else
+  // also the sum MPs' CSR
+  int form = IGN_RES_ALL_LDS;
+  if (lds[0] > kResidentMaxDynLds || p->resident_path_global) {
+    if (!p->resident_pg) return IGN_OK;
+    form = lds[1] <= kResidentMaxDynLds ? IGN_RES_PATH_GLOBAL : IGN_RES_PATH_CSR_GLOBAL;
+    if (lds[form] > kResidentMaxDynLds) return IGN_OK;
   }
-  std::vector<int64_t> pov(po.begin(), po.end()), lov(lo.begin(), lo.end());
+  HIP_TRY(resident_prepare_device());
+  std::vector<int64_t> pov(po.begin(), po.end());
   int rc;
-  if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_link_off, lov)) ||
+  for (int s = 0; s < S; ++s) {
+    std::vector<int64_t> sov(so[s]->begin(), so[s]->end());
+    if ((rc = dev_upload(b, &b->d_res_src_off[s], sov))) return rc;
+  }
+  if ((rc = dev_upload(b, &b->d_res_path_off, pov)) || (rc = dev_upload(b, &b->d_res_urow_off, uo)) ||
       (rc = dev_upload(b, &b->d_res_ptile_off, ptile_off)) || (rc = dev_upload(b, &b->d_res_hdr, hdr)) ||
       (rc = dev_upload(b, &b->d_res_lmsg_off, lmsg_off)) || (rc = dev_upload(b, &b->d_res_lmsg_ptr, lmsg_ptr)) ||
       (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)) || (rc = dev_upload(b, &b->d_res_lorder, lorder)) ||
-      (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
+      (rc = dev_upload(b, &b->d_res_lnseg, lnseg)) || (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
       (rc = dev_upload(b, &b->d_res_lcode, lcode)))
     return rc;
-  b->res_lds = lds;
-  b->res_pg = pg;
-  // one launch reads the features, the tile headers (T times, from L2 after the first), the step
-  // codes, the sum MP's CSR and writes the final states once: the HBM floor
-  const int64_t P = b->rows[path], L = b->rows[link];
-  b->res_bytes = 4.0 * (P * p->ents[path].feature_total + L * p->ents[link].feature_total) + 4.0 * hdr.size() +
-                 2.0 * (double)lcode.size() + 4.0 * lmsg_ptr.size() + 2.0 * lmsg_src.size() +
-                 4.0 * 32 * (P + L);
-  // global-path form: the path states live in global memory, so every iteration moves them once
-  // in and out of the ordered update and once per message into the sum (rows of 128 B), and the
-  // ordered update reads its step codes again
-  if (pg)
-    b->res_bytes += p->T * (128.0 * (2.0 * P + (double)lmsg_src.size()) + 2.0 * (double)lcode.size());
-  // the MPs' FLOPs per iteration (the sum update's aggregation and GRU step, the ordered update's
-  // h.U and gates) plus the ordered MP's input projection of every link state
-  b->res_flops = p->T * (ma.flops + ms.flops + 2.0 * L * 32 * 96);
-  // the matrix pipe: phase A's split-fp16 h.U (3 products x 3 gates x 2 tiles per wave step), B2's
-  // split-bf16 GRU step (2 x 18 per half tile), B3's projection (3 gates x 2 x 6, T - 1 times), all
-  // 16x16x32; iteration 0's projection on f32 MFMA (3 gates x 2 tiles x 8 k-steps per link tile)
-  double link_tiles = 0;
-  for (int g = 0; g < G; ++g) link_tiles += (double)((lo[g + 1] - lo[g] + 15) / 16);
-  b->res_mfma_bf16 = (p->T * (res_wave_steps * 18.0 + link_tiles * 72.0) + (p->T - 1) * link_tiles * 36.0) * kMfmaBf16Flops;
-  b->res_mfma_f32 = link_tiles * 48.0 * kMfmaF32Flops;
+  b->res_lds = lds[form];
+  b->res_form = form;
+  // the cost model of one launch (ign_batch_resident_info)
+  ign_resident_info_t& ri = b->res_info;
+  ri = ign_resident_info_t{};
+  ri.active = 1;
+  ri.form = form;
+  ri.lds_bytes = (int64_t)lds[form];
+  ri.tile_steps = (int64_t)(tile_steps * p->T);
+  ri.seg_rows = seg_rows;
+  ri.messages = lmsg_off[G];
+  double utiles = 0;
+  for (int g = 0; g < G; ++g) utiles += (double)((Ls(0, g) + 15) / 16 + (Ls(1, g) + 15) / 16);
+  ri.union_tiles = (int64_t)utiles;
+  // compulsory: the features, tile headers, step codes and the sum CSR read once, the final states
+  // written once
+  const int64_t P = b->rows[path], Urows = uo[G];
+  double feat = 4.0 * P * p->ents[path].feature_total;
+  for (int s = 0; s < S; ++s) feat += 4.0 * b->rows[sh.src_ent[s]] * p->ents[sh.src_ent[s]].feature_total;
+  ri.bytes_compulsory = feat + 4.0 * hdr.size() + 2.0 * (double)lcode.size() + 4.0 * lmsg_ptr.size() +
+                        2.0 * lmsg_src.size() + 4.0 * 32 * (P + Urows);
+  // global-path forms: every iteration moves each path row once in and out of the ordered update and
+  // once per message into the sums (rows of 128 B) and reads the step codes again; the CSR-global
+  // form also reads the message rows every iteration
+  if (form != IGN_RES_ALL_LDS)
+    ri.bytes_roundtrip = p->T * (128.0 * (2.0 * P + (double)lmsg_src.size()) + 2.0 * (double)lcode.size());
+  if (form == IGN_RES_PATH_CSR_GLOBAL) ri.bytes_roundtrip += p->T * 2.0 * (double)lmsg_src.size();
+  // B_stage of every MP (MPB::bytes), T times
+  double stage = ma.bytes, mflops = ma.flops;
+  for (int s = 0; s < S; ++s) {
+    stage += b->mp[sh.sum_mp[s]].bytes;
+    mflops += b->mp[sh.sum_mp[s]].flops;
+  }
+  ri.bytes_stage = p->T * stage;
+  // the MPs' FLOPs per iteration plus the ordered MP's input projection of every union row
+  ri.flops = p->T * (mflops + 2.0 * Urows * 32 * 96);
+  // the matrix pipe: phase A's split-fp16 h.U (3 products x 3 gates x 2 tiles per tile-step), the
+  // split-bf16 GRU step (2 x 36 per tile), the projection (3 gates x 2 x 6, T - 1 times), all
+  // 16x16x32; iteration 0's projection on f32 MFMA (3 gates x 2 tiles x 8 k-steps per union tile;
+  // the projection's tiles straddle the entities, ceil(U / 16) per graph)
+  double ptiles = 0;
+  for (int g = 0; g < G; ++g) ptiles += (double)((uo[g + 1] - uo[g] + 15) / 16);
+  ri.mfma_bf16 = (p->T * (tile_steps * 18.0 + utiles * 72.0) + (p->T - 1) * utiles * 36.0) * kMfmaBf16Flops;
+  ri.mfma_f32 = ptiles * 48.0 * kMfmaF32Flops;
   b->resident = true;
   return IGN_OK;
 }
@@ -1162,19 +1255,19 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         for (int g = 0; g < G; ++g)
           max_src_rows = std::max(max_src_rows, b->row_off[mp.src[0].entity][g + 1] - b->row_off[mp.src[0].entity][g]);
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
-      // windowed aggregation pays where each destination gathers many messages (one lane per
-      // destination otherwise walks a long dependent chain): auto threshold 64 per destination
       // IGN_SUM_WINDOW: -1 auto, 0 off (one lane group per destination walks its messages in the
-      // GRU-step kernel), 1 windowed, 2 segmented for every sum MP.  Auto takes the segmented sum
-      // where the lane walk is latency-bound by long per-destination chains: >= 64 messages per
-      // destination (Q-size's path -> node update, ~144 per node: 4.36-4.39 ms/step against 5.19
-      // windowed and 5.51 lane-walk).  The rule reads the MP's mean in-degree, a property of the
-      // graphs rather than of the batch size, so a graph's predictions stay bitwise the same alone
-      // and in any batch (the two kernels add a destination's messages in different orders).
-      // RouteNet synth50's links (~36 per link) keep the lane walk: 2.755 against 2.838 ms/step.
-      const bool high = ND > 0 && (double)mdst.size() >= 64.0 * (double)ND;
+      // GRU-step kernel), 1 windowed, 2 segmented for every destination.  Auto takes the segmented
+      // sum (one wave per destination) for the destinations whose lane walk would be a long dependent
+      // chain: >= 64 messages (seg_min_messages; Q-size's path -> node update, ~140 per node: 4.36-4.39
+      // ms/step against 5.19 windowed and 5.51 lane-walk in round 4).  The rule reads each
+      // destination's own in-degree, a property of its graph, so a graph's predictions stay bitwise
+      // the same alone and in any batch (the two kernels add a destination's messages in different
+      // orders), and the graph-resident forward takes the same order per row (resident.hip B1).
       const bool window = p->sum_window == 1;
-      const bool seg = p->sum_window == 2 || (p->sum_window < 0 && high);
+      int64_t n_seg = 0;   // order is sorted by message count, descending: the segmented rows lead
+      if (!window && !halo)
+        while (n_seg < ND && ptr[n_seg + 1] - ptr[n_seg] >= seg_min_messages(p)) ++n_seg;
+      const bool seg = n_seg > 0;
       if (window && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() &&
           b->halo[mp.src[0].entity] == 0 && (DIN == 16 || DIN == 32 || DIN == 64) && max_src_rows <= 4 * win_rows) {
         const int se = mp.src[0].entity;
@@ -1221,13 +1314,20 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
           return rc;
       } else if (seg && mp.aggr == IGN_AGGR_SUM && S == 1 && mp.nn[0].layers.empty() && b->halo[mp.src[0].entity] == 0 &&
                  (DIN == 16 || DIN == 32 || DIN == 64)) {
-        // segmented sum (sum_seg_kernel over the MP's own CSR, one wave per destination), then the
-        // GRU step on x through an identity CSR, as for the windowed sum
-        hvec<int32_t> id_ptr(ND + 1);
-        hvec<uint32_t> id_src(ND);
-        for (int64_t i = 0; i <= ND; ++i) id_ptr[i] = (int32_t)i;
-        for (int64_t i = 0; i < ND; ++i) id_src[i] = (uint32_t)order[i];   // slot 0: the x table
+        // segmented sum (sum_seg_kernel over the MP's own CSR, one wave per destination) for order
+        // positions [0, n_seg), then the GRU step over a mixed CSR: those positions read their x
+        // from the xsum table (one message, slot 1; the lane walk adds it to zero exactly), the
+        // others their own messages (slot 0)
+        hvec<int32_t> id_ptr(ND + 1, 0);
+        hvec<uint32_t> id_src;
+        id_src.reserve((size_t)(n_seg + (ptr[ND] - ptr[n_seg])));
+        for (int64_t i = 0; i < ND; ++i) {
+          if (i < n_seg) id_src.push_back((1u << IGN_SLOT_SHIFT) | (uint32_t)order[i]);
+          else id_src.insert(id_src.end(), msrc.begin() + ptr[i], msrc.begin() + ptr[i + 1]);
+          id_ptr[i + 1] = (int32_t)id_src.size();
+        }
         mb.sum_seg = true;
+        mb.n_seg = n_seg;
         if ((rc = dev_upload(b.get(), &mb.d_id_ptr, id_ptr)) || (rc = dev_upload(b.get(), &mb.d_id_src, id_src)) ||
             (rc = dev_alloc(b.get(), &mb.d_xsum, std::max<int64_t>(ND, 1) * DIN)))
           return rc;
@@ -1298,6 +1398,12 @@ int ign_batch_info(const ign_batch* b, ign_batch_info_t* o) {
   o->edges_per_forward = b->edges_per_forward;
   o->gru_steps_per_forward = b->gru_steps;
   for (size_t e = 0; e < b->rows.size() && e < 8; ++e) o->rows[e] = b->rows[e];
+  return IGN_OK;
+}
+
+int ign_batch_resident_info(const ign_batch* b, ign_resident_info_t* o) {
+  if (!b || !o) return fail(IGN_ERR_INVALID, "null argument");
+  *o = b->resident ? b->res_info : ign_resident_info_t{};
   return IGN_OK;
 }
 
@@ -1521,8 +1627,13 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
       // windowed or segmented aggregation (sum MPs over all destinations): the sum kernel writes x,
       // then the GRU step reads it through an identity CSR (one message per destination: x itself)
       const bool pre = (mb.n_win_wg > 0 || mb.sum_seg) && part == IGN_PART_ALL && mp.aggr == IGN_AGGR_SUM;
-      SrcBases xb{};
-      xb.base[0] = mb.d_xsum;
+      SrcBases xb{};   // windowed: every x from the xsum table (slot 0); segmented: the mixed CSR's slot 1
+      if (mb.sum_seg) {
+        xb = sbases;
+        xb.base[1] = mb.d_xsum;
+      } else {
+        xb.base[0] = mb.d_xsum;
+      }
       SumGruArgs a{hin, hout, pre ? xb : sbases, pre ? mb.d_order : mb.d_order + first,
                    pre ? mb.d_id_ptr : mb.d_msg_ptr + first, pre ? mb.d_id_src : mb.d_msg_src,
                    p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, count, p->xcd_remap};
@@ -1562,7 +1673,7 @@ int ign_forward_mp(ign_plan* p, ign_batch* b, int32_t mi, int32_t part) {
                bf ? tiles * (sv == 8 ? 3 : 6) * 3 * (cp.H / 16) * (mp.din / 32 + cp.H / 32) * kMfmaBf16Flops : 0,
                bf ? 0 : sum_mfma_f32(count, mp.din, cp.H));
       if (pre && mb.sum_seg) {
-        SumSegArgs sa{sbases.base[0], mb.d_order, mb.d_msg_ptr, mb.d_msg_src, mb.d_xsum, mb.n_dst};
+        SumSegArgs sa{sbases.base[0], mb.d_order, mb.d_msg_ptr, mb.d_msg_src, mb.d_xsum, mb.n_seg};
         HIP_TRY(launch_sum_seg(sa, mp.din, st));
       } else if (pre) {
         SumWinArgs wa{sbases.base[0], mb.d_win_wg, mb.d_win_dst, mb.d_win_ptr, mb.d_win_src, mb.d_xsum, mb.n_win_wg};
@@ -1691,18 +1802,16 @@ int copy_out(ign_plan* p, ign_batch* b, float* pred_out) {
 }
 
 // the whole MP loop of a resident batch in one launch; the final states land in
-// buffer 0 of both entities
+// buffer 0 of every entity
 static int resident_forward(ign_plan* p, ign_batch* b) {
+  ResShape sh;
+  if (!resident_plan_shape(p, &sh)) return fail(IGN_ERR_RUNTIME, "resident batch on a plan of another shape");
   const MPP& a = p->mps[0];
-  const MPP& s = p->mps[1];
-  const int link = a.src[0].entity, path = a.dst;
-  const MPB& ma = b->mp[0];
-  const MPB& ms = b->mp[1];
   const CellP& ca = p->cells[a.cell];
-  const CellP& cs = p->cells[s.cell];
+  const int path = sh.path;
   ResidentArgs r{};
   r.path_off = b->d_res_path_off;
-  r.link_off = b->d_res_link_off;
+  r.urow_off = b->d_res_urow_off;
   r.ptile_off = b->d_res_ptile_off;
   r.hdr = b->d_res_hdr;
   r.lcode_off = b->d_res_lcode_off;
@@ -1711,27 +1820,35 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.lmsg_ptr = b->d_res_lmsg_ptr;
   r.lmsg_src = b->d_res_lmsg_src;
   r.lorder = b->d_res_lorder;
+  r.lnseg = b->d_res_lnseg;
   r.path_feat = b->d_feat[path];
   r.path_F = p->ents[path].feature_total;
-  r.link_feat = b->d_feat[link];
-  r.link_F = p->ents[link].feature_total;
   r.path_state = b->d_state[0][path];
-  r.link_state = b->d_state[0][link];
+  r.n_src = sh.n_src;
+  for (int s = 0; s < sh.n_src; ++s) {
+    const int e = sh.src_ent[s];
+    const CellP& cs = p->cells[p->mps[sh.sum_mp[s]].cell];
+    r.src_off[s] = b->d_res_src_off[s];
+    r.src_feat[s] = b->d_feat[e];
+    r.src_F[s] = p->ents[e].feature_total;
+    r.src_state[s] = b->d_state[0][e];
+    r.sWbf[s] = p->d_packed + cs.pk_wbf;
+    r.sUbf[s] = p->d_packed + cs.pk_ubf;
+    r.sum_bias[s] = p->d_packed + cs.pk_b;
+  }
   r.Uh = p->d_packed + ca.pk_uh;
   r.seq_bias = p->d_packed + ca.pk_b;
-  r.sWbf = p->d_packed + cs.pk_wbf;
-  r.sUbf = p->d_packed + cs.pk_ubf;
-  r.sum_bias = p->d_packed + cs.pk_b;
   r.proj_W = p->d_packed + ca.pk_wbf;
   r.proj_b = p->d_packed + ca.pk_b;
   r.proj_Wf = p->d_packed + ca.pk_w;
   r.T = p->T;
+  const ign_resident_info_t& ri = b->res_info;
   Timer tm{p};
-  tm.begin(K_RESIDENT, b->res_flops, b->res_bytes, b->res_mfma_bf16, b->res_mfma_f32);
-  HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, b->res_pg, p->stream));
+  tm.begin(K_RESIDENT, ri.flops, ri.bytes_stage, ri.mfma_bf16, ri.mfma_f32);
+  HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, b->res_form, p->stream));
   tm.end();
   b->cur[path] = 0;
-  b->cur[link] = 0;
+  for (int s = 0; s < sh.n_src; ++s) b->cur[sh.src_ent[s]] = 0;
   return IGN_OK;
 }
 

@@ -175,6 +175,8 @@ struct MPB {
   // (graph, destination chunk) from LDS windows, then the GRU step reads x through an identity CSR
   int64_t n_win_wg = 0;
   bool sum_seg = false;        // segmented sum (sum_seg_kernel) into d_xsum, then the GRU step
+  int64_t n_seg = 0;           // ... for order positions [0, n_seg): destinations with >= 64 messages
+                               // (seg_min_messages); the GRU step reads their x from d_xsum (slot 1)
   int64_t* d_win_wg = nullptr;
   int32_t* d_win_dst = nullptr;
   int32_t* d_win_ptr = nullptr;
@@ -315,17 +317,19 @@ struct ign_batch {
   bool resident = false;
   bool res_tried = false;         // resident_batch ran (lazily, at the first ign_forward)
   size_t res_lds = 0;
-  bool res_pg = false;            // resident_forward_kernel<true>: path states in the state buffer
-  double res_bytes = 0, res_flops = 0;   // per launch: HBM bytes it must move, FLOPs it executes
-  double res_mfma_bf16 = 0, res_mfma_f32 = 0;   // ... and what its MFMAs execute (16-bit / f32 pipes)
+  int res_form = 0;               // IGN_RES_ALL_LDS / IGN_RES_PATH_GLOBAL / IGN_RES_PATH_CSR_GLOBAL
+  ign_resident_info_t res_info{}; // per launch: bytes (compulsory, round trips, SURVEY B_stage), FLOPs,
+                                  // MFMA FLOPs, tile-steps (ign_batch_resident_info)
   int64_t* d_res_path_off = nullptr;
-  int64_t* d_res_link_off = nullptr;
+  int64_t* d_res_src_off[kResidentMaxSrc] = {nullptr, nullptr};
+  int64_t* d_res_urow_off = nullptr;
   int32_t* d_res_ptile_off = nullptr;
   int32_t* d_res_hdr = nullptr;
   int32_t* d_res_lmsg_off = nullptr;
   int32_t* d_res_lmsg_ptr = nullptr;
   uint16_t* d_res_lmsg_src = nullptr;
   uint16_t* d_res_lorder = nullptr;
+  int32_t* d_res_lnseg = nullptr;
   int32_t* d_res_lcode_off = nullptr;
   uint16_t* d_res_lcode = nullptr;
   std::vector<char> proj_ready;

@@ -168,42 +168,53 @@ struct SumSegArgs {
 };
 hipError_t launch_sum_seg(const SumSegArgs& args, int din, hipStream_t st);
 
-// Graph-resident forward of a RouteNet-shaped model (resident.hip): one workgroup per graph runs the
-// T iterations of one ordered MP (src -> dst, single source) and one sum MP (dst -> src), H = DIN =
-// 32, with the graph's states and projected table in LDS; writes the final states of both entities.
+// Graph-resident forward (resident.hip): one workgroup per graph runs the T iterations of one ordered
+// MP into the "path" entity from S <= 2 source entities ("links"; Q-size: links and nodes, the
+// interleave) and, for each source entity, one sum MP from the paths back to it (RouteNet: S = 1),
+// H = DIN = 32, with the graph's source-entity states and the projected table in LDS; writes the
+// final states of every entity.  The source entities' rows of a graph form one "union" row range:
+// entity 0's rows, then entity 1's.
 constexpr int kResidentWaves = 16;
+constexpr int kResidentMaxSrc = 2;
+constexpr int kResidentMaxTiles = 2 * kResidentWaves;   // union-row tiles of a graph (B2/B3: two per wave)
 constexpr int kResidentStateStride = 36;    // LDS floats per 32-wide state row
 constexpr int kResidentTableStride = 100;   // LDS floats per 96-wide projected row
 constexpr size_t kResidentMaxDynLds = 144 * 1024;   // + ~14.5 KB static (U pieces, biases)
+enum { IGN_RES_ALL_LDS = 0, IGN_RES_PATH_GLOBAL = 1, IGN_RES_PATH_CSR_GLOBAL = 2 };   // kernel forms
 struct ResidentArgs {
   const int64_t* path_off;    // [G + 1] rows of the ordered MP's destination entity ("paths") per graph
-  const int64_t* link_off;    // [G + 1] rows of its source entity ("links") per graph
+  const int64_t* src_off[kResidentMaxSrc];   // [G + 1] rows of each source entity per graph
+  const int64_t* urow_off;    // [G + 1] graph g's union rows start here (lmsg_ptr, lorder)
   const int32_t* ptile_off;   // [G + 1] first header of graph g (multiples of 16)
   const int32_t* hdr;         // [headers][4] per graph, its paths by length descending, padded to whole
                               // tiles: {local path row, final_len (0: padding), local step offset,
                               // first step's local code}
   const int32_t* lcode_off;   // [G + 1] graph g's ordered-MP step codes start here in lcode
-  const uint16_t* lcode;      //   local link rows (L_g = the hole), then max_len + 8 hole codes
+  const uint16_t* lcode;      //   local union rows (U_g = the hole), then max_len + 8 hole codes
   const int32_t* lmsg_off;    // [G + 1] graph g's sum-MP messages start here in lmsg_src; its CSR
-  const int32_t* lmsg_ptr;    //   [link_off[g] + g ...][L_g + 1] local offsets, by local link row
-  const uint16_t* lmsg_src;   //   local path rows, each link's messages in the sum MP's order
-  const uint16_t* lorder;     // [link rows] per graph, its local links by message count, descending
+  const int32_t* lmsg_ptr;    //   [urow_off[g] + g ...][U_g + 1] local offsets, by local union row
+  const uint16_t* lmsg_src;   //   local path rows, each union row's messages in its sum MP's order
+  const uint16_t* lorder;     // [union rows] per graph, its local union rows by message count, descending
+  const int32_t* lnseg;       // [G] the first lnseg[g] rows of lorder (>= 64 messages) take
+                              // sum_seg_kernel's summation order, the others the lane walk
   const float* path_feat; int path_F;
-  const float* link_feat; int link_F;
+  const float* src_feat[kResidentMaxSrc]; int src_F[kResidentMaxSrc];
   float* path_state;          // [rows][32] final states
-  float* link_state;
+  float* src_state[kResidentMaxSrc];
   const void* Uh;             // the ordered MP's U, scaled fp16 pieces (pack_u_f16) + exponent
   const float* seq_bias;      // the ordered MP's combined biases [4][H]
-  const void* sWbf;           // the sum MP's W / U split-bf16 pieces, combined biases
-  const void* sUbf;
-  const float* sum_bias;
+  const void* sWbf[kResidentMaxSrc];   // each sum MP's W / U split-bf16 pieces, combined biases
+  const void* sUbf[kResidentMaxSrc];
+  const float* sum_bias[kResidentMaxSrc];
   const void* proj_W;         // the ordered MP's input kernel as split-bf16 pieces, its biases
   const float* proj_b;
   const float* proj_Wf;       // ... and as project_kernel's f32 fragments (the iteration-0 projection)
   int T;
+  int n_src;
 };
-hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, bool path_global,
-                                   hipStream_t st);
+// the kernels' dynamic-LDS limit, once per device: call before any launch or stream capture
+hipError_t resident_prepare_device();
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, int form, hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

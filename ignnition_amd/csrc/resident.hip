@@ -1,19 +1,21 @@
 // resident.hip — the graph-resident forward for small graphs (RouteNet-shaped models).
 //
-// The batched kernels (seq_gru_h16, sum_gru_g32) run every MP over the whole batch: one launch per MP
-// and iteration, states and projected tables in HBM / Infinity Cache between launches.  For graphs
-// whose states fit in LDS (GEANT2: 552 paths, 74 links; NSFNET) the sum update is the slow part:
-// 2.4 k link tiles per 512-graph batch leave ~2 waves per SIMD, each walking chains of up to 90
-// dependent row loads (DESIGN.md §3b''').  Here one workgroup owns one graph for all T iterations:
-//   LDS: path states [P][36], link states [L][36], the ordered MP's projected table [L + 1][100]
-//        (the hole row last), U's fp16 pieces;
-//   per iteration: phase A, the ordered update (link -> path, seq_gru_h16's tile loop over the
-//        graph's paths sorted by length; the projected rows and states come from LDS), barrier,
-//        phase B, the sum update (path -> link) in three passes over all 16 waves: B1 the message
-//        sums (sum_gru_g32's adds in message order, one lane per (link, float4 column), the local
-//        CSR in LDS), B2 its split-bf16 GRU step (one wave per (link tile, column half)), B3 the
-//        next iteration's projection of the new link states (sum_gru_g32's fused projection, one
-//        wave per (link tile, gate)), barriers between.
+// The batched kernels (seq_gru_h16, sum_gru_g32, sum_seg) run every MP over the whole batch: one
+// launch per MP and iteration, states and projected tables in HBM / Infinity Cache between launches.
+// Here one workgroup owns one graph for all T iterations of a model of this shape: one ordered MP
+// into the "path" entity from S <= 2 source entities (RouteNet: links; Q-size: links and nodes,
+// interleaved), and for each source entity a sum MP from the paths back to it.  The source entities'
+// rows of the graph form one "union" row range (entity 0's rows, then entity 1's); the ordered MP's
+// projected table has one row per union row plus the hole row.
+//   LDS: path states [P][36] (or, for graphs whose paths do not fit, the batch's state buffer in
+//        HBM / L2), union-row states [U][36], the projected table [U + 1][100] (the hole row last),
+//        the sum MPs' CSR by union row (or, when it does not fit, read from L2), U's fp16 pieces;
+//   per iteration: phase A, the ordered update (seq_gru_h16's tile loop over the graph's paths
+//        sorted by length; projected rows and states from LDS), barrier, phase B, the sum updates
+//        over all 16 waves: B1 the message sums (high in-degree rows: sum_seg_kernel's wave per
+//        row; the others: sum_gru_g32's adds in message order, one lane per (row, float4 column)),
+//        barrier, B2+B3 per union-row tile (at most two per wave): the split-bf16 GRU step with the
+//        tile's own sum MP's weights, then the next iteration's projection of the new states.
 // The arithmetic per row is that of the batched kernels: the same message order, pieces, products
 // and gate formulas (iteration 0 projects with project_kernel's f32 MFMA, later iterations with
 // sum_gru_g32's fused split-bf16 projection), so the predictions are the batched forward's bits and
@@ -23,6 +25,10 @@
 // Only the final states leave the workgroup; the batched readout then runs on the path states.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <mutex>
+#include <vector>
+
 #include "kernels.h"
 #include "device_common.h"
 
@@ -68,8 +74,8 @@ __device__ __forceinline__ void split_frags1(const f4* v, bf8 (&f)[3][1]) {
   f[2][0] = __builtin_bit_cast(bf8, w2);
 }
 
-// the ordered MP's projected row of a link state in the B layout (sum_gru_g32's fused projection:
-// split-bf16 x6, the pieces of W' from L2), written to the LDS table row ll
+// the ordered MP's projected row of a union-row state in the B layout (sum_gru_g32's fused
+// projection: split-bf16 x6, the pieces of W' from L2), written to the LDS table row ll
 __device__ __forceinline__ void project_row(const ResidentArgs& a, const f4 (&hn)[2], float* tab, int ll, bool valid,
                                             int lane, int g) {
   // an opaque lane offset: keeps the loop-invariant fragment addresses from being hoisted out of the
@@ -123,16 +129,59 @@ __device__ __forceinline__ void project_row_f32(const ResidentArgs& a, const f4 
   }
 }
 
+// one output half (16 columns, t) of sum_gru_g32's split-bf16 GRU step for a tile of 16 union rows:
+// x.W and h.U piece products (x6) from the sum MP's pieces in L2, then the gates
+__device__ __forceinline__ f4 gru_half(const void* Wbf, const void* Ubf, const float* bias, const bf8 (&xf)[3][1],
+                                       const bf8 (&hf)[3][1], const f4 ho, int t, int lane, int g) {
+  constexpr int H = 32, NT = 2;
+  int lofs = lane + 64 * t;   // opaque: the fragment addresses stay inside the loop (as project_row)
+  asm volatile("" : "+v"(lofs));
+  const bf8* sW = static_cast<const bf8*>(Wbf);
+  const bf8* sU = static_cast<const bf8*>(Ubf);
+  const int u0 = 16 * t + 4 * g;
+  f4 az = ld4(bias + 0 * H + u0), ar = ld4(bias + 1 * H + u0);
+  f4 ax = ld4(bias + 2 * H + u0), ah = ld4(bias + 3 * H + u0);
+#pragma unroll
+  for (int pu = 2; pu >= 0; --pu) {
+    const bf8 wz = sW[((pu * 3 + 0) * NT) * 64 + lofs];
+    const bf8 wr = sW[((pu * 3 + 1) * NT) * 64 + lofs];
+    const bf8 wh = sW[((pu * 3 + 2) * NT) * 64 + lofs];
+#pragma unroll
+    for (int ph = 2 - pu; ph >= 0; --ph) {
+      az = MFMA_BF(wz, xf[ph][0], az);
+      ar = MFMA_BF(wr, xf[ph][0], ar);
+      ax = MFMA_BF(wh, xf[ph][0], ax);
+    }
+    const bf8 uz = sU[((pu * 3 + 0) * NT) * 64 + lofs];
+    const bf8 ur = sU[((pu * 3 + 1) * NT) * 64 + lofs];
+    const bf8 uh = sU[((pu * 3 + 2) * NT) * 64 + lofs];
+#pragma unroll
+    for (int ph = 2 - pu; ph >= 0; --ph) {
+      az = MFMA_BF(uz, hf[ph][0], az);
+      ar = MFMA_BF(ur, hf[ph][0], ar);
+      ah = MFMA_BF(uh, hf[ph][0], ah);
+    }
+  }
+  f4 hn;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float z = sig2_(az[r]);
+    const float rg = sig2_(ar[r]);
+    const float cnd = tanh2_(ax[r] + rg * ah[r]);
+    hn[r] = cnd + z * (ho[r] - cnd);
+  }
+  return hn;
+}
+
 }  // namespace
 
 // PG: the path states stay in the batch's state buffer in HBM / L2 (rows of 32 floats) and the
 // ordered MP's step codes are read from global memory: the form for graphs whose path states do
-// not fit (synth50: 2 450 paths); LDS then holds the link states, the projected table and the
-// sum MP's CSR
-template <bool PG>
+// not fit (synth50: 2 450 paths).  CL: the sum MPs' CSR (message rows) in LDS; else read from L2
+// (Q-size synth50: its two sum MPs' 14 k messages do not fit beside the 250 union rows' table)
+template <bool PG, bool CL>
 __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs a) {
   constexpr int H = 32, NT = 2, KS = 1, NF = 6 * NT * KS;   // U's fp16 pieces: 2 pieces x 3 gates x NT
-  constexpr int NFB = 18;                                     // bf16 pieces of W / U per matrix (g32)
   __shared__ h8 su[NF * 64];
   __shared__ float sbn[kW][H];
   __shared__ float sbias[H];
@@ -140,20 +189,23 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   extern __shared__ float dyn[];
   const int gph = blockIdx.x;
   const int64_t p0 = a.path_off[gph], P = a.path_off[gph + 1] - p0;
-  const int64_t l0 = a.link_off[gph], L = a.link_off[gph + 1] - l0;
+  const int64_t s00 = a.src_off[0][gph], L0 = a.src_off[0][gph + 1] - s00;
+  const int64_t s10 = a.n_src > 1 ? a.src_off[1][gph] : 0;
+  const int64_t L1 = a.n_src > 1 ? a.src_off[1][gph + 1] - s10 : 0;
+  const int64_t U = L0 + L1;   // union rows: entity 0's, then entity 1's
   constexpr int SPP = PG ? H : SP;   // row stride of the path states
   float* hP = PG ? a.path_state + p0 * H : dyn;
   float* hL = PG ? dyn : hP + P * SP;
-  float* tab = hL + L * SP;
-  int* smp = reinterpret_cast<int*>(tab + (L + 1) * ST);   // the sum MP's CSR by local link row
-  uint16_t* slo = reinterpret_cast<uint16_t*>(smp + L + 1);   // link order for the message sums
-  uint16_t* sms_l = slo + ((L + 1) & ~1);
+  float* tab = hL + U * SP;
+  int* smp = reinterpret_cast<int*>(tab + (U + 1) * ST);   // the sum MPs' CSR by local union row
+  uint16_t* slo = reinterpret_cast<uint16_t*>(smp + U + 1);   // union-row order for the message sums
+  uint16_t* sms_l = slo + ((U + 1) & ~1);
   const int64_t ms0 = a.lmsg_off[gph], M = a.lmsg_off[gph + 1] - ms0;
-  uint16_t* scd_l = sms_l + M;   // the ordered MP's local step codes
+  uint16_t* scd_l = sms_l + (CL ? M : 0);   // the ordered MP's local step codes
   const int64_t cd0 = a.lcode_off[gph], NC = a.lcode_off[gph + 1] - cd0;
-  const uint16_t* sms = sms_l;                      // in LDS in both forms
-  const uint16_t* scd = PG ? a.lcode + cd0 : scd_l;   // PG: read from global memory
-  float* xs = tab;   // phase B's message sums [L][SP] alias the (consumed) projected table
+  const uint16_t* sms = CL ? sms_l : a.lmsg_src + ms0;   // LDS, or L2 (!CL)
+  const uint16_t* scd = PG ? a.lcode + cd0 : scd_l;      // PG: read from global memory
+  float* xs = tab;   // phase B's message sums [U][SP] alias the (consumed) projected table
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
 #ifdef IGN_RES_STAMP
@@ -174,26 +226,31 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     const int c = (int)(i - r * H);
     hP[r * SPP + c] = c < a.path_F ? a.path_feat[(p0 + r) * a.path_F + c] : 0.f;
   }
-  for (int64_t i = tid; i < L * H; i += 64 * kW) {
+  for (int64_t i = tid; i < U * H; i += 64 * kW) {
     const int64_t r = i / H;
     const int c = (int)(i - r * H);
-    hL[r * SP + c] = c < a.link_F ? a.link_feat[(l0 + r) * a.link_F + c] : 0.f;
+    const bool e1 = r >= L0;
+    const int F = e1 ? a.src_F[1] : a.src_F[0];
+    const float* f = e1 ? a.src_feat[1] + (s10 + r - L0) * F : a.src_feat[0] + (s00 + r) * F;
+    hL[r * SP + c] = c < F ? f[c] : 0.f;
   }
-  for (int i = tid; i < 3 * H; i += 64 * kW) tab[L * ST + i] = a.proj_b[i];   // the hole row: b' alone
+  for (int i = tid; i < 3 * H; i += 64 * kW) tab[U * ST + i] = a.proj_b[i];   // the hole row: b' alone
   {
-    const int* gp = a.lmsg_ptr + l0 + gph;
-    for (int64_t i = tid; i <= L; i += 64 * kW) smp[i] = gp[i];
-    for (int64_t i = tid; i < M; i += 64 * kW) sms_l[i] = a.lmsg_src[ms0 + i];
-    for (int64_t i = tid; i < L; i += 64 * kW) slo[i] = a.lorder[l0 + i];
+    const int64_t u0 = a.urow_off[gph];
+    const int* gp = a.lmsg_ptr + u0 + gph;
+    for (int64_t i = tid; i <= U; i += 64 * kW) smp[i] = gp[i];
+    if constexpr (CL)
+      for (int64_t i = tid; i < M; i += 64 * kW) sms_l[i] = a.lmsg_src[ms0 + i];
+    for (int64_t i = tid; i < U; i += 64 * kW) slo[i] = a.lorder[u0 + i];
     if constexpr (!PG)
       for (int64_t i = tid; i < NC; i += 64 * kW) scd_l[i] = a.lcode[cd0 + i];
   }
   __syncthreads();
-  const int64_t nlt = (L + 15) / 16;   // link tiles
+  const int64_t nut = (U + 15) / 16;   // union-row tiles of the projection
   // the first iteration's projected table
-  for (int64_t k = wave; k < nlt; k += kW) {
+  for (int64_t k = wave; k < nut; k += kW) {
     const int64_t idx = 16 * k + j;
-    const bool valid = idx < L;
+    const bool valid = idx < U;
     const int ll = valid ? (int)idx : 0;
     f4 h[NT];
 #pragma unroll
@@ -344,11 +401,55 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     IGN_STAMP(t_a);
     s_ab += t_a - t_b;
 #endif
-    // ---- phase B: the sum update, in three passes over all 16 waves ----
-    // B1: the message sums, one lane per (link, float4 column): the adds of sum_gru_g32's lane walk
-    // (message order from zero, per column), the codes from LDS
-    for (int64_t i = tid; i < L * (H / 4); i += 64 * kW) {
-      const int64_t ll = slo[i >> 3];   // links by message count, descending: the long chains first
+    // ---- phase B: the sum updates ----
+    // B1: the message sums.  Rows with >= 64 messages (lorder's first nseg, per destination as the
+    // batched forward decides): sum_seg_kernel<32, 4>'s order, one wave per row -- lane (c, q) adds
+    // messages q, q + 8, ... of the row (columns 4c .. 4c + 3), four rows in flight, then the eight
+    // partial sums pairwise across lanes (xor 32, 16, 8).  The others: sum_gru_g32's lane walk, one
+    // lane per (row, float4 column) adding in message order from zero, long chains first.
+    const int nseg = a.lnseg[gph];
+    for (int k = wave; k < nseg; k += kW) {
+      const int ll = slo[k];
+      int lo = lane;   // opaque: the lane's column pointer stays inside the loop (no spill, as project_row)
+      asm volatile("" : "+v"(lo));
+      const int c = lo & 7, q = lo >> 3;
+      const int m0 = smp[ll], m1 = smp[ll + 1];
+      const int last = m1 > m0 ? m1 - 1 : m0;
+      const float* hp = hP + 4 * c;
+      f4 acc = {0, 0, 0, 0};
+      int cc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = m0 + 8 * u + q;
+        cc[u] = m1 > m0 ? sms[i < last ? i : last] : 0;
+      }
+      for (int m = m0; m < m1; m += 32) {
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = lds4(hp + cc[u] * SPP);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // the next round's rows, clamped into the range
+          const int i = m + 8 * (4 + u) + q;
+          cc[u] = sms[i < last ? i : last];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool on = m + 8 * u + q < m1;
+          const f4 s = acc + v[u];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] = on ? s[e] : acc[e];
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 8; o >>= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += __shfl_xor(acc[e], o);
+      if (q == 0) lds4w(xs + ll * SP + 4 * c, acc);
+    }
+    int tlw = tid;   // opaque (as above)
+    asm volatile("" : "+v"(tlw));
+    for (int64_t i = (int64_t)nseg * 8 + tlw; i < U * (H / 4); i += 64 * kW) {
+      const int64_t ll = slo[i >> 3];   // rows by message count, descending: the long chains first
       const int c4 = (int)(i & 7);
       const int m0 = smp[ll], m1 = smp[ll + 1];
       const float* hp = hP + 4 * c4;
@@ -382,155 +483,59 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     }
     __syncthreads();
 #ifdef IGN_RES_STAMP
-    {   // B1's end (after its barrier): n_at accumulates B1, n_bt B1 + B2 (diagnostic fields)
+    {   // B1's end (after its barrier): n_at accumulates B1
       unsigned long long t_c;
       IGN_STAMP(t_c);
       n_at += t_c - t_a;
     }
 #endif
-    // B2: the split-bf16 GRU step (sum_gru_g32's): one output half (16 columns) of a link tile
+    // B2 + B3, one wave per union-row tile (tiles w and w + 16; a tile holds one entity's rows):
+    // the GRU step of both column halves with the tile's own sum MP's weights, the new states, then
+    // the next iteration's projected rows of the tile.  Each wave reads its tiles' message sums into
+    // registers before a barrier: they alias table rows that other waves' projections overwrite (a
+    // tile's states are only written by its own wave: read after the barrier)
     const bool last = it + 1 == a.T;
-    const bf8* sW = static_cast<const bf8*>(a.sWbf);
-    const bf8* sU = static_cast<const bf8*>(a.sUbf);
-    auto gru_half = [&](const bf8 (&xf)[3][1], const bf8 (&hf)[3][1], const f4 ho, int t) __attribute__((always_inline)) {
-      int lofs = lane + 64 * t;   // opaque: the fragment addresses stay inside the loop (as project_row)
-      asm volatile("" : "+v"(lofs));
-      const int u0 = 16 * t + 4 * g;
-      f4 az = ld4(a.sum_bias + 0 * H + u0), ar = ld4(a.sum_bias + 1 * H + u0);
-      f4 ax = ld4(a.sum_bias + 2 * H + u0), ah = ld4(a.sum_bias + 3 * H + u0);
+    const int nt0 = (int)((L0 + 15) / 16);
+    const int ntt = nt0 + (int)((L1 + 15) / 16);
+    f4 xr[2][2];
 #pragma unroll
-      for (int pu = 2; pu >= 0; --pu) {
-        const bf8 wz = sW[((pu * 3 + 0) * NT) * 64 + lofs];
-        const bf8 wr = sW[((pu * 3 + 1) * NT) * 64 + lofs];
-        const bf8 wh = sW[((pu * 3 + 2) * NT) * 64 + lofs];
-#pragma unroll
-        for (int ph = 2 - pu; ph >= 0; --ph) {
-          az = MFMA_BF(wz, xf[ph][0], az);
-          ar = MFMA_BF(wr, xf[ph][0], ar);
-          ax = MFMA_BF(wh, xf[ph][0], ax);
-        }
-        const bf8 uz = sU[((pu * 3 + 0) * NT) * 64 + lofs];
-        const bf8 ur = sU[((pu * 3 + 1) * NT) * 64 + lofs];
-        const bf8 uh = sU[((pu * 3 + 2) * NT) * 64 + lofs];
-#pragma unroll
-        for (int ph = 2 - pu; ph >= 0; --ph) {
-          az = MFMA_BF(uz, hf[ph][0], az);
-          ar = MFMA_BF(ur, hf[ph][0], ar);
-          ah = MFMA_BF(uh, hf[ph][0], ah);
-        }
-      }
-      f4 hn;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = sig2_(az[r]);
-        const float rg = sig2_(ar[r]);
-        const float cnd = tanh2_(ax[r] + rg * ah[r]);
-        hn[r] = cnd + z * (ho[r] - cnd);
-      }
-      return hn;
-    };
-#ifdef IGN_RES_B23_SPLIT   // A/B: B2 and B3 as separate passes whatever the link count
-    const bool fused23 = false;
-#else
-    const bool fused23 = nlt <= kW;   // block-uniform
-#endif
-    if (fused23) {
-      // B2 + B3 in one pass, one wave per link tile: the GRU step of both halves, the new states,
-      // then the next iteration's projected rows of the tile.  The message sums are read into
-      // registers before a barrier: they alias table rows that other waves' projections overwrite
-      const int64_t k = wave;
-      const bool act = k < nlt;   // wave-uniform
-      const int64_t idx = 16 * k + j;
-      const bool valid = act && idx < L;
+    for (int q = 0; q < 2; ++q) {
+      const int k = wave + kW * q;
+      const bool act = k < ntt;   // wave-uniform
+      const bool e1 = k >= nt0;
+      const int64_t idx = e1 ? L0 + 16 * (k - nt0) + j : 16 * k + j;
+      const bool valid = act && idx < (e1 ? U : L0);
       const int ll = valid ? (int)idx : 0;
-      f4 x[2], h[2];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        x[c] = act ? lds4(xs + (int64_t)ll * SP + 16 * c + 4 * g) : f4{0, 0, 0, 0};
-        h[c] = act ? lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g) : f4{0, 0, 0, 0};
-      }
-      __syncthreads();
-      if (act) {
-        bf8 xf[3][1], hf[3][1];
-        split_frags1(x, xf);
-        split_frags1(h, hf);
-        f4 hn[NT];
+      for (int c = 0; c < 2; ++c) xr[q][c] = act ? lds4(xs + (int64_t)ll * SP + 16 * c + 4 * g) : f4{0, 0, 0, 0};
+    }
+    __syncthreads();
 #pragma unroll
-        for (int t = 0; t < NT; ++t) hn[t] = gru_half(xf, hf, h[t], t);
-        if (valid) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn[t]);
-        }
-        if (!last) project_row(a, hn, tab, ll, valid, lane, g);
-      }
-    } else {
-    // B2 as its own pass: one wave per (link tile, half); the new states are written after a
-    // barrier (the other half's wave still reads the old ones)
-    const int64_t nb2 = 2 * nlt, rounds2 = (nb2 + kW - 1) / kW;
-    for (int64_t rr = 0; rr < rounds2; ++rr) {
-      const int64_t item = rr * kW + wave;
-      const bool act = item < nb2;   // wave-uniform
-      const int64_t k = act ? item >> 1 : 0;
-      const int t = (int)(item & 1);
-      const int64_t idx = 16 * k + j;
-      const bool valid = act && idx < L;
+    for (int q = 0; q < 2; ++q) {
+      const int k = wave + kW * q;
+      if (k >= ntt) break;   // wave-uniform
+      const int e1 = k >= nt0;
+      const int64_t idx = e1 ? L0 + 16 * (k - nt0) + j : 16 * k + j;
+      const bool valid = idx < (e1 ? U : L0);
       const int ll = valid ? (int)idx : 0;
-      f4 hn = {0, 0, 0, 0};
-      if (act) {
-        f4 x[2], h[2];
+      f4 hr[2];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          x[c] = lds4(xs + (int64_t)ll * SP + 16 * c + 4 * g);
-          h[c] = lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g);
-        }
-        bf8 xf[3][1], hf[3][1];
-        split_frags1(x, xf);
-        split_frags1(h, hf);
-        hn = gru_half(xf, hf, t ? h[1] : h[0], t);
+      for (int c = 0; c < 2; ++c) hr[c] = lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g);
+      bf8 xf[3][1], hf[3][1];
+      split_frags1(xr[q], xf);
+      split_frags1(hr, hf);
+      const void* W = e1 ? a.sWbf[1] : a.sWbf[0];
+      const void* Ub = e1 ? a.sUbf[1] : a.sUbf[0];
+      const float* bias = e1 ? a.sum_bias[1] : a.sum_bias[0];
+      f4 hn[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) hn[t] = gru_half(W, Ub, bias, xf, hf, hr[t], t, lane, g);
+      if (valid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn[t]);
       }
-      __syncthreads();
-      if (valid) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn);
+      if (!last) project_row(a, hn, tab, ll, valid, lane, g);
     }
-    static_assert(NFB == 18, "g32 piece layout");
-#ifdef IGN_RES_STAMP
-    {
-      unsigned long long t_c;
-      IGN_STAMP(t_c);
-      n_bt += t_c - t_a;
-    }
-#endif
-    // B3: the next iteration's projected table (sum_gru_g32's fused projection), one wave per
-    // (link tile, gate)
-    if (!last) {
-      __syncthreads();
-      const bf8* pw = static_cast<const bf8*>(a.proj_W);
-      for (int64_t item = wave; item < 3 * nlt; item += kW) {
-        const int64_t k = item / 3;
-        const int G = (int)(item - 3 * k);
-        const int64_t idx = 16 * k + j;
-        const bool valid = idx < L;
-        const int ll = valid ? (int)idx : 0;
-        f4 h[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) h[c] = lds4(hL + (int64_t)ll * SP + 16 * c + 4 * g);
-        bf8 pf[3][1];
-        split_frags1(h, pf);
-        int lofs = lane + 64 * NT * G;
-        asm volatile("" : "+v"(lofs));
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-          f4 acc = ld4(a.proj_b + G * H + 16 * i + 4 * g);
-#pragma unroll
-          for (int pu = 2; pu >= 0; --pu) {
-            const bf8 w = pw[(pu * 3 * NT + i) * 64 + lofs];
-#pragma unroll
-            for (int ph = 2 - pu; ph >= 0; --ph) acc = MFMA_BF(w, pf[ph][0], acc);
-          }
-          if (valid) lds4w(tab + (int64_t)ll * ST + G * H + 16 * i + 4 * g, acc);
-        }
-      }
-    }
-    }   // B2, B3 as separate passes
 #ifdef IGN_RES_STAMP
     IGN_STAMP(t_b);
     s_bw += t_b - t_a;
@@ -555,29 +560,45 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       const int c4 = (int)(i - r * (H / 4));
       st4(a.path_state + (p0 + r) * H + 4 * c4, lds4(hP + r * SP + 4 * c4));
     }
-  for (int64_t i = tid; i < L * (H / 4); i += 64 * kW) {
+  for (int64_t i = tid; i < U * (H / 4); i += 64 * kW) {
     const int64_t r = i / (H / 4);
     const int c4 = (int)(i - r * (H / 4));
-    st4(a.link_state + (l0 + r) * H + 4 * c4, lds4(hL + r * SP + 4 * c4));
+    float* o = r >= L0 ? a.src_state[1] + (s10 + r - L0) * H : a.src_state[0] + (s00 + r) * H;
+    st4(o + 4 * c4, lds4(hL + r * SP + 4 * c4));
   }
 }
 
-hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, bool path_global,
-                                   hipStream_t st) {
-  if (n_graphs == 0) return hipSuccess;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* k : {reinterpret_cast<const void*>(resident_forward_kernel<false>),
-                          reinterpret_cast<const void*>(resident_forward_kernel<true>)}) {
-      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResidentMaxDynLds);
-      if (e != hipSuccess) return e;
-    }
-    attr = true;
+// once per device, before any launch or capture (resident_batch calls it)
+hipError_t resident_prepare_device() {
+  static std::mutex mu;
+  static std::vector<char> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)done.size() <= dev) done.resize(dev + 1, 0);
+  if (done[dev]) return hipSuccess;
+  for (const void* k : {reinterpret_cast<const void*>(resident_forward_kernel<false, true>),
+                        reinterpret_cast<const void*>(resident_forward_kernel<true, true>),
+                        reinterpret_cast<const void*>(resident_forward_kernel<true, false>)}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResidentMaxDynLds);
+    if (e != hipSuccess) return e;
   }
-  if (lds_bytes > kResidentMaxDynLds) return hipErrorInvalidValue;
-  if (path_global)
-    hipLaunchKernelGGL(resident_forward_kernel<true>, dim3((unsigned)n_graphs), dim3(64 * kW), lds_bytes, st, a);
+  done[dev] = 1;
+  return hipSuccess;
+}
+
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, int form, hipStream_t st) {
+  if (n_graphs == 0) return hipSuccess;
+  if (lds_bytes > kResidentMaxDynLds || a.n_src < 1 || a.n_src > kResidentMaxSrc) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)n_graphs), block(64 * kW);
+  if (form == IGN_RES_PATH_CSR_GLOBAL)
+    hipLaunchKernelGGL((resident_forward_kernel<true, false>), grid, block, lds_bytes, st, a);
+  else if (form == IGN_RES_PATH_GLOBAL)
+    hipLaunchKernelGGL((resident_forward_kernel<true, true>), grid, block, lds_bytes, st, a);
+  else if (form == IGN_RES_ALL_LDS)
+    hipLaunchKernelGGL((resident_forward_kernel<false, true>), grid, block, lds_bytes, st, a);
   else
-    hipLaunchKernelGGL(resident_forward_kernel<false>, dim3((unsigned)n_graphs), dim3(64 * kW), lds_bytes, st, a);
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }

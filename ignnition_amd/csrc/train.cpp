@@ -652,7 +652,12 @@ int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* gra
   if (rc) return rc;
   if (!dpred || !grads) return fail(IGN_ERR_INVALID, "null argument");
   TrainState* t = b->train;
-  if (!t->forward_done) return fail(IGN_ERR_INVALID, "ign_backward needs a preceding ign_forward_train");
+  if (!t->forward_done)
+    return fail(IGN_ERR_INVALID, "ign_backward needs a preceding ign_forward_train (a backward consumes the "
+                "forward's saved activations: one backward per forward)");
+  // the readout backward below may write gradient rows over the saved activations (fuse_outer_bwd):
+  // a second backward of the same forward would read them as activations
+  t->forward_done = false;
   hipStream_t st = p->stream;
   const int E = (int)p->ents.size();
   const int64_t P = b->n_pred;

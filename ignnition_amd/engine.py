@@ -700,6 +700,15 @@ class Batch:
         """dpred, grads: device tensors ([predictions * units], [n_params])."""
         check(lib.ign_backward(self.engine.handle, self.handle, _ptr(dpred), _ptr(grads)))
 
+    def resident_info(self) -> dict:
+        """The graph-resident forward of this batch (decided at its first forward): whether it
+        runs, its form and LDS, and the per-launch cost model (ign_batch_resident_info)."""
+        r = _lib.ResidentInfo()
+        if not hasattr(lib, "ign_batch_resident_info"):   # an A/B build of an older tree (IGN_AB_LIB=1)
+            return {"active": 0}
+        check(lib.ign_batch_resident_info(self.handle, C.byref(r)))
+        return {name: getattr(r, name) for name, _ in _lib.ResidentInfo._fields_}
+
     def state_slot(self, entity: str) -> int:
         s = C.c_int32()
         check(lib.ign_batch_state_slot(self.handle, self.engine.plan.entities.index(entity), C.byref(s)))

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 10
+#define IGN_ABI_VERSION 11
 
 enum ign_status {
   IGN_OK = 0,
@@ -257,6 +257,28 @@ int  ign_batch_create(ign_plan* plan, const ign_batch_desc* desc, ign_batch** ou
 void ign_batch_destroy(ign_batch* batch);
 int  ign_batch_info(const ign_batch* batch, ign_batch_info_t* out);
 
+/* The graph-resident forward of a batch (ABI 11): decided at the batch's first
+ * ign_forward (before it, active = 0), with the per-launch cost model of its one launch. */
+typedef struct {
+  int32_t active;                  /* 1: ign_forward runs the whole MP loop as one launch */
+  int32_t form;                    /* 0: every state in LDS; 1: path states in HBM / L2; 2: ... and the
+                                      sum MPs' CSR read from L2 */
+  int64_t lds_bytes;               /* dynamic LDS per workgroup (the batch's largest graph) */
+  int64_t tile_steps;              /* phase A: 16-path tile-steps per launch (T x per tile its longest
+                                      sequence) */
+  int64_t union_tiles;             /* phase B: 16-row tiles of the source entities' rows, per iteration */
+  int64_t seg_rows;                /* rows whose message sum takes sum_seg's wave-per-row order */
+  int64_t messages;                /* sum-MP messages per iteration */
+  double  bytes_compulsory;        /* features, index tables read once, final states written once */
+  double  bytes_roundtrip;         /* global-path forms: the path states' (and CSR's) L2 round trips */
+  double  bytes_stage;             /* sum over the T iterations' MPs of
+                                      B_stage = E (4 + 4H) + 2 N_d 4H + 4 (N_d + 1) */
+  double  flops;                   /* executed FLOPs (fp32-equivalent) */
+  double  mfma_bf16;               /* FLOPs issued on the 16-bit matrix pipe */
+  double  mfma_f32;                /* ... on the f32 matrix pipe */
+} ign_resident_info_t;
+int  ign_batch_resident_info(const ign_batch* batch, ign_resident_info_t* out);
+
 /* Full forward (hidden-state init, T x stages x MPs, readout) on the plan stream.
  * pred_out: host pointer (copied + synchronised) or NULL (stays on device, async).
  * Untimed forwards on a non-null stream replay one hipGraph captured per batch on first use
@@ -303,7 +325,10 @@ int  ign_gather_rows(ign_plan* plan, const float* src, int64_t ld, const int32_t
 int  ign_batch_enable_training(ign_plan* plan, ign_batch* batch);
 /* forward of ComnetModel.call keeping the activations; pred_out: host or NULL (see ign_forward) */
 int  ign_forward_train(ign_plan* plan, ign_batch* batch, float* pred_out);
-/* grads[n_params] = dLoss/dparams for dLoss/dpredictions = dpred[predictions * output_units] */
+/* grads[n_params] = dLoss/dparams for dLoss/dpredictions = dpred[predictions * output_units].
+ * A backward consumes its forward: the readout backward writes gradient rows over the saved
+ * activations, so a second ign_backward / ign_backward_begin returns IGN_ERR_INVALID until the
+ * next ign_forward_train. */
 int  ign_backward(ign_plan* plan, ign_batch* batch, const float* dpred, float* grads);
 /* The same two calls in steps, for a training step on an edge-cut partition (ABI 9): the caller
  * exchanges halo rows between the steps (ignnition_amd/partition.py EdgeCutTraining).

@@ -123,6 +123,26 @@ def test_adam_step_matches_keras_restatement():
     np.testing.assert_array_equal(Batch(fresh, graphs).forward(), Batch(eng, graphs).forward())
 
 
+def test_backward_consumes_the_forward():
+    """The readout backward writes the output layer's gradient rows over the saved activations
+    (fuse_outer_bwd), so a second backward of one forward is refused (ign_backward, ignmp.h); after
+    the next forward_train the backward runs again and gives the same bits."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 1)
+    prm = MPPlan.from_model_info(mi).init_params(1, bias_scale=0.1)
+    eng, b, pred, loss, g, grads = _engine_grads(desc, dims, graphs, labels, prm)
+    first = grads.clone()
+    y = torch.tensor(np.concatenate([np.asarray(l, np.float32).reshape(-1) for l in labels]), device="cuda")
+    dpred = torch.empty_like(y)
+    eng.mse_loss(b.predictions_ptr(), y, dpred)
+    with pytest.raises(Exception, match="one backward per forward"):
+        b.backward(dpred, grads)
+    b.forward_train(to_host=False)
+    eng.mse_loss(b.predictions_ptr(), y, dpred)
+    b.backward(dpred, grads)
+    torch.cuda.synchronize()
+    assert torch.equal(grads, first)
+
+
 def test_training_reduces_loss():
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 4)
     prm = MPPlan.from_model_info(mi).init_params(0)

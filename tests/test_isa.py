@@ -94,4 +94,4 @@ def test_resident_forward_fits_its_workgroup(asm_resident):
         print(name, vgpr.group(1), scratch.group(1))
         assert vgpr and int(vgpr.group(1)) <= 128, name
         assert scratch and int(scratch.group(1)) == 0, name
-    assert found == 2
+    assert found == 3

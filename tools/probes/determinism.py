@@ -35,5 +35,6 @@ for n in names:
     env = dict(os.environ)
     if n != "default":
         env["IGN_LIB_PATH"] = os.path.join(REPO, "ignnition_amd", "ab", "lib_%s.so" % n)
+        env["IGN_AB_LIB"] = "1"   # an A/B build may predate symbols _lib.py binds (as tools/ab_bitwise.py)
     r = subprocess.run([sys.executable, "-c", CHILD % REPO], env=env, capture_output=True, text=True, timeout=300)
     print("%-10s %s" % (n, r.stdout.strip() or r.stderr[-500:]), flush=True)
