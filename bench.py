@@ -770,18 +770,30 @@ def dry_run(args, dist, rank, world, mi, graphs, synthetic):
         emi, eplan, egraphs, part = edge_cut_parts(args, dist, rank, world)
         name = eplan.entities[0]
         halo = send = 0
+        recv_c, send_c = [0] * world, [0] * world   # rows this rank receives from / sends to each rank
         if part is not None:
             partition.exchange_requests([part], partition.TorchComm(dist, None))
             halo, send = part.halos[name].n_halo, len(part.halos[name].send_rows)
+            recv_c, send_c = list(part.halos[name].recv_counts), list(part.halos[name].send_counts)
             e_local = workloads.edges_per_forward(emi, [part.inputs])
         else:
             e_local = workloads.edges_per_forward(emi, egraphs)
         tot_e, tot_halo, tot_send = _reduce(dist, [e_local, halo, send], "sum")
+        # per rank pair: recv[i][j] (rows rank i reads from j) must equal send[j][i] (rows j sends i)
+        recv_m = [[0] * world for _ in range(world)]
+        send_m = [[0] * world for _ in range(world)]
+        recv_m[rank], send_m[rank] = recv_c, send_c
+        flat = _reduce(dist, [v for row in recv_m for v in row] + [v for row in send_m for v in row], "sum")
+        recv_m = [[int(flat[i * world + j]) for j in range(world)] for i in range(world)]
+        send_m = [[int(flat[world * world + i * world + j]) for j in range(world)] for i in range(world)]
         whole = workloads.edges_per_forward(emi, egraphs)
         edge_cut = {"value": None, "unit": "edges/s", "n_ranks": world, "nodes": args.edge_cut_nodes,
                     "edges_per_step": int(tot_e), "edges_per_step_whole_graph": int(whole),
                     "edges_match_whole_graph": int(tot_e) == int(whole),
-                    "halo_rows": {"total": int(tot_halo)}, "send_rows_total": int(tot_send), "dry_run": True}
+                    "halo_rows": {"total": int(tot_halo)}, "send_rows_total": int(tot_send),
+                    "halo_recv_by_pair": recv_m, "halo_send_by_pair": send_m,
+                    "halo_symmetric": all(recv_m[i][j] == send_m[j][i] for i in range(world) for j in range(world)),
+                    "dry_run": True}
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,

@@ -174,7 +174,10 @@ hipError_t launch_sum_seg(const SumSegArgs& args, int din, hipStream_t st);
 // H = DIN = 32, with the graph's source-entity states and the projected table in LDS; writes the
 // final states of every entity.  The source entities' rows of a graph form one "union" row range:
 // entity 0's rows, then entity 1's.
-constexpr int kResidentWaves = 16;
+#ifndef IGN_RES_WAVES   // A/B builds only (the host's eligibility assumes the default)
+#define IGN_RES_WAVES 16
+#endif
+constexpr int kResidentWaves = IGN_RES_WAVES;
 constexpr int kResidentMaxSrc = 2;
 constexpr int kResidentMaxTiles = 2 * kResidentWaves;   // union-row tiles of a graph (B2/B3: two per wave)
 constexpr int kResidentStateStride = 36;    // LDS floats per 32-wide state row

@@ -1766,7 +1766,11 @@ __global__ __launch_bounds__(64 * WAVES) void readout_h16_kernel(Readout3Args a,
       const u4v* src = W2v + (int64_t)nv * CHF + piece * 64 + lane;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+#ifndef IGN_RO_ABL_NODMA   // timing ablation (wrong results): every chunk reuses chunk 0
       asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+#else
+      (void)src; (void)m0;
+#endif
 #pragma clang diagnostic pop
     }
     __builtin_amdgcn_sched_barrier(0);

@@ -264,6 +264,9 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #endif
 
   const int64_t pt0 = a.ptile_off[gph], npt = (a.ptile_off[gph + 1] - pt0) / 16;
+#ifdef IGN_RES_PRIO   // A/B: static priority for the second-dispatched half (MI355X_MICROARCH.md, item 4)
+  if (wave >= kW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int it = 0; it < a.T; ++it) {
     // ---- phase A: the ordered update (seq_gru_h16's tile loop over the graph's path tiles) ----
 #ifdef IGN_RES_STATIC
@@ -357,25 +360,53 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
             h8 w[3];
 #pragma unroll
             for (int G = 0; G < 3; ++G) w[G] = su[((pu * 3 + G) * NT + i) * KS * 64 + lofs];
+#ifndef IGN_RES_ABL_MFMA
 #pragma unroll
             for (int ph = 1; ph >= 0; --ph) {
               if (pu + ph > 1) continue;
 #pragma unroll
               for (int G = 0; G < 3; ++G) acc[G][i] = MFMA_H(w[G], hf[ph][0], acc[G][i]);
             }
+#else   // timing ablation (wrong results): no MFMAs, the state still flows into the gates
+#pragma unroll
+            for (int G = 0; G < 3; ++G) acc[G][i] += h[i] + __builtin_bit_cast(f4, w[G]);
+#endif
           }
         const bool act = t < Lr;
+#ifdef IGN_RES_ABL_GATE   // timing ablation (wrong results): one fma per element instead of the gates
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(acc[0][i][r], c, xx[0][i][r])));
-            const float rc = rcpf_(fmaf(__builtin_amdgcn_exp2f(fmaf(acc[1][i][r], c, xx[1][i][r])), SS, SS));
-            const float n = S * tanh2_(fmaf(rc, acc[2][i][r], xx[2][i][r]));
-            const float hn = n + z * (h[i][r] - n);
-            if constexpr (decltype(masked)::value) h[i][r] = act ? hn : h[i][r];
-            else h[i][r] = hn;
-          }
+          for (int r = 0; r < 4; ++r)
+            h[i][r] = fmaf(fmaf(acc[0][i][r], c, xx[0][i][r]), 1e-3f, fmaf(acc[2][i][r], c, xx[2][i][r]) * 1e-3f);
+        (void)masked; (void)act;
+        return;
+#endif
+        // the gates stage by stage across the lane's 8 elements (the same arithmetic as seq_gru_h16, so the
+        // same bits): the exponentials of all 8, then the reciprocals, then the candidates; the compiler
+        // otherwise chains each element's exp -> rcp through one register (phase A -2.4 %, stamps)
+        float ez[8], er[8], zz[8], gg[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ez[e] = __builtin_amdgcn_exp2f(fmaf(acc[0][e >> 2][e & 3], c, xx[0][e >> 2][e & 3]));
+          er[e] = __builtin_amdgcn_exp2f(fmaf(acc[1][e >> 2][e & 3], c, xx[1][e >> 2][e & 3]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          zz[e] = rcpf_(1.0f + ez[e]);
+          gg[e] = fmaf(rcpf_(fmaf(er[e], SS, SS)), acc[2][e >> 2][e & 3], xx[2][e >> 2][e & 3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = e >> 2, r = e & 3;
+          const float n = S * tanh2_(gg[e]);
+          const float hn = n + zz[e] * (h[i][r] - n);
+          if constexpr (decltype(masked)::value) h[i][r] = act ? hn : h[i][r];
+          else h[i][r] = hn;
+        }
+
       };
       // the tile's shortest sequence: its last real path's (tiles are padded at the graph's end)
       const int Lmin = __builtin_amdgcn_readlane(Lr, (int)min<int64_t>(15, P - 1 - 16 * k));

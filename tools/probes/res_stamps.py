@@ -21,7 +21,8 @@ from ignnition_amd.engine import Batch, Engine, MPPlan  # noqa: E402
 
 def main():
     n = int(os.environ.get("GRAPHS", "256"))
-    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", os.environ.get("TOPO", "geant2"), n)
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs(os.environ.get("MODEL", "routenet"),
+                                                            os.environ.get("TOPO", "geant2"), n)
     plan = MPPlan.from_model_info(mi)
     eng = Engine(plan, 0)
     eng.set_params(plan.init_params(seed=0, bias_scale=0.05))
@@ -32,7 +33,7 @@ def main():
     fn = _lib.lib.ign_debug_res_stamps
     fn.restype = C.c_int
     fn.argtypes = [C.c_void_p, C.c_int]
-    W = 16
+    W = int(os.environ.get("RES_WAVES", "16"))
     buf = np.zeros(256 * W * 8, np.uint64)
     rc = fn(buf.ctypes.data_as(C.c_void_p), buf.size)
     v = buf.reshape(256, W, 8)[:min(n, 256)].astype(np.float64)
@@ -45,6 +46,10 @@ def main():
            "B1_cycles_per_wave_mean": float(v[:, :, 5].mean()),
            "B1_B2_cycles_per_wave_mean": float(v[:, :, 6].mean()),
            "A_work_per_wave": [float(x) for x in v[:, :, 1].mean(axis=0)],
+           # phase A's wall cycles (work + barrier wait, the same span for every wave) per tile-step of
+           # one SIMD (the graph's tile-steps over its 4 SIMDs), against tools/isa_mix.py's issue floor
+           "phase_A_cycles_per_tile_step_per_simd": float((v[:, :, 1] + v[:, :, 2]).mean()) /
+                                                     (b.resident_info()["tile_steps"] / n / 4.0),
            "B_work_per_wave": [float(x) for x in v[:, :, 3].mean(axis=0)]}
     print(json.dumps(out, indent=1))
 
