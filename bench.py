@@ -383,6 +383,7 @@ def main():
     from ignnition_amd import workloads
     from ignnition_amd.engine import Batch, Engine, MPPlan, SplitBatch
 
+    fresh_stats = None   # --fresh-batches: the main thread's wait for the next batch vs the step itself
     engines = []   # every engine of the step (--streams: one per sub-batch)
     subs = []      # --streams: the sub-batches
     batches = []   # the forward's batches (resident_info)
@@ -507,8 +508,17 @@ def main():
             batches = trainer.prefetch(source.ids(), depth=args.input_workers + 1, workers=args.input_workers,
                                        load=source.load)
 
+        pipe_t = {"wait_s": 0.0, "step_s": 0.0, "steps": 0}
+
         def step():   # train_and_evaluate's loop (FO:108-166): next batch from the pipeline, one step
-            trainer.train_prepared(*next(batches))
+            t0 = time.perf_counter()
+            nb = next(batches)
+            t1 = time.perf_counter()
+            trainer.train_prepared(*nb)
+            pipe_t["wait_s"] += t1 - t0
+            pipe_t["step_s"] += time.perf_counter() - t1
+            pipe_t["steps"] += 1
+        fresh_stats = pipe_t
         if not args.no_prefetch:
             cleanup.append(batches.close)
     elif args.streams > 1 and not args.train and len(graphs) > 1:
@@ -696,6 +706,12 @@ def main():
     }
     if edge_cut is not None:
         line[edge_cut_key(args.edge_cut_nodes)] = edge_cut
+    if fresh_stats and fresh_stats["steps"]:
+        n = fresh_stats["steps"]   # warm-up included
+        line["input_pipeline"] = {"workers": 0 if args.no_prefetch else args.input_workers,
+                                  "ms_waiting_for_batch": round(1e3 * fresh_stats["wait_s"] / n, 2),
+                                  "ms_in_step": round(1e3 * fresh_stats["step_s"] / n, 2), "steps": n,
+                                  "host_cpus_granted": int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None}
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
