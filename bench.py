@@ -446,10 +446,13 @@ def main():
     halo_rows = 0
     if args.streams <= 0:
         # auto: more, smaller sub-batches where the kernels are short -- small graphs (GEANT2, NSFNET)
-        # or a step of three or more MPs per iteration (Q-size: 4.15-4.18 ms/step with 4 streams
-        # against 4.39-4.41 with 2; RouteNet synth50 is flat from 2 to 4: profiles/r04/streams/)
+        # or, on the batched launches, a step of three or more MPs per iteration (Q-size: 4.15-4.18
+        # ms/step with 4 streams against 4.39-4.41 with 2; profiles/r04/streams/).  On the
+        # graph-resident forward Q-size takes 2 (3.247 ms against 3.316 with 1 and 3.308 with 4,
+        # profiles/r05/streams/), RouteNet synth50 2 (flat from 2 to 4 in round 4)
         sizes = [int(np.asarray(g[k]).reshape(())) for g in graphs[:1] for k in g if k.startswith("num_")]
-        args.streams = 4 if (sizes and max(sizes) < 1000) or len(plan.mps) >= 3 else 2
+        batched = os.environ.get("IGN_RESIDENT") == "0"
+        args.streams = 4 if (sizes and max(sizes) < 1000) or (batched and len(plan.mps) >= 3) else 2
     if synthetic and world > 1:
         import torch
         from ignnition_amd import partition
