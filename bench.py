@@ -37,9 +37,9 @@ PEAK_HBM_GBS = 8000.0
 PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md), the split-bf16 kernels' pipe
 CLOCK_GHZ = 2.4                  # MI355X peak engine clock (spec), the issue roof's clock
 N_CU = 256
-RES_KERNEL = {0: "_Z23resident_forward_kernelILb0ELb1EEv12ResidentArgs",   # form -> instance (resident.hip)
-              1: "_Z23resident_forward_kernelILb1ELb1EEv12ResidentArgs",
-              2: "_Z23resident_forward_kernelILb1ELb0EEv12ResidentArgs"}
+RES_KERNEL = {0: "_Z23resident_forward_kernelILb0ELb1ELb0EEv12ResidentArgs",   # form -> instance (resident.hip)
+              1: "_Z23resident_forward_kernelILb1ELb1ELb0EEv12ResidentArgs",
+              2: "_Z23resident_forward_kernelILb1ELb0ELb0EEv12ResidentArgs"}
 
 
 def parse():

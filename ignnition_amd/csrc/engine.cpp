@@ -223,6 +223,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
     p->resident_path_global = atoi(v) == 2;
   }
   if (const char* v = getenv("IGN_RESIDENT_PG")) p->resident_pg = atoi(v) != 0;
+  if (const char* v = getenv("IGN_RESIDENT_TRAIN")) p->resident_train = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_H16")) p->train_dense_h16 = atoi(v) != 0;
@@ -719,7 +720,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   std::vector<std::vector<int32_t>> pp(G);
   const int64_t ND = (int64_t)ma.h_order.size();
   for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
-  hvec<int32_t> ptile_off(G + 1, 0), hdr, lcode_off(G + 1, 0);
+  hvec<int32_t> ptile_off(G + 1, 0), hdr, hsb, lcode_off(G + 1, 0);
   double tile_steps = 0;
   hvec<uint16_t> lcode;
   size_t lds[3] = {0, 0, 0};
@@ -733,6 +734,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       const int32_t len = ma.h_len[i], sp = ma.h_step_ptr[i];
       hdr.push_back((int32_t)(ma.h_order[i] - po[g]));
       hdr.push_back(len);
+      hsb.push_back(sp + (int32_t)i);   // the training forward's hs_save rows of position i
       hdr.push_back((int32_t)(lcode.size() - c0));
       for (int32_t t = 0; t < len; ++t) {
         const uint32_t c = ma.h_step_code[sp + t];
@@ -752,8 +754,9 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     }
     const int32_t pad = (int32_t)(lcode.size() - c0);
     lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)U);
-    for (int64_t k = n; k < np; ++k) {   // padding: length 0, hole codes
-      hdr.push_back(0);
+    for (int64_t k = n; k < np; ++k) {   // padding: row -1, length 0, hole codes
+      hsb.push_back(0);
+      hdr.push_back(-1);
       hdr.push_back(0);
       hdr.push_back(pad);
       hdr.push_back((int32_t)U);
@@ -772,6 +775,9 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     form = lds[1] <= kResidentMaxDynLds ? IGN_RES_PATH_GLOBAL : IGN_RES_PATH_CSR_GLOBAL;
     if (lds[form] > kResidentMaxDynLds) return IGN_OK;
   }
+  // the training forward's form: path states in global memory always (their versions)
+  b->res_train_form = lds[1] <= kResidentMaxDynLds ? IGN_RES_PATH_GLOBAL : IGN_RES_PATH_CSR_GLOBAL;
+  b->res_train_lds = lds[b->res_train_form];
   HIP_TRY(resident_prepare_device());
   std::vector<int64_t> pov(po.begin(), po.end());
   int rc;
@@ -784,6 +790,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       (rc = dev_upload(b, &b->d_res_lmsg_off, lmsg_off)) || (rc = dev_upload(b, &b->d_res_lmsg_ptr, lmsg_ptr)) ||
       (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)) || (rc = dev_upload(b, &b->d_res_lorder, lorder)) ||
       (rc = dev_upload(b, &b->d_res_lnseg, lnseg)) || (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
+      (rc = dev_upload(b, &b->d_res_hsb, hsb)) ||
       (rc = dev_upload(b, &b->d_res_lcode, lcode)))
     return rc;
   b->res_lds = lds[form];
@@ -1801,9 +1808,11 @@ int copy_out(ign_plan* p, ign_batch* b, float* pred_out) {
   return IGN_OK;
 }
 
+}  // namespace
+
 // the whole MP loop of a resident batch in one launch; the final states land in
-// buffer 0 of every entity
-static int resident_forward(ign_plan* p, ign_batch* b) {
+// buffer 0 of every entity, or (save: the training forward) in the state versions save names
+extern "C++" int ign::resident_launch(ign_plan* p, ign_batch* b, const ResidentSave* save) {
   ResShape sh;
   if (!resident_plan_shape(p, &sh)) return fail(IGN_ERR_RUNTIME, "resident batch on a plan of another shape");
   const MPP& a = p->mps[0];
@@ -1842,19 +1851,50 @@ static int resident_forward(ign_plan* p, ign_batch* b) {
   r.proj_b = p->d_packed + ca.pk_b;
   r.proj_Wf = p->d_packed + ca.pk_w;
   r.T = p->T;
+  r.seg_on = save ? 0 : 1;   // the training forward's sums are all lane walks (sum_gru_g32 with x_save)
+  if (save) {
+    r.path_ver = save->path_ver;
+    r.hs_save = save->hs_save;
+    r.hsb = b->d_res_hsb;
+    for (int s = 0; s < sh.n_src; ++s) {
+      r.src_ver[s] = save->src_ver[s];
+      r.x_save[s] = save->x_save[s];
+    }
+  }
   const ign_resident_info_t& ri = b->res_info;
   Timer tm{p};
   tm.begin(K_RESIDENT, ri.flops, ri.bytes_stage, ri.mfma_bf16, ri.mfma_f32);
-  HIP_TRY(launch_resident_forward(r, b->G, b->res_lds, b->res_form, p->stream));
+  HIP_TRY(launch_resident_forward(r, b->G, save ? b->res_train_lds : b->res_lds, save ? b->res_train_form : b->res_form,
+                                  save != nullptr, p->stream));
   tm.end();
-  b->cur[path] = 0;
-  for (int s = 0; s < sh.n_src; ++s) b->cur[sh.src_ent[s]] = 0;
+  if (!save) {
+    b->cur[path] = 0;
+    for (int s = 0; s < sh.n_src; ++s) b->cur[sh.src_ent[s]] = 0;
+  }
   return IGN_OK;
 }
 
+// the batch's resident tables, built once (the first ign_forward or training forward)
+extern "C++" int ign::resident_tables(ign_plan* p, ign_batch* b) {
+  if (b->res_tried) return IGN_OK;
+  b->res_tried = true;
+  return resident_batch(p, b);
+}
+
+// MPs 1 .. S of a resident plan: the sum MP back to each source entity of MP 0 (s order)
+extern "C++" int ign::resident_sum_mps(const ign_plan* p, int* sum_mp, int* n_src) {
+  ResShape sh;
+  if (!resident_plan_shape(p, &sh)) return 0;
+  *n_src = sh.n_src;
+  for (int s = 0; s < sh.n_src; ++s) sum_mp[s] = sh.sum_mp[s];
+  return 1;
+}
+
+namespace {
+
 int forward_body(ign_plan* p, ign_batch* b) {
   if (b->resident) {
-    const int rc = resident_forward(p, b);
+    const int rc = resident_launch(p, b, nullptr);
     return rc ? rc : readout(p, b);
   }
   int rc = ign_forward_begin(p, b);
@@ -1913,10 +1953,7 @@ int ign_forward_end(ign_plan* p, ign_batch* b, float* pred_out) {
 int ign_forward(ign_plan* p, ign_batch* b, float* pred_out) {
   int rc = check_pb(p, b);
   if (rc) return rc;
-  if (!b->res_tried) {   // before any capture: the tables are uploaded here
-    b->res_tried = true;
-    if ((rc = resident_batch(p, b))) return rc;
-  }
+  if ((rc = resident_tables(p, b))) return rc;   // before any capture: the tables are uploaded here
   // HIP event records captured into a graph report 0 ms on this runtime, so timed forwards
   // launch directly; untimed ones replay the captured graph
   if (p->use_graph && p->stream && !p->timing) {

@@ -270,6 +270,7 @@ struct ign_plan {
   bool resident = true;           // graph-resident forward for small RouteNet-shaped graphs (IGN_RESIDENT=0: off)
   bool resident_pg = true;        // ... with the path states in global memory where they do not fit LDS (IGN_RESIDENT_PG)
   bool resident_path_global = false;   // IGN_RESIDENT=2: that form for every eligible batch (tests)
+  bool resident_train = true;     // the training forward on the resident form's SAVE variant (IGN_RESIDENT_TRAIN=0: off)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
                                   // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
                                   // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);
@@ -332,6 +333,9 @@ struct ign_batch {
   int32_t* d_res_lnseg = nullptr;
   int32_t* d_res_lcode_off = nullptr;
   uint16_t* d_res_lcode = nullptr;
+  int32_t* d_res_hsb = nullptr;   // per header: the training forward's hs_save row of the position
+  int res_train_form = 0;         // the training forward's form (path states in global memory) ...
+  size_t res_train_lds = 0;       // ... and its dynamic LDS
   std::vector<char> proj_ready;
   float* d_ro_in = nullptr;                     // concat scratch (multi-input readout)
   std::vector<float*> d_ro_tmp;                 // generic readout intermediates
@@ -353,6 +357,16 @@ struct ign_batch {
 };
 
 namespace ign {
+// the graph-resident forward (engine.cpp, resident.hip): save = the training forward's state versions
+struct ResidentSave {
+  float* const* path_ver;                    // [T + 1] the path entity's versions
+  float* const* src_ver[kResidentMaxSrc];    // [T + 1] per source entity of the ordered MP
+  float* const* hs_save;                     // [T] the ordered MP's per-step states
+  float* const* x_save[kResidentMaxSrc];     // [T] per source entity: its sum MP's message sums
+};
+int resident_tables(ign_plan* p, ign_batch* b);   // once per batch; leaves b->resident false if not eligible
+int resident_launch(ign_plan* p, ign_batch* b, const ResidentSave* save);
+int resident_sum_mps(const ign_plan* p, int* sum_mp, int* n_src);   // 0: not a resident plan shape
 int set_device(int dev);
 int ensure_device(ign_plan* p);
 int dev_alloc(ign_batch* b, float** out, int64_t n);

@@ -214,10 +214,22 @@ struct ResidentArgs {
   const float* proj_Wf;       // ... and as project_kernel's f32 fragments (the iteration-0 projection)
   int T;
   int n_src;
+  int seg_on;                 // 0: every message sum as the lane walk (the training forward's sums)
+  // SAVE (the training forward, global-path forms): iteration it's ordered MP reads the path states
+  // path_ver[it] and writes path_ver[it + 1] and every step's state into hs_save[it] from row hsb of
+  // each position (seq_gru_h16<SAVE>'s layout); the sum MPs write their message sums into
+  // x_save[s][it] and their new states into src_ver[s][it + 1]; every iteration projects with f32
+  // MFMA (build_table's project_kernel).  ver[.][0] hold the initial states (init_state).
+  float* const* path_ver;
+  float* const* src_ver[kResidentMaxSrc];
+  float* const* hs_save;
+  float* const* x_save[kResidentMaxSrc];
+  const int32_t* hsb;         // [headers] the position's first hs_save row (step_ptr + order position)
 };
 // the kernels' dynamic-LDS limit, once per device: call before any launch or stream capture
 hipError_t resident_prepare_device();
-hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, int form, hipStream_t st);
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, int form, bool save,
+                                   hipStream_t st);
 bool readout3_supported(int din, int n1, int n2, int act1, int act2);
 hipError_t launch_readout3(const Readout3Args& args, int din, int n1, int n2, hipStream_t st);
 // readout on split-bf16 contractions (fp32-exact operands; passes 6 or 9), weights from

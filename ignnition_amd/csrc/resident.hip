@@ -179,8 +179,9 @@ __device__ __forceinline__ f4 gru_half(const void* Wbf, const void* Ubf, const f
 // ordered MP's step codes are read from global memory: the form for graphs whose path states do
 // not fit (synth50: 2 450 paths).  CL: the sum MPs' CSR (message rows) in LDS; else read from L2
 // (Q-size synth50: its two sum MPs' 14 k messages do not fit beside the 250 union rows' table)
-template <bool PG, bool CL>
+template <bool PG, bool CL, bool SAVE>
 __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs a) {
+  static_assert(PG || !SAVE, "the training form keeps the path states in global memory (versions)");
   constexpr int H = 32, NT = 2, KS = 1, NF = 6 * NT * KS;   // U's fp16 pieces: 2 pieces x 3 gates x NT
   __shared__ h8 su[NF * 64];
   __shared__ float sbn[kW][H];
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   const int64_t L1 = a.n_src > 1 ? a.src_off[1][gph + 1] - s10 : 0;
   const int64_t U = L0 + L1;   // union rows: entity 0's, then entity 1's
   constexpr int SPP = PG ? H : SP;   // row stride of the path states
-  float* hP = PG ? a.path_state + p0 * H : dyn;
+  float* hP = PG ? (SAVE ? a.path_ver[0] : a.path_state) + p0 * H : dyn;   // (SAVE: per iteration below)
   float* hL = PG ? dyn : hP + P * SP;
   float* tab = hL + U * SP;
   int* smp = reinterpret_cast<int*>(tab + (U + 1) * ST);   // the sum MPs' CSR by local union row
@@ -220,8 +221,8 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     for (int e = tid; e < NF * 64; e += 64 * kW) dst[e] = src[e];
   }
   const int es = __float_as_int(reinterpret_cast<const float*>(a.Uh)[(int64_t)NF * 64 * 4]);
-  // GM:396-400: state_0 = [features | zeros]
-  for (int64_t i = tid; i < P * H; i += 64 * kW) {
+  // GM:396-400: state_0 = [features | zeros] (SAVE: path_ver[0] holds it already)
+  for (int64_t i = SAVE ? P * H : tid; i < P * H; i += 64 * kW) {
     const int64_t r = i / H;
     const int c = (int)(i - r * H);
     hP[r * SPP + c] = c < a.path_F ? a.path_feat[(p0 + r) * a.path_F + c] : 0.f;
@@ -268,6 +269,10 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   if (wave >= kW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
   for (int it = 0; it < a.T; ++it) {
+    // the path states this iteration reads (hPi) and writes (hPo): one buffer, or the versions
+    const float* hPi = SAVE ? a.path_ver[it] + p0 * H : hP;
+    float* hPo = SAVE ? a.path_ver[it + 1] + p0 * H : hP;
+    float* hsv = SAVE ? a.hs_save[it] : nullptr;
     // ---- phase A: the ordered update (seq_gru_h16's tile loop over the graph's path tiles) ----
 #ifdef IGN_RES_STATIC
     auto claim = [&](int k) -> int { return k < 0 ? wave : k + kW; };   // A/B: wave w takes tiles w, w + 16, ...
@@ -289,14 +294,22 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       const int kn = claim(k);
       if (kn < npt) hd_next = *reinterpret_cast<const i4v*>(a.hdr + 4 * (pt0 + 16 * kn + j));
       const int Lr = hd[1];
-      const bool valid = Lr > 0;   // tile padding: length 0
+      const bool valid = hd[0] >= 0;   // tile padding: row -1 (a real path may have length 0)
       const int64_t rl = valid ? hd[0] : 0;
       const int cbase = hd[2];   // (an index, not a pointer: one VGPR live through the tile)
       f4 h[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const f4 v = lds4(hP + rl * SPP + 16 * t + 4 * g);
+        const f4 v = lds4(hPi + rl * SPP + 16 * t + 4 * g);
         h[t] = valid ? v : f4{0, 0, 0, 0};
+      }
+      int hb = 0;   // SAVE: the position's first hs_save row, the state before the sequence
+      if constexpr (SAVE) {
+        hb = a.hsb[pt0 + 16 * k + j];
+        if (valid) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) st4(hsv + (int64_t)hb * H + 16 * t + 4 * g, h[t]);
+        }
       }
       f4 x[3][NT];
       auto load_x = [&](uint32_t code, f4 (&xx)[3][NT]) __attribute__((always_inline)) {
@@ -413,13 +426,19 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       for (int t = 0;;) {
         if (t < Lmin) step(t, x, std::false_type{});
         else step(t, x, std::true_type{});
+        if constexpr (SAVE) {   // the state after step t (seq_gru_h16<SAVE>'s save)
+          if (valid && t < Lr) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i) st4(hsv + (int64_t)(hb + t + 1) * H + 16 * i + 4 * g, h[i] * iS);
+          }
+        }
         if (++t >= Lmax) break;
         load_x(code, x);
         code = scd[cbase + t + 1];
       }
       if (valid) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) lds4w(hP + rl * SPP + 16 * t + 4 * g, h[t] * iS);
+        for (int t = 0; t < NT; ++t) lds4w(hPo + rl * SPP + 16 * t + 4 * g, h[t] * iS);
       }
       k = kn;
     }
@@ -438,7 +457,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     // messages q, q + 8, ... of the row (columns 4c .. 4c + 3), four rows in flight, then the eight
     // partial sums pairwise across lanes (xor 32, 16, 8).  The others: sum_gru_g32's lane walk, one
     // lane per (row, float4 column) adding in message order from zero, long chains first.
-    const int nseg = a.lnseg[gph];
+    const int nseg = a.seg_on ? a.lnseg[gph] : 0;
     for (int k = wave; k < nseg; k += kW) {
       const int ll = slo[k];
       int lo = lane;   // opaque: the lane's column pointer stays inside the loop (no spill, as project_row)
@@ -446,7 +465,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       const int c = lo & 7, q = lo >> 3;
       const int m0 = smp[ll], m1 = smp[ll + 1];
       const int last = m1 > m0 ? m1 - 1 : m0;
-      const float* hp = hP + 4 * c;
+      const float* hp = hPo + 4 * c;
       f4 acc = {0, 0, 0, 0};
       int cc[4];
 #pragma unroll
@@ -483,7 +502,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       const int64_t ll = slo[i >> 3];   // rows by message count, descending: the long chains first
       const int c4 = (int)(i & 7);
       const int m0 = smp[ll], m1 = smp[ll + 1];
-      const float* hp = hP + 4 * c4;
+      const float* hp = hPo + 4 * c4;
       f4 x = {0, 0, 0, 0};
       int m = m0;
       if constexpr (PG) {   // rows from L2: sixteen in flight (two groups of eight double-buffered
@@ -511,6 +530,10 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       }
       for (; m < m1; ++m) x = x + lds4(hp + sms[m] * SPP);
       lds4w(xs + ll * SP + 4 * c4, x);
+      if constexpr (SAVE) {   // sum_gru_g32's x_save, by the entity's global row
+        const bool e1 = ll >= L0;
+        st4((e1 ? a.x_save[1][it] + (s10 + ll - L0) * H : a.x_save[0][it] + (s00 + ll) * H) + 4 * c4, x);
+      }
     }
     __syncthreads();
 #ifdef IGN_RES_STAMP
@@ -564,8 +587,16 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       if (valid) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn[t]);
+        if constexpr (SAVE) {   // the entity's next version
+          float* o = e1 ? a.src_ver[1][it + 1] + (s10 + ll - L0) * H : a.src_ver[0][it + 1] + (s00 + ll) * H;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) st4(o + 16 * t + 4 * g, hn[t]);
+        }
       }
-      if (!last) project_row(a, hn, tab, ll, valid, lane, g);
+      if (!last) {
+        if constexpr (SAVE) project_row_f32(a, hn, tab, ll, valid, lane, g);   // build_table's projection
+        else project_row(a, hn, tab, ll, valid, lane, g);
+      }
     }
 #ifdef IGN_RES_STAMP
     IGN_STAMP(t_b);
@@ -584,7 +615,9 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     o[7] = t_a - t_0;
   }
 #endif
-  // the final states leave the workgroup (the readout and ign_batch_state read them)
+  // the final states leave the workgroup (the readout and ign_batch_state read them; SAVE: the
+  // versions hold every state already)
+  if constexpr (SAVE) return;
   if constexpr (!PG)   // PG: the path states are already there
     for (int64_t i = tid; i < P * (H / 4); i += 64 * kW) {
       const int64_t r = i / (H / 4);
@@ -609,9 +642,11 @@ hipError_t resident_prepare_device() {
   std::lock_guard<std::mutex> lk(mu);
   if ((int)done.size() <= dev) done.resize(dev + 1, 0);
   if (done[dev]) return hipSuccess;
-  for (const void* k : {reinterpret_cast<const void*>(resident_forward_kernel<false, true>),
-                        reinterpret_cast<const void*>(resident_forward_kernel<true, true>),
-                        reinterpret_cast<const void*>(resident_forward_kernel<true, false>)}) {
+  for (const void* k : {reinterpret_cast<const void*>(resident_forward_kernel<false, true, false>),
+                        reinterpret_cast<const void*>(resident_forward_kernel<true, true, false>),
+                        reinterpret_cast<const void*>(resident_forward_kernel<true, false, false>),
+                        reinterpret_cast<const void*>(resident_forward_kernel<true, true, true>),
+                        reinterpret_cast<const void*>(resident_forward_kernel<true, false, true>)}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResidentMaxDynLds);
     if (e != hipSuccess) return e;
   }
@@ -619,16 +654,22 @@ hipError_t resident_prepare_device() {
   return hipSuccess;
 }
 
-hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, int form, hipStream_t st) {
+hipError_t launch_resident_forward(const ResidentArgs& a, int n_graphs, size_t lds_bytes, int form, bool save,
+                                   hipStream_t st) {
   if (n_graphs == 0) return hipSuccess;
   if (lds_bytes > kResidentMaxDynLds || a.n_src < 1 || a.n_src > kResidentMaxSrc) return hipErrorInvalidValue;
+  if (save && (form == IGN_RES_ALL_LDS || !a.path_ver || !a.hs_save || !a.hsb)) return hipErrorInvalidValue;
   const dim3 grid((unsigned)n_graphs), block(64 * kW);
-  if (form == IGN_RES_PATH_CSR_GLOBAL)
-    hipLaunchKernelGGL((resident_forward_kernel<true, false>), grid, block, lds_bytes, st, a);
+  if (save && form == IGN_RES_PATH_CSR_GLOBAL)
+    hipLaunchKernelGGL((resident_forward_kernel<true, false, true>), grid, block, lds_bytes, st, a);
+  else if (save)
+    hipLaunchKernelGGL((resident_forward_kernel<true, true, true>), grid, block, lds_bytes, st, a);
+  else if (form == IGN_RES_PATH_CSR_GLOBAL)
+    hipLaunchKernelGGL((resident_forward_kernel<true, false, false>), grid, block, lds_bytes, st, a);
   else if (form == IGN_RES_PATH_GLOBAL)
-    hipLaunchKernelGGL((resident_forward_kernel<true, true>), grid, block, lds_bytes, st, a);
+    hipLaunchKernelGGL((resident_forward_kernel<true, true, false>), grid, block, lds_bytes, st, a);
   else if (form == IGN_RES_ALL_LDS)
-    hipLaunchKernelGGL((resident_forward_kernel<false, true>), grid, block, lds_bytes, st, a);
+    hipLaunchKernelGGL((resident_forward_kernel<false, true, false>), grid, block, lds_bytes, st, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -86,6 +86,7 @@ struct TrainState {
   // edge-cut driver exchanges halo rows between the steps
   int f_it = 0, f_mi = 0;
   bool f_open = false;
+  float** res_ptrs = nullptr;   // the graph-resident training forward's version / save pointer arrays
   int b_ri = -1;
   bool b_open = false;
   hvec<int> dcur;                          // backward: current gradient buffer per entity
@@ -641,9 +642,61 @@ int ign_forward_train_end(ign_plan* p, ign_batch* b, float* pred_out) {
   return IGN_OK;
 }
 
+// The training forward's whole MP loop as one graph-resident launch (resident.hip's SAVE form,
+// DESIGN.md §3d) where the plan and batch allow it: the same states, per-step saves, message sums and
+// versions as ign_forward_train_mp's launches, and the same MP-instance records for the backward
+static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
+  *done = false;
+  int sum_mp[kResidentMaxSrc] = {-1, -1}, S = 0;
+  if (!p->resident_train || !resident_sum_mps(p, sum_mp, &S)) return IGN_OK;
+  int rc = resident_tables(p, b);
+  if (rc || !b->resident) return rc;
+  TrainState* t = b->train;
+  const int path = p->mps[0].dst, T = p->T;
+  int src_ent[kResidentMaxSrc] = {-1, -1};
+  for (int s = 0; s < S; ++s) src_ent[s] = p->mps[0].src[s].entity;
+  if ((int)t->ver[path].size() != T + 1) return IGN_OK;
+  for (int s = 0; s < S; ++s)
+    if ((int)t->ver[src_ent[s]].size() != T + 1) return IGN_OK;
+  // pointer arrays: path versions [T + 1] | per source: versions [T + 1] | hs_save [T] | per source: x_save [T]
+  const int64_t n_ptr = (T + 1) * (1 + S) + T * (1 + S);
+  if (!t->res_ptrs) {
+    hvec<float*> v;
+    for (int k = 0; k <= T; ++k) v.push_back(t->ver[path][k]);
+    for (int s = 0; s < S; ++s)
+      for (int k = 0; k <= T; ++k) v.push_back(t->ver[src_ent[s]][k]);
+    for (int k = 0; k < T; ++k) v.push_back(t->mp[0].hs[k]);
+    for (int s = 0; s < S; ++s)
+      for (int k = 0; k < T; ++k) v.push_back(t->mp[sum_mp[s]].xs[k]);
+    if ((int64_t)v.size() != n_ptr) return fail(IGN_ERR_RUNTIME, "resident training pointers");
+    if ((rc = tupload(t, &t->res_ptrs, v))) return rc;
+  }
+  ResidentSave sv{};
+  sv.path_ver = t->res_ptrs;
+  for (int s = 0; s < S; ++s) sv.src_ver[s] = t->res_ptrs + (T + 1) * (1 + s);
+  sv.hs_save = t->res_ptrs + (T + 1) * (1 + S);
+  for (int s = 0; s < S; ++s) sv.x_save[s] = t->res_ptrs + (T + 1) * (1 + S) + T * (1 + s);
+  if ((rc = resident_launch(p, b, &sv))) return rc;
+  // the records ign_forward_train_mp would have left (GM:404-603 order)
+  for (int it = 0; it < T; ++it)
+    for (int mi = 0; mi < (int)p->mps.size(); ++mi) {
+      const MPP& mp = p->mps[mi];
+      MPRec rec{mi, it, t->cur[mp.dst], {0, 0, 0, 0}};
+      for (size_t s = 0; s < mp.src.size(); ++s) rec.src_v[s] = t->cur[mp.src[s].entity];
+      t->cur[mp.dst] = rec.v_in + 1;
+      t->recs.push_back(rec);
+    }
+  t->f_it = T;
+  t->f_mi = 0;
+  *done = true;
+  return IGN_OK;
+}
+
 int ign_forward_train(ign_plan* p, ign_batch* b, float* pred_out) {
   int rc = ign_forward_train_begin(p, b);
-  for (int k = 0; !rc && k < p->T * (int)p->mps.size(); ++k) rc = ign_forward_train_mp(p, b);
+  bool done = false;
+  if (!rc) rc = resident_train_forward(p, b, &done);
+  for (int k = 0; !rc && !done && k < p->T * (int)p->mps.size(); ++k) rc = ign_forward_train_mp(p, b);
   return rc ? rc : ign_forward_train_end(p, b, pred_out);
 }
 

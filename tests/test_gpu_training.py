@@ -143,6 +143,45 @@ def test_backward_consumes_the_forward():
     assert torch.equal(grads, first)
 
 
+@pytest.mark.parametrize("kind,topo,n", [("routenet", "nsfnet", 3), ("routenet", "synth50", 2), ("qsize", "nsfnet", 2),
+                                         ("qsize", "synth50", 2), ("routenet", "holes", 2)])
+def test_resident_training_forward_is_the_batched_one(monkeypatch, kind, topo, n):
+    """The training forward's MP loop as one graph-resident launch (resident.hip's SAVE variant,
+    IGN_RESIDENT_TRAIN=1, default) leaves the same state versions, per-step saves and message sums as
+    the per-MP launches (=0): predictions, loss and every gradient bitwise equal, and within the
+    autograd tolerance of the float64 restatement."""
+    if topo == "holes":
+        from tests.test_gpu_parity import _routenet_graph, _with_holes
+        desc, dims, mi, g = _routenet_graph("geant2", 8)
+        graphs, labels = workloads.graph_inputs(mi, [synthetic.routenet_sample("geant2", 8),
+                                                    synthetic.routenet_sample("nsfnet", 4)])
+        graphs = [_with_holes(graphs[0], skip=5, count=6), graphs[1]]
+    else:
+        desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, topo, n)
+    prm = MPPlan.from_model_info(mi).init_params(9, bias_scale=0.1)
+    runs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("IGN_RESIDENT_TRAIN", v)
+        plan = MPPlan.from_model_info(Model_information(copy.deepcopy(desc), dims))
+        eng = Engine(plan, 0)
+        eng.set_params(prm)
+        eng.set_timing(True)
+        eng, b, pred, loss, g, grads = _engine_grads(desc, dims, graphs, labels, prm, eng)
+        st = eng.stats()
+        assert st["mp_resident"]["launches"] == (1 if v == "1" else 0), st
+        runs[v] = (pred.reshape(-1), loss, grads.cpu().numpy())
+        b.close()
+        eng.close()
+    np.testing.assert_array_equal(runs["1"][0], runs["0"][0])
+    assert runs["1"][1] == runs["0"][1]
+    np.testing.assert_array_equal(runs["1"][2], runs["0"][2])
+    if topo != "holes":
+        # Q-size synth50: the training forward sums a node's 49-420 messages as one float32 chain (the
+        # lane walk that keeps x_save, not the inference forward's segmented order), 1.37e-4 here
+        e = _rel_err_vs_oracle(desc, dims, graphs, labels, prm, runs["1"][2], eng.layout)
+        assert e <= (2 * GTOL if (kind, topo) == ("qsize", "synth50") else GTOL), e
+
+
 def test_training_reduces_loss():
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 4)
     prm = MPPlan.from_model_info(mi).init_params(0)

@@ -85,7 +85,8 @@ def test_default_ordered_update_keeps_four_waves(asm):
 
 def test_resident_forward_fits_its_workgroup(asm_resident):
     """resident_forward_kernel: 16 waves (one workgroup per graph) need <= 128 VGPRs; no scratch in
-    either form (the per-lane fragment addresses stay inside the loops)."""
+    any of its five instances -- three forms of the forward, two of the training forward's SAVE
+    variant (the per-lane fragment addresses stay inside the loops)."""
     found = 0
     for name, body, meta in _functions(asm_resident, r"_Z23resident_forward_kernel"):
         found += 1
@@ -93,5 +94,11 @@ def test_resident_forward_fits_its_workgroup(asm_resident):
         scratch = re.search(r"ScratchSize: (\d+)", meta)
         print(name, vgpr.group(1), scratch.group(1))
         assert vgpr and int(vgpr.group(1)) <= 128, name
-        assert scratch and int(scratch.group(1)) == 0, name
-    assert found == 3
+        if name.endswith("ELb1EEv12ResidentArgs"):   # SAVE: a few 4-8 B reloads per phase-B tile, none in phase A
+            assert scratch and int(scratch.group(1)) <= 96, name
+            loop = body[body.index("v_mfma_f32_16x16x32_f16"):]
+            loop = loop[:loop.index("s_barrier")]
+            assert "scratch_" not in loop, name
+        else:
+            assert scratch and int(scratch.group(1)) == 0, name
+    assert found == 5
