@@ -521,6 +521,7 @@ def main():
             pipe_t["wait_s"] += t1 - t0
             pipe_t["step_s"] += time.perf_counter() - t1
             pipe_t["steps"] += 1
+        pipe_t["trainer"] = trainer
         fresh_stats = pipe_t
         if not args.no_prefetch:
             cleanup.append(batches.close)
@@ -715,6 +716,10 @@ def main():
                                   "ms_waiting_for_batch": round(1e3 * fresh_stats["wait_s"] / n, 2),
                                   "ms_in_step": round(1e3 * fresh_stats["step_s"] / n, 2), "steps": n,
                                   "host_cpus_granted": int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None}
+        sp = getattr(fresh_stats.get("trainer"), "step_prof", None)
+        if sp and sp["steps"]:   # IGN_STEP_PROF=1: the step's host phases (ms per step)
+            line["input_pipeline"]["step_phases_ms"] = {k: round(1e3 * v / sp["steps"], 2) for k, v in sp.items()
+                                                        if k != "steps"}
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -11,7 +11,7 @@
 // IGN_POOL=0 bypasses the cache (hipMalloc / hipFree per block).  IGN_POOL_POISON=1 fills every
 // scratch block it hands out with NaN (0xFF bytes): the parity tests under it show that no kernel
 // reads batch scratch it has not written (tests/test_gpu_parity.py).  IGN_POOL_CACHE_GB caps the
-// idle bytes kept (default 16; ign_plan_trim_cache releases them all).
+// idle bytes kept (default: half the device's memory; ign_plan_trim_cache releases them all).
 //
 // The host side has the same problem: the batch builders' index tables are ~10^8 bytes of host
 // memory per batch.  hvec (engine_internal.h) draws blocks >= 1 MiB from a process-wide cache
@@ -73,14 +73,17 @@ struct DevPool {
   int device = 0;
 
   // free idle blocks whose fence has completed, oldest classes' first, until idle_bytes <= target;
-  // with wait, also those still in flight (their fences are waited for)
-  void trim(size_t target, bool wait) {
+  // with wait, also those still in flight (their fences are waited for).  With out, the blocks are
+  // only taken out of the cache and handed back for the caller to hipFree once it has dropped the
+  // lock (hipFree waits for the device: under the lock it stalled every other thread's release)
+  void trim(size_t target, bool wait, std::vector<void*>* out = nullptr) {
     for (auto it = idle.begin(); it != idle.end() && idle_bytes > target;) {
       auto& v = it->second;
       for (size_t i = 0; i < v.size() && idle_bytes > target;) {
         if (wait && v[i].fence->ev) hipEventSynchronize(v[i].fence->ev);
         if (v[i].fence->ready()) {
-          hipFree(v[i].ptr);
+          if (out) out->push_back(v[i].ptr);
+          else hipFree(v[i].ptr);
           idle_bytes -= it->first;
           v.erase(v.begin() + i);
         } else {
@@ -102,7 +105,15 @@ std::shared_ptr<DevPool> pool_create(int device) {
   pool->device = device;
   pool->enabled = env_int("IGN_POOL", 1) != 0;
   pool->poison = env_int("IGN_POOL_POISON", 0) != 0;
-  pool->cap = (size_t)std::max(0, env_int("IGN_POOL_CACHE_GB", 16)) << 30;
+  // default cap: half the device's memory.  A training batch of 512 x synth50 holds ~11 GB of
+  // device blocks and the input pipeline keeps workers + 1 of them in flight; under a smaller cap
+  // (16 GB before) every release trimmed blocks with hipFree -- which waits for the device -- under
+  // the pool lock that the step's own release then waited for: 22 -> 57 ms per fresh-batch step
+  size_t half = (size_t)16 << 30;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.totalGlobalMem / 2 > half) half = prop.totalGlobalMem / 2;
+  const int gb = env_int("IGN_POOL_CACHE_GB", -1);
+  pool->cap = gb >= 0 ? (size_t)gb << 30 : half;
   return pool;
 }
 
@@ -167,16 +178,20 @@ void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t a
     fence->ev = nullptr;
     if (after) hipStreamSynchronize(after);
   }
-  std::lock_guard<std::mutex> g(pool->mu);
-  for (void* b : blocks) {
-    auto it = pool->live.find(b);
-    if (it == pool->live.end()) continue;   // not ours (cannot happen): leave it alone
-    const size_t cls = it->second;
-    pool->live.erase(it);
-    pool->idle[cls].push_back({b, fence});
-    pool->idle_bytes += cls;
+  std::vector<void*> victims;
+  {
+    std::lock_guard<std::mutex> g(pool->mu);
+    for (void* b : blocks) {
+      auto it = pool->live.find(b);
+      if (it == pool->live.end()) continue;   // not ours (cannot happen): leave it alone
+      const size_t cls = it->second;
+      pool->live.erase(it);
+      pool->idle[cls].push_back({b, fence});
+      pool->idle_bytes += cls;
+    }
+    if (pool->idle_bytes > pool->cap) pool->trim(pool->cap, false, &victims);
   }
-  if (pool->idle_bytes > pool->cap) pool->trim(pool->cap, false);
+  for (void* v : victims) hipFree(v);
 }
 
 // ---- host blocks ----------------------------------------------------------------------------
@@ -186,8 +201,9 @@ struct HostCache {
   std::mutex mu;
   std::map<size_t, std::vector<void*>> idle;   // by size class
   std::unordered_map<void*, bool> pinned;      // every live or idle block -> registered for DMA
-  size_t idle_bytes = 0;
+  size_t idle_bytes = 0, live_bytes = 0;
   size_t cap = 0;
+  int64_t n_map = 0, n_unmap = 0;   // IGN_BUILD_PROF: blocks mapped + pinned, and unpinned + unmapped
   HostCache() { cap = (size_t)std::max(0, env_int("IGN_HOST_CACHE_GB", 4)) << 30; }
   void unmap(void* p, size_t cls) {
     auto it = pinned.find(p);
@@ -196,6 +212,7 @@ struct HostCache {
       pinned.erase(it);
     }
     munmap(p, cls);
+    n_unmap++;
   }
 };
 
@@ -221,6 +238,7 @@ void* host_block_alloc(size_t bytes) {
       void* p = it->second.back();
       it->second.pop_back();
       c.idle_bytes -= cls;
+      c.live_bytes += cls;
       return p;
     }
   }
@@ -233,6 +251,8 @@ void* host_block_alloc(size_t bytes) {
   if (!reg) (void)hipGetLastError();
   std::lock_guard<std::mutex> g(c.mu);
   c.pinned[p] = reg;
+  c.live_bytes += cls;
+  c.n_map++;
   return p;
 }
 
@@ -243,6 +263,7 @@ void host_block_free(void* p, size_t bytes) {
   std::lock_guard<std::mutex> g(c.mu);
   c.idle[cls].push_back(p);
   c.idle_bytes += cls;
+  c.live_bytes -= cls;
   // over the cap: unmap idle blocks, largest classes first
   for (auto it = c.idle.rbegin(); c.idle_bytes > c.cap && it != c.idle.rend(); ++it)
     while (c.idle_bytes > c.cap && !it->second.empty()) {
@@ -270,6 +291,15 @@ void host_cache_trim() {
     c.idle_bytes -= kv.first * kv.second.size();
     kv.second.clear();
   }
+}
+
+void host_cache_stats(int64_t* live, int64_t* idle, int64_t* maps, int64_t* unmaps) {
+  HostCache& c = host_cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  *live = (int64_t)c.live_bytes;
+  *idle = (int64_t)c.idle_bytes;
+  *maps = c.n_map;
+  *unmaps = c.n_unmap;
 }
 
 void pool_stats(DevPool* pool, int64_t* live_bytes, int64_t* idle_bytes) {

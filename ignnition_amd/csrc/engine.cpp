@@ -22,6 +22,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -89,6 +90,114 @@ hipStream_t upload_stream() {
   hipStream_t& s = streams[dev];
   if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
   return s;
+}
+
+namespace {
+struct UploadState {   // per host thread and device
+  char* stage = nullptr;
+  size_t cap = 0, used = 0;
+  int depth = 0;             // nested UploadScopes
+  bool pending = false;
+  int n = 0;                 // IGN_BUILD_PROF counters of the current scope
+  size_t bytes = 0, staged = 0;
+  double t_copy = 0, t_wait = 0;
+  ~UploadState() {   // thread exit (a batch-builder thread): its copies were waited for by its scopes
+    if (stage) hipHostFree(stage);
+  }
+};
+UploadState& upload_state() {
+  thread_local std::vector<std::unique_ptr<UploadState>> st;   // (owners: the arena is freed once)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if ((int)st.size() <= dev) st.resize(dev + 1);
+  if (!st[dev]) st[dev] = std::make_unique<UploadState>();
+  return *st[dev];
+}
+bool env_flag(const char* name, bool dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) != 0 : dflt;
+}
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+constexpr size_t kStageMax = (size_t)4 << 20;   // larger copies come from pinned hvec blocks: direct DMA
+}  // namespace
+
+hipError_t upload_flush() {
+  UploadState& u = upload_state();
+  if (!u.pending) return hipSuccess;
+  const double t = now_ms();
+  const hipError_t e = hipStreamSynchronize(upload_stream());
+  u.t_wait += now_ms() - t;
+  u.pending = false;
+  u.used = 0;
+  return e;
+}
+
+hipError_t upload_bytes(void* dst, const void* src, size_t bytes) {
+  static const bool defer = env_flag("IGN_UPLOAD_DEFER", true);
+  UploadState& u = upload_state();
+  hipStream_t us = upload_stream();
+  u.n++;
+  u.bytes += bytes;
+  const double t = now_ms();
+  hipError_t e;
+  if (defer && u.depth > 0 && bytes <= kStageMax) {
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (u.used + need > u.cap) {
+      if ((e = upload_flush()) != hipSuccess) return e;   // the arena's copies have landed: reuse it
+      if (need > u.cap) {
+        if (u.stage) hipHostFree(u.stage);
+        u.stage = nullptr;
+        u.cap = std::max(need, (size_t)32 << 20);
+        if ((e = hipHostMalloc((void**)&u.stage, u.cap, hipHostMallocDefault)) != hipSuccess) {
+          u.stage = nullptr;
+          u.cap = 0;
+          return e;
+        }
+      }
+    }
+    char* sp = u.stage + u.used;
+    memcpy(sp, src, bytes);
+    u.used += need;
+    u.staged += bytes;
+    u.pending = true;
+    e = hipMemcpyAsync(dst, sp, bytes, hipMemcpyHostToDevice, us);
+    u.t_copy += now_ms() - t;
+    return e;
+  }
+  e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, us);
+  if (e == hipSuccess) {
+    u.pending = true;
+    e = upload_flush();   // the source may die after the call (and the arena's copies land with it)
+  }
+  u.t_copy += now_ms() - t;
+  return e;
+}
+
+UploadScope::UploadScope(const char* w) : what(w), t0(now_ms()) {
+  UploadState& u = upload_state();
+  if (u.depth++ == 0) {
+    u.n = 0;
+    u.bytes = u.staged = 0;
+    u.t_copy = u.t_wait = 0;
+  }
+}
+
+UploadScope::~UploadScope() {
+  UploadState& u = upload_state();
+  // every path out of a builder (errors included) leaves no copy in flight from the arena
+  u.pending = true;
+  upload_flush();
+  if (--u.depth == 0 && env_flag("IGN_BUILD_PROF", false)) {
+    int64_t live, idle, maps, unmaps;
+    host_cache_stats(&live, &idle, &maps, &unmaps);
+    fprintf(stderr,
+            "[ign-build] %s: %.2f ms, %d copies, %.1f MB (%.1f MB staged), enqueue %.2f ms, wait %.2f ms; "
+            "host blocks live %.0f MB idle %.0f MB, mapped %lld unmapped %lld\n",
+            what, now_ms() - t0, u.n, u.bytes / 1e6, u.staged / 1e6, u.t_copy, u.t_wait, live / 1e6, idle / 1e6,
+            (long long)maps, (long long)unmaps);
+  }
 }
 
 int dev_alloc(ign_batch* b, float** out, int64_t n) {
@@ -754,8 +863,8 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     }
     const int32_t pad = (int32_t)(lcode.size() - c0);
     lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)U);
-    for (int64_t k = n; k < np; ++k) {   // padding: row -1, length 0, hole codes
-      hsb.push_back(0);
+    for (int64_t k = n; k < np; ++k) {   // padding: row -1, length 0, hole codes, hs_save's pad row
+      hsb.push_back((int32_t)(ma.n_steps + ND));
       hdr.push_back(-1);
       hdr.push_back(0);
       hdr.push_back(pad);
@@ -850,6 +959,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   if (G <= 0) return fail(IGN_ERR_INVALID, "num_graphs must be > 0");
   int rc = ensure_device(p);
   if (rc) return rc;
+  UploadScope scope("ign_batch_create");
   std::unique_ptr<ign_batch, void (*)(ign_batch*)> b(new ign_batch(), ign_batch_destroy);
   b->plan = p;
   b->pool = p->pool;
@@ -1368,13 +1478,21 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     }
   }
   if ((rc = dev_alloc(b.get(), &b->d_pred, P * b->out_units))) return rc;
+  // the resident tables here, on the building thread, not at the first forward: a training loop's
+  // builders run ahead of the step, and the step's thread would otherwise build them inside the step
+  // (fresh 512 x synth50 batches: 28 -> 56 ms per step once the training forward went resident)
+  static const bool eager = env_flag("IGN_RESIDENT_EAGER", true);
+  if (eager && (rc = resident_tables(p, b.get()))) return rc;
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // every clear has landed before the batch is used
+  HIP_TRY(upload_flush());                           // (and every staged copy)
   *out = b.release();
   return IGN_OK;
 }
 
 void ign_batch_destroy(ign_batch* b) {
   if (!b) return;
+  static const bool prof = env_flag("IGN_BUILD_PROF", false);
+  const double t0 = prof ? now_ms() : 0.0;
   if (b->plan) {
     hipSetDevice(b->plan->device);
     // With the block cache every released block carries an event recorded on the plan stream
@@ -1384,9 +1502,15 @@ void ign_batch_destroy(ign_batch* b) {
     if (b->plan->stream && (b->graph || !pool_enabled(b->pool.get()))) hipStreamSynchronize(b->plan->stream);
   }
   if (b->graph) hipGraphExecDestroy(b->graph);
+  const double t1 = prof ? now_ms() : 0.0;
   if (b->train) train_state_destroy(b->train);
+  const double t2 = prof ? now_ms() : 0.0;
   if (b->pool) pool_release(b->pool.get(), b->allocs, b->plan ? b->plan->stream : nullptr);
+  const double t3 = prof ? now_ms() : 0.0;
   delete b;
+  if (prof)
+    fprintf(stderr, "[ign-build] ign_batch_destroy: %.2f ms (sync %.2f, training state %.2f, blocks %.2f, host %.2f)\n",
+            now_ms() - t0, t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
 }
 
 int ign_plan_trim_cache(ign_plan* p) {

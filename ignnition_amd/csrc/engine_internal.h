@@ -393,6 +393,22 @@ int64_t space_rows(const ign_plan* p, const ign_batch* b, const RoTensor& t);
 // worker thread does not wait for, or serialise with, the GPU step running on the engine's stream
 // (the training input pipeline overlaps them, ignnition_amd/training.py BatchPrefetcher).
 hipStream_t upload_stream();
+// Host -> device copies of the batch builders.  Inside an UploadScope (ign_batch_create,
+// ign_batch_enable_training) a copy of up to 4 MiB goes through the thread's pinned staging arena
+// and is not waited for: the scope waits once, at its end, for all of them (a builder used to wait
+// for every one of ~10^2 small copies, and eight builders waiting on the runtime at once stretched
+// each stage 2-4x).  Larger copies, and every copy outside a scope, are waited for at once (their
+// source may die after the call).  IGN_UPLOAD_DEFER=0 waits for every copy.  IGN_BUILD_PROF=1
+// prints each scope's copy count, bytes and time spent enqueueing and waiting to stderr.
+hipError_t upload_bytes(void* dst, const void* src, size_t bytes);
+void host_cache_stats(int64_t* live, int64_t* idle, int64_t* maps, int64_t* unmaps);
+hipError_t upload_flush();   // wait for this thread's pending copies
+struct UploadScope {
+  explicit UploadScope(const char* what);
+  ~UploadScope();
+  const char* what;
+  double t0;
+};
 template <typename T, typename A>
 int dev_upload(ign_batch* b, T** out, const std::vector<T, A>& host) {
   size_t n = std::max<size_t>(host.size(), 1);
@@ -400,10 +416,8 @@ int dev_upload(ign_batch* b, T** out, const std::vector<T, A>& host) {
   hipError_t e = pool_alloc(b->pool.get(), &p, n * sizeof(T), false);
   if (e != hipSuccess) return fail(IGN_ERR_OOM, "device alloc (%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
   b->allocs.push_back(p);
-  hipStream_t us = upload_stream();
-  if (!host.empty()) HIP_TRY(hipMemcpyAsync(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice, us));
-  else HIP_TRY(hipMemsetAsync(p, 0, sizeof(T), us));
-  HIP_TRY(hipStreamSynchronize(us));   // the host vector may die after the call
+  if (!host.empty()) HIP_TRY(upload_bytes(p, host.data(), host.size() * sizeof(T)));
+  else HIP_TRY(hipMemsetAsync(p, 0, sizeof(T), upload_stream()));
   *out = static_cast<T*>(p);
   return IGN_OK;
 }

@@ -55,6 +55,23 @@ constexpr int ST = kResidentTableStride;   // LDS row stride of a 96-wide projec
 
 __device__ __forceinline__ f4 lds4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void lds4w(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+// a pointer read from a pointer array (the training form's versions and saves) is generic: its loads
+// and stores would be flat_*, which count in both vmcnt and lgkmcnt and complete out of order, so
+// the compiler waits for both counters to drain (every LDS read waits for the step's hs stores).  A
+// round trip through the global address space lets the compiler issue them as global_*
+__device__ __forceinline__ float* in_global(float* p) {
+  return (float*)(__attribute__((address_space(1))) float*)p;
+}
+__device__ __forceinline__ void gst4(float* p, f4 v) { *(__attribute__((address_space(1))) f4*)p = v; }
+// the path states: global memory (PG) or LDS
+template <bool G> __device__ __forceinline__ f4 ldp4(const float* p) {
+  if constexpr (G) return *(const __attribute__((address_space(1))) f4*)p;
+  else return lds4(p);
+}
+template <bool G> __device__ __forceinline__ void stp4(float* p, f4 v) {
+  if constexpr (G) *(__attribute__((address_space(1))) f4*)p = v;
+  else lds4w(p, v);
+}
 
 // the three exact bf16 pieces of a lane's 8 values in the chained B layout (kernels_bf.hip)
 __device__ __forceinline__ void split_frags1(const f4* v, bf8 (&f)[3][1]) {
@@ -195,7 +212,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   const int64_t L1 = a.n_src > 1 ? a.src_off[1][gph + 1] - s10 : 0;
   const int64_t U = L0 + L1;   // union rows: entity 0's, then entity 1's
   constexpr int SPP = PG ? H : SP;   // row stride of the path states
-  float* hP = PG ? (SAVE ? a.path_ver[0] : a.path_state) + p0 * H : dyn;   // (SAVE: per iteration below)
+  float* hP = PG ? (SAVE ? in_global(a.path_ver[0]) : a.path_state) + p0 * H : dyn;   // (SAVE: per iteration below)
   float* hL = PG ? dyn : hP + P * SP;
   float* tab = hL + U * SP;
   int* smp = reinterpret_cast<int*>(tab + (U + 1) * ST);   // the sum MPs' CSR by local union row
@@ -270,9 +287,9 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #endif
   for (int it = 0; it < a.T; ++it) {
     // the path states this iteration reads (hPi) and writes (hPo): one buffer, or the versions
-    const float* hPi = SAVE ? a.path_ver[it] + p0 * H : hP;
-    float* hPo = SAVE ? a.path_ver[it + 1] + p0 * H : hP;
-    float* hsv = SAVE ? a.hs_save[it] : nullptr;
+    const float* hPi = SAVE ? in_global(a.path_ver[it]) + p0 * H : hP;
+    float* hPo = SAVE ? in_global(a.path_ver[it + 1]) + p0 * H : hP;
+    float* hsv = SAVE ? in_global(a.hs_save[it]) : nullptr;
     // ---- phase A: the ordered update (seq_gru_h16's tile loop over the graph's path tiles) ----
 #ifdef IGN_RES_STATIC
     auto claim = [&](int k) -> int { return k < 0 ? wave : k + kW; };   // A/B: wave w takes tiles w, w + 16, ...
@@ -300,7 +317,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       f4 h[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const f4 v = lds4(hPi + rl * SPP + 16 * t + 4 * g);
+        const f4 v = ldp4<PG>(hPi + rl * SPP + 16 * t + 4 * g);
         h[t] = valid ? v : f4{0, 0, 0, 0};
       }
       int hb = 0;   // SAVE: the position's first hs_save row, the state before the sequence
@@ -308,7 +325,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         hb = a.hsb[pt0 + 16 * k + j];
         if (valid) {
 #pragma unroll
-          for (int t = 0; t < NT; ++t) st4(hsv + (int64_t)hb * H + 16 * t + 4 * g, h[t]);
+          for (int t = 0; t < NT; ++t) gst4(hsv + (int64_t)hb * H + 16 * t + 4 * g, h[t]);
         }
       }
       f4 x[3][NT];
@@ -427,10 +444,12 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         if (t < Lmin) step(t, x, std::false_type{});
         else step(t, x, std::true_type{});
         if constexpr (SAVE) {   // the state after step t (seq_gru_h16<SAVE>'s save)
-          if (valid && t < Lr) {
+          // every lane stores (a conditional store block would make the compiler wait for the stores
+          // before the next step's code is used): a lane past its sequence rewrites its final row with
+          // the same bits (its state no longer changes), a padding lane writes the pad row (hsb)
+          const int hr = hb + min(t + 1, Lr);
 #pragma unroll
-            for (int i = 0; i < NT; ++i) st4(hsv + (int64_t)(hb + t + 1) * H + 16 * i + 4 * g, h[i] * iS);
-          }
+          for (int i = 0; i < NT; ++i) gst4(hsv + (int64_t)hr * H + 16 * i + 4 * g, h[i] * iS);
         }
         if (++t >= Lmax) break;
         load_x(code, x);
@@ -438,7 +457,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       }
       if (valid) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) lds4w(hPo + rl * SPP + 16 * t + 4 * g, h[t] * iS);
+        for (int t = 0; t < NT; ++t) stp4<PG>(hPo + rl * SPP + 16 * t + 4 * g, h[t] * iS);
       }
       k = kn;
     }
@@ -476,7 +495,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       for (int m = m0; m < m1; m += 32) {
         f4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = lds4(hp + cc[u] * SPP);
+        for (int u = 0; u < 4; ++u) v[u] = ldp4<PG>(hp + cc[u] * SPP);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {   // the next round's rows, clamped into the range
           const int i = m + 8 * (4 + u) + q;
@@ -513,7 +532,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
           for (int u = 0; u < 16; ++u) rr[u] = sms[m + u];
           f4 v[16];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) v[u] = lds4(hp + rr[u] * SPP);
+          for (int u = 0; u < 16; ++u) v[u] = ldp4<PG>(hp + rr[u] * SPP);
 #pragma unroll
           for (int u = 0; u < 16; ++u) x = x + v[u];
         }
@@ -524,15 +543,15 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         for (int u = 0; u < 8; ++u) rr[u] = sms[m + u];
         f4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds4(hp + rr[u] * SPP);
+        for (int u = 0; u < 8; ++u) v[u] = ldp4<PG>(hp + rr[u] * SPP);
 #pragma unroll
         for (int u = 0; u < 8; ++u) x = x + v[u];
       }
-      for (; m < m1; ++m) x = x + lds4(hp + sms[m] * SPP);
+      for (; m < m1; ++m) x = x + ldp4<PG>(hp + sms[m] * SPP);
       lds4w(xs + ll * SP + 4 * c4, x);
       if constexpr (SAVE) {   // sum_gru_g32's x_save, by the entity's global row
         const bool e1 = ll >= L0;
-        st4((e1 ? a.x_save[1][it] + (s10 + ll - L0) * H : a.x_save[0][it] + (s00 + ll) * H) + 4 * c4, x);
+        gst4((e1 ? a.x_save[1][it] + (s10 + ll - L0) * H : a.x_save[0][it] + (s00 + ll) * H) + 4 * c4, x);
       }
     }
     __syncthreads();
@@ -588,9 +607,9 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
 #pragma unroll
         for (int t = 0; t < NT; ++t) lds4w(hL + (int64_t)ll * SP + 16 * t + 4 * g, hn[t]);
         if constexpr (SAVE) {   // the entity's next version
-          float* o = e1 ? a.src_ver[1][it + 1] + (s10 + ll - L0) * H : a.src_ver[0][it + 1] + (s00 + ll) * H;
+          float* o = in_global(e1 ? a.src_ver[1][it + 1] + (s10 + ll - L0) * H : a.src_ver[0][it + 1] + (s00 + ll) * H);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) st4(o + 16 * t + 4 * g, hn[t]);
+          for (int t = 0; t < NT; ++t) gst4(o + 16 * t + 4 * g, hn[t]);
         }
       }
       if (!last) {

@@ -122,10 +122,7 @@ int tupload(TrainState* t, T** out, const std::vector<T, A>& h) {
   hipError_t e = pool_alloc(t->pool, &p, n * sizeof(T), h.empty());
   if (e != hipSuccess) return fail(IGN_ERR_OOM, "training buffers: device alloc: %s", hipGetErrorString(e));
   t->allocs.push_back(p);
-  if (!h.empty()) {
-    HIP_TRY(hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, upload_stream()));
-    HIP_TRY(hipStreamSynchronize(upload_stream()));
-  }
+  if (!h.empty()) HIP_TRY(upload_bytes(p, h.data(), h.size() * sizeof(T)));
   *out = static_cast<T*>(p);
   return IGN_OK;
 }
@@ -235,6 +232,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   if (b->train) return IGN_OK;
   int rc = ensure_device(p);
   if (rc) return rc;
+  UploadScope scope("ign_batch_enable_training");
   const int E = (int)p->ents.size();
   for (size_t c = 0; c < p->cells.size(); ++c) {
     const CellP& cp = p->cells[c];
@@ -287,7 +285,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       mt.hs_rows = mb.n_steps + mb.n_dst;
       for (int it = 0; it < p->T; ++it) {
         float* f = nullptr;
-        if ((rc = talloc(t.get(), &f, mt.hs_rows * H))) return rc;
+        // + one pad row: the resident training forward's padding lanes store there (resident.hip)
+        if ((rc = talloc(t.get(), &f, (mt.hs_rows + 1) * H))) return rc;
         mt.hs.push_back(f);
       }
       {
@@ -320,7 +319,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
             }
           }
       }, tptr, tidx);
-      ga_n = std::max(ga_n, mb.n_steps * 3 * H);
+      ga_n = std::max(ga_n, (mb.n_steps + 1) * 3 * H);   // + the pad slot row (seq_gru_bwd_kernel)
       gu_n = std::max(gu_n, mt.hs_rows * 3 * H);
       need_part(mt.hs_rows, H, 3 * H);
       if (p->bwd_fuse && seq_bwd_fused_supported(H)) part_n = std::max(part_n, seq_bwd_partial_floats(H));
@@ -407,6 +406,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       HIP_TRY(hipMemcpyAsync(es.data(), mb.d_edge_src[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost, upload_stream()));
       HIP_TRY(hipMemcpyAsync(ed.data(), mb.d_edge_dst[s], ne * sizeof(int32_t), hipMemcpyDeviceToHost, upload_stream()));
       HIP_TRY(hipStreamSynchronize(upload_stream()));
+      HIP_TRY(upload_flush());
       hvec<std::pair<int64_t, int32_t>> ks(ne), kd(ne);
       for (int64_t e = 0; e < ne; ++e) {
         ks[e] = {es[e], (int32_t)e};
@@ -491,6 +491,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   }
   if ((rc = talloc(t.get(), &t->part, part_n)) || (rc = talloc(t.get(), &t->bsum, (32 + 1) * 3 * 32))) return rc;
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // IGN_POOL_POISON fills have landed
+  HIP_TRY(upload_flush());                           // (and every staged copy)
   b->train = t.release();
   return IGN_OK;
 }

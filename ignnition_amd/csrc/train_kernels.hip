@@ -150,6 +150,9 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
     const int row = hd[0];
     const int L = hd[1];
     const int64_t sp = valid ? hd[2] : 0;
+    // where this lane's ga stores go once past its sequence (seq_gru_bwd's FUSE store rule below):
+    // its own step 0 row, or for a padding position the pad slot (its step_ptr, row n_steps)
+    const int gpast = hd[2];
     const uint32_t code_last = (uint32_t)hd[3];
     const int64_t hbase = valid ? sp + pos : 0;
     f4 dh[NT];
@@ -342,14 +345,20 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
         for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
       }
       if (step > 0) load_rows(hbase + (step - 1 < L ? step - 1 : 0), code_next);
+      // FUSE: every lane stores, so no branch skips the stores and the step's closing wait for the
+      // prefetched rows can leave them in flight (a conditional store block made the compiler merge
+      // its two paths into vmcnt(0): each step waited for its ga stores to reach memory).  A lane past
+      // its sequence stores its zeros to its own step 0 row (its real step 0, stored later by the
+      // same lane, wins); a padding lane to the pad slot, row n_steps (hdr; ga has one more row)
+      const int gi = act ? (int)i : gpast;
 #ifdef IGN_BWD_ABL_NOGA
       if (act && !FUSE) {   // timing-only ablation: no ga stores (wrong gradients)
 #else
-      if (act) {
+      if (FUSE || act) {
 #endif
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          float* pa = a.ga + i * (3 * H) + 16 * t + 4 * g;
+          float* pa = a.ga + (int64_t)gi * (3 * H) + 16 * t + 4 * g;
           st4(pa, gz[t]);
           st4(pa + H, gr[t]);
           st4(pa + 2 * H, gh[t]);

@@ -17,6 +17,8 @@
 from __future__ import annotations
 
 import math
+import os
+import time
 
 import numpy as np
 
@@ -82,6 +84,9 @@ class Trainer:
         self.device = dev
         self.dist = dist
         self.iterations = 0
+        # IGN_STEP_PROF=1: host seconds per phase of train_prepared (bench.py --fresh-batches reports them)
+        self.step_prof = (dict.fromkeys(("forward_enqueue", "loss_wait", "backward_enqueue", "close", "l2_wait",
+                                         "steps"), 0.0) if os.environ.get("IGN_STEP_PROF") == "1" else None)
         self.output_name, _, self.output_denorm = model_info.get_output_info()
 
     @property
@@ -120,11 +125,23 @@ class Trainer:
 
     def train_prepared(self, b, y) -> dict:
         """One optimizer step on a batch made by ``prepare`` (closed here)."""
+        prof = self.step_prof
+        tick = time.perf_counter if prof is not None else None
+        t0 = tick() if tick else 0.0
         try:
             b.forward_train(to_host=False)
+            if tick:
+                t1 = tick()
+                prof["forward_enqueue"] += t1 - t0
             dpred = self.torch.empty_like(y)
             loss = self.engine.mse_loss(b.predictions_ptr(), y, dpred)
+            if tick:
+                t2 = tick()
+                prof["loss_wait"] += t2 - t1
             b.backward(dpred, self.grads)
+            if tick:
+                t3 = tick()
+                prof["backward_enqueue"] += t3 - t2
             if self.dist is not None and self.dist.is_initialized() and self.dist.get_world_size() > 1:
                 if self.dist.get_backend() == "gloo":   # CPU collectives (tests, rehearsals): host-staged
                     g = self.grads.cpu()
@@ -137,8 +154,16 @@ class Trainer:
             self.engine.adam_step(self.grads, self.m, self.v, self.iterations, lr, self.beta1, self.beta2, self.epsilon)
             self.iterations += 1
         finally:
+            if tick:
+                t4 = tick()
             b.close()
+            if tick:
+                t5 = tick()
+                prof["close"] += t5 - t4
         reg = self.engine.l2_loss()
+        if tick:
+            prof["l2_wait"] += tick() - t5
+            prof["steps"] += 1
         return {"loss": loss, "regularization_loss": reg, "total_loss": loss + reg, "learning_rate": lr,
                 "step": self.iterations}
 
