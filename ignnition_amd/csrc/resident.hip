@@ -443,13 +443,12 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
       for (int t = 0;;) {
         if (t < Lmin) step(t, x, std::false_type{});
         else step(t, x, std::true_type{});
-        if constexpr (SAVE) {   // the state after step t (seq_gru_h16<SAVE>'s save)
-          // every lane stores (a conditional store block would make the compiler wait for the stores
-          // before the next step's code is used): a lane past its sequence rewrites its final row with
-          // the same bits (its state no longer changes), a padding lane writes the pad row (hsb)
-          const int hr = hb + min(t + 1, Lr);
+        if constexpr (SAVE) {   // the state after step t, but the last (seq_gru_h16<SAVE>'s save less
+                                // its final row: the next path version, which the backward never reads)
+          if (t + 1 < Lr) {
 #pragma unroll
-          for (int i = 0; i < NT; ++i) gst4(hsv + (int64_t)hr * H + 16 * i + 4 * g, h[i] * iS);
+            for (int i = 0; i < NT; ++i) gst4(hsv + (int64_t)(hb + t + 1) * H + 16 * i + 4 * g, h[i] * iS);
+          }
         }
         if (++t >= Lmax) break;
         load_x(code, x);

@@ -649,7 +649,10 @@ int ign_forward_train_end(ign_plan* p, ign_batch* b, float* pred_out) {
 static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
   *done = false;
   int sum_mp[kResidentMaxSrc] = {-1, -1}, S = 0;
-  if (!p->resident_train || !resident_sum_mps(p, sum_mp, &S)) return IGN_OK;
+  // the resident form computes the ordered update with seq_gru_h16's arithmetic and leaves each
+  // sequence's final state row unsaved: only under the backward that recomputes those gates and never
+  // reads that row (the fused split-fp16 one; the unfused one contracts every hs row)
+  if (!p->resident_train || !resident_sum_mps(p, sum_mp, &S) || train_seq_variant(p, 32) != 6) return IGN_OK;
   int rc = resident_tables(p, b);
   if (rc || !b->resident) return rc;
   TrainState* t = b->train;

@@ -94,11 +94,15 @@ def test_resident_forward_fits_its_workgroup(asm_resident):
         scratch = re.search(r"ScratchSize: (\d+)", meta)
         print(name, vgpr.group(1), scratch.group(1))
         assert vgpr and int(vgpr.group(1)) <= 128, name
-        if name.endswith("ELb1EEv12ResidentArgs"):   # SAVE: a few 4-8 B reloads per phase-B tile, none in phase A
+        if name.endswith("ELb1EEv12ResidentArgs"):   # SAVE: a few 4-8 B reloads per tile, none per step
             assert scratch and int(scratch.group(1)) <= 96, name
-            loop = body[body.index("v_mfma_f32_16x16x32_f16"):]
-            loop = loop[:loop.index("s_barrier")]
-            assert "scratch_" not in loop, name
+            # phase A's step loop: from the loop header that precedes the first split-fp16 MFMA to
+            # the last branch back to it
+            m = body.index("v_mfma_f32_16x16x32_f16")
+            h = body.rindex("Loop Header", 0, m)
+            label = re.findall(r"^(\.LBB\w+):", body[:h], re.M)[-1]
+            start, back = body.index(label + ":"), body.rindex(label, m)
+            assert back > m and "scratch_" not in body[start:back], name
         else:
             assert scratch and int(scratch.group(1)) == 0, name
     assert found == 5
