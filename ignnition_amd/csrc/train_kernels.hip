@@ -927,6 +927,59 @@ TsPlan ts_plan(int64_t n_rows, int M, int N, int ones) {
   return p;
 }
 
+// The N = 1 contraction (a 1-unit output layer's weight gradient, attention's score vectors):
+// part[chunk][m][0] = sum_r A[r][m] B[r], part[chunk][M][0] = sum_r B[r] (ones).  One wave per row
+// in turn, lane l holding columns 4l .. 4l + 3 (M <= 256): each row is one contiguous read, where
+// the MFMA kernel's lanes read 4-B column pieces of 8 rows (2.9 TB/s on the readout's 256-wide
+// activations); the block's four waves add in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void tsgemv_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                     int ldb, int64_t n_rows, int M, int ones, int64_t chunk,
+                                                     float* __restrict__ part) {
+  __shared__ f4 sp[4][64];
+  __shared__ float sb[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min<int64_t>(n_rows, r0 + chunk);
+  const bool on = 4 * lane < M;
+  f4 acc = {0, 0, 0, 0};
+  float bs = 0.f;
+  int64_t r = r0 + wave;
+  for (; r + 12 < r1; r += 16) {   // four rows of this wave in flight
+    f4 a[4];
+    float b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = on ? ld4(A + (r + 4 * u) * lda + 4 * lane) : f4{0, 0, 0, 0};
+      b[u] = B[(r + 4 * u) * ldb];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = fmaf(a[u][q], b[u], acc[q]);
+      bs += b[u];
+    }
+  }
+  for (; r < r1; r += 4) {
+    const f4 a = on ? ld4(A + r * lda + 4 * lane) : f4{0, 0, 0, 0};
+    const float b = B[r * ldb];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = fmaf(a[q], b, acc[q]);
+    bs += b;
+  }
+  sp[wave][lane] = acc;
+  if (lane == 0) sb[wave] = bs;
+  __syncthreads();
+  if (wave == 0) {
+    f4 t = sp[0][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) t = t + sp[w][lane];
+    float* P = part + (int64_t)blockIdx.x * (M + ones);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * lane + q < M) P[4 * lane + q] = t[q];
+    if (ones && lane == 0) P[M] = ((sb[0] + sb[1]) + sb[2]) + sb[3];
+  }
+}
+
 __global__ __launch_bounds__(256) void tsgemm_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                      int ldb, int64_t n_rows, int M, int N, int ones, int64_t chunk,
                                                      float* __restrict__ part) {
@@ -1350,7 +1403,11 @@ hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, i
   dim3 grid((unsigned)p.chunks, (unsigned)((p.tiles + wpb - 1) / wpb));
   // split-bf16 contraction (kernels_bf.hip) when A is present; the plan's IGN_TSGEMM_BF=0 keeps f32 MFMA
   hipError_t e;
-  if (g_tsgemm_bf && A) {
+  if (A && N == 1 && M % 4 == 0 && M <= 256 && lda % 4 == 0 && ((uintptr_t)A & 15) == 0) {   // exact f32 fma
+    hipLaunchKernelGGL(tsgemv_kernel, dim3((unsigned)p.chunks), dim3(256), 0, st, A, lda, B, ldb, n_rows, M, ones,
+                       p.chunk, part);
+    e = hipGetLastError();
+  } else if (g_tsgemm_bf && A) {
     e = launch_tsgemm_bf(A, lda, B, ldb, n_rows, M, N, ones, p.chunk, p.chunks, p.tiles, wpb, part, st);
   } else {
     hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
