@@ -31,9 +31,12 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
-        return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not force and not needs_build():
+        tool = os.path.join(HERE, "..", "tools", "isa_mix.py")
+        if os.path.exists(tool) and (not os.path.exists(ISA_MIX) or os.path.getmtime(tool) > os.path.getmtime(ISA_MIX)):
+            write_isa_mix(hipcc)   # the library is current, the instruction-mix tool is not
+        return OUT
     os.makedirs(OBJ, exist_ok=True)
 
     def compile_one(src):
