@@ -87,6 +87,15 @@ struct TrainState {
   int f_it = 0, f_mi = 0;
   bool f_open = false;
   float** res_ptrs = nullptr;   // the graph-resident training forward's version / save pointer arrays
+  // weight gradients formed once per MP instance (T of them per backward) keep their partial tiles
+  // here and are reduced once, at ign_backward_end, in instance order (IGN_DEFER_WGRAD=0: per instance)
+  struct DeferredGrad {
+    int64_t off_c, off_cb;   // gradient offsets in the parameter layout (off_cb -1: no bias column)
+    int M, N, ones;
+    float* part;
+    int64_t cap, used;   // chunk slots (plus the reduction's scratch after cap)
+  };
+  std::vector<DeferredGrad> defer;
   int b_ri = -1;
   bool b_open = false;
   hvec<int> dcur;                          // backward: current gradient buffer per entity
@@ -124,6 +133,33 @@ int tupload(TrainState* t, T** out, const std::vector<T, A>& h) {
   t->allocs.push_back(p);
   if (!h.empty()) HIP_TRY(upload_bytes(p, h.data(), h.size() * sizeof(T)));
   *out = static_cast<T*>(p);
+  return IGN_OK;
+}
+
+// C (+ Cb) += A^T B over n_rows rows, its partial tiles parked for ign_backward_end's reduction
+// when C has a deferred slot with room (else reduced now, as launch_tsgemm_add)
+int tsgemm_deferred(TrainState* t, const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
+                    float* C, float* Cb, hipStream_t st) {
+  const int ones = Cb != nullptr;
+  const int64_t ch = tsgemm_chunks(n_rows, M, N, ones);
+  for (auto& d : t->defer)
+    if (t->grads + d.off_c == C && (d.off_cb < 0 ? Cb == nullptr : Cb == t->grads + d.off_cb) && d.M == M &&
+        d.N == N && d.used + ch <= d.cap) {
+      HIP_TRY(launch_tsgemm_partials(A, lda, B, ldb, n_rows, M, N, ones, d.part + d.used * (int64_t)(M + ones) * N, st));
+      d.used += ch;
+      return IGN_OK;
+    }
+  HIP_TRY(launch_tsgemm_add(A, lda, B, ldb, n_rows, M, N, t->part, C, Cb, st));
+  return IGN_OK;
+}
+
+int tsgemm_deferred_flush(TrainState* t, hipStream_t st) {
+  for (auto& d : t->defer)
+    if (d.used) {
+      HIP_TRY(launch_partials_reduce_add(d.part, d.used, d.M, d.N, d.ones, t->grads + d.off_c,
+                                         d.off_cb < 0 ? nullptr : t->grads + d.off_cb, st));
+      d.used = 0;
+    }
   return IGN_OK;
 }
 
@@ -490,6 +526,39 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       return rc;
   }
   if ((rc = talloc(t.get(), &t->part, part_n)) || (rc = talloc(t.get(), &t->bsum, (32 + 1) * 3 * 32))) return rc;
+  if (const char* v = getenv("IGN_DEFER_WGRAD"); !v || atoi(v) != 0) {
+    // the per-instance weight gradients of the plain sum and ordered MPs (ign_backward_mp): one slot
+    // per (gradient tensor, shape), room for every instance of a backward
+    struct Want { int64_t c, cb; int M, N, ones; int64_t chunks; };
+    std::vector<Want> want;
+    auto add = [&](int64_t c, int64_t cb, int M, int N, int64_t rows) {
+      const int ones = cb >= 0;
+      const int64_t ch = tsgemm_chunks(rows, M, N, ones) * p->T;
+      for (auto& w : want)
+        if (w.c == c && w.cb == cb && w.M == M && w.N == N) { w.chunks += ch; return; }
+      want.push_back({c, cb, M, N, ones, ch});
+    };
+    for (size_t mi = 0; mi < p->mps.size(); ++mi) {
+      const MPP& mp = p->mps[mi];
+      const MPB& mb = b->mp[mi];
+      const CellP& cp = p->cells[mp.cell];
+      bool nets = false;
+      for (auto& nn : mp.nn) nets = nets || !nn.layers.empty();
+      if (nets || mp.feature_concat) continue;
+      const int H = cp.H, H3 = 3 * cp.H, DIN = mp.din;
+      if (mp.sorted) {
+        for (size_t s2 = 0; s2 < mp.src.size(); ++s2) add(cp.off_k, -1, DIN, H3, t->mp[mi].trows[s2]);
+      } else if (mp.aggr == IGN_AGGR_SUM) {
+        add(cp.off_k, cp.off_b, DIN, H3, mb.n_dst);
+        add(cp.off_rk, cp.off_b + H3, H, H3, mb.n_dst);
+      }
+    }
+    for (auto& w : want) {
+      TrainState::DeferredGrad d{w.c, w.cb, w.M, w.N, w.ones, nullptr, w.chunks, 0};
+      if ((rc = talloc(t.get(), &d.part, (w.chunks + kTsReduceSegs) * (int64_t)(w.M + w.ones) * w.N))) return rc;
+      t->defer.push_back(d);
+    }
+  }
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // IGN_POOL_POISON fills have landed
   HIP_TRY(upload_flush());                           // (and every staged copy)
   b->train = t.release();
@@ -936,7 +1005,7 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
           HIP_TRY(launch_row_gemm_t_generic(t->dtab, mt.trows[s], H3, p->d_params + cp.off_k + koff, sdin, target,
                                             net ? 0 : 1, -1, nullptr, st));
         } else {
-          HIP_TRY(launch_tsgemm_add(srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, t->part, gk, nullptr, st));
+          if ((rc = tsgemm_deferred(t, srcs[s], DIN, t->dtab, H3, mt.trows[s], DIN, H3, gk, nullptr, st))) return rc;
           HIP_TRY(launch_row_gemm_t(t->dtab, mt.trows[s], H3, p->d_packed + cp.pk_wt, DIN, target, net ? 0 : 1, -1,
                                     nullptr, st));
         }
@@ -947,8 +1016,9 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
       SumBwdArgs a{mt.xs[rec.it], hin, p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b,
                    p->d_packed + cp.pk_wt, p->d_packed + cp.pk_ut, dh_in, dh_out, t->dx, t->ga, t->gu, mb.n_dst};
       HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
-      HIP_TRY(launch_tsgemm_add(mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, t->part, gk, gb, st));
-      HIP_TRY(launch_tsgemm_add(hin, H, t->gu, H3, mb.n_dst, H, H3, t->part, grk, gb + H3, st));
+      if ((rc = tsgemm_deferred(t, mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, gk, gb, st)) ||
+          (rc = tsgemm_deferred(t, hin, H, t->gu, H3, mb.n_dst, H, H3, grk, gb + H3, st)))
+        return rc;
       if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343 (see train_kernels.hip)
         if ((rc = attention_weights(p, b, mp, mb, srcs, hin, st))) return rc;   // this instance's weights
         const int F = DIN;
@@ -1010,6 +1080,7 @@ int ign_backward_end(ign_plan* p, ign_batch* b) {
   t->b_open = false;
   hipStream_t st = p->stream;
   float* grads = t->grads;
+  if ((rc = tsgemm_deferred_flush(t, st))) return rc;
   for (auto& mp : p->mps)   // message-network l2 terms (AUX:833-834), once per step
     for (auto& nn : mp.nn)
       for (size_t l = 0; l < nn.layers.size(); ++l) {

@@ -105,6 +105,12 @@ void set_tsgemm_bf(bool on);
 // C[m][n] (row m = M: Cb[n]) += sum of nchunks partial tiles part[c][M + ones][N], in chunk order
 hipError_t launch_partials_reduce_add(float* part, int64_t nchunks, int M, int N, int ones, float* C, float* Cb,
                                       hipStream_t st);
+// the reduction of partial tiles uses this many chunk slots after the partials as scratch
+constexpr int kTsReduceSegs = 64;
+// the contraction's partial tiles only (tsgemm_chunks of them at part), for a reduction later
+int64_t tsgemm_chunks(int64_t n_rows, int M, int N, int ones);
+hipError_t launch_tsgemm_partials(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
+                                  int ones, float* part, hipStream_t st);
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
                              float* part, float* C, float* Cb, hipStream_t st);
 // forward Dense layer for the training readout: y = act(x W + b), MFMA when packed fragments exist

@@ -909,7 +909,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __rest
 // holds ~8k waves; two reduction passes (segments, then final) sum the partials in a fixed order.
 constexpr int kTsWaves = 8192;
 constexpr int kBwdMaxWaves = 4096;   // fused ordered backward: partial slots
-constexpr int kTsSegs = 64;
+constexpr int kTsSegs = kTsReduceSegs;
 
 struct TsPlan {
   int Mx, tiles;
@@ -1393,10 +1393,20 @@ int64_t tsgemm_partial_floats(int64_t n_rows, int M, int N) {
   return (p.chunks + kTsSegs) * (int64_t)p.Mx * N;
 }
 
+int64_t tsgemm_chunks(int64_t n_rows, int M, int N, int ones) { return n_rows ? ts_plan(n_rows, M, N, ones).chunks : 0; }
+
 hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
                              float* part, float* C, float* Cb, hipStream_t st) {
   if (n_rows == 0) return hipSuccess;
   const int ones = Cb != nullptr;
+  const hipError_t e = launch_tsgemm_partials(A, lda, B, ldb, n_rows, M, N, ones, part, st);
+  if (e != hipSuccess) return e;
+  return launch_partials_reduce_add(part, tsgemm_chunks(n_rows, M, N, ones), M, N, ones, C, Cb, st);
+}
+
+hipError_t launch_tsgemm_partials(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,
+                                  int ones, float* part, hipStream_t st) {
+  if (n_rows == 0) return hipSuccess;
   const TsPlan p = ts_plan(n_rows, M, N, ones);
   // one wave per 64x64 tile: a 1- or 2-tile contraction gets 1- or 2-wave blocks, no idle waves
   const int wpb = std::min(4, p.tiles);
@@ -1413,8 +1423,7 @@ hipError_t launch_tsgemm_add(const float* A, int lda, const float* B, int ldb, i
     hipLaunchKernelGGL(tsgemm_kernel, grid, dim3(64 * wpb), 0, st, A, lda, B, ldb, n_rows, M, N, ones, p.chunk, part);
     e = hipGetLastError();
   }
-  if (e != hipSuccess) return e;
-  return launch_partials_reduce_add(part, p.chunks, M, N, ones, C, Cb, st);
+  return e;
 }
 
 // C[m][n] (+ Cb[n] for the ones row m = M) += sum over chunks c of part[c][m][n], in chunk order

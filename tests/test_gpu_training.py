@@ -182,6 +182,23 @@ def test_resident_training_forward_is_the_batched_one(monkeypatch, kind, topo, n
         assert e <= (2 * GTOL if (kind, topo) == ("qsize", "synth50") else GTOL), e
 
 
+def test_deferred_weight_gradient_reduction(monkeypatch):
+    """The sum and ordered MPs' per-instance weight gradients keep their partial tiles and are reduced
+    once per backward (IGN_DEFER_WGRAD=1, default) instead of once per MP instance (=0): the same
+    gradients up to fp32 reassociation, bitwise deterministic, and within the autograd tolerance."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs("qsize", "nsfnet", 3)
+    prm = MPPlan.from_model_info(mi).init_params(12, bias_scale=0.1)
+    got = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("IGN_DEFER_WGRAD", v)
+        eng, _, _, _, _, g = _engine_grads(desc, dims, graphs, labels, prm)
+        got[v] = g.cpu().numpy()
+        if v == "1":
+            np.testing.assert_array_equal(got[v], _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy())
+    assert np.linalg.norm(got["1"].astype(np.float64) - got["0"]) <= 1e-6 * np.linalg.norm(got["0"])
+    assert _rel_err_vs_oracle(desc, dims, graphs, labels, prm, got["1"], eng.layout) <= GTOL
+
+
 def test_training_reduces_loss():
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 4)
     prm = MPPlan.from_model_info(mi).init_params(0)
