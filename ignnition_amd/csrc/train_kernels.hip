@@ -920,7 +920,14 @@ TsPlan ts_plan(int64_t n_rows, int M, int N, int ones) {
   TsPlan p;
   p.Mx = M + ones;
   p.tiles = ((p.Mx + 63) / 64) * ((N + 63) / 64);
-  const int64_t max_chunks = std::max<int64_t>(1, (n_rows + 255) / 256);
+  // at least 128 rows per chunk (IGN_TS_MIN_ROWS): the MP weight gradients (32-33 x 96 over ~10^5
+  // rows) had one wave per SIMD at 256 (416 chunks x 2 tiles); at 128 the step is 0.18 ms shorter, at
+  // 64 the larger reduction eats the gain (r05_c40.sh)
+  static const int64_t min_rows = [] {
+    const char* v = getenv("IGN_TS_MIN_ROWS");
+    return v && atoi(v) >= 32 ? (int64_t)atoi(v) : (int64_t)128;
+  }();
+  const int64_t max_chunks = std::max<int64_t>(1, (n_rows + min_rows - 1) / min_rows);
   p.chunks = std::max<int64_t>(1, std::min<int64_t>((kTsWaves + p.tiles - 1) / p.tiles, max_chunks));
   p.chunk = ((n_rows + p.chunks - 1) / p.chunks + 15) / 16 * 16;
   p.chunks = std::max<int64_t>(1, (n_rows + p.chunk - 1) / p.chunk);
