@@ -190,7 +190,7 @@ struct ResidentArgs {
   const int64_t* urow_off;    // [G + 1] graph g's union rows start here (lmsg_ptr, lorder)
   const int32_t* ptile_off;   // [G + 1] first header of graph g (multiples of 16)
   const int32_t* hdr;         // [headers][4] per graph, its paths by length descending, padded to whole
-                              // tiles: {local path row, final_len (0: padding), local step offset,
+                              // tiles: {local path row (-1: padding), final_len, local step offset,
                               // first step's local code}
   const int32_t* lcode_off;   // [G + 1] graph g's ordered-MP step codes start here in lcode
   const uint16_t* lcode;      //   local union rows (U_g = the hole), then max_len + 8 hole codes

@@ -197,7 +197,11 @@ __device__ __forceinline__ f4 gru_half(const void* Wbf, const void* Ubf, const f
 // not fit (synth50: 2 450 paths).  CL: the sum MPs' CSR (message rows) in LDS; else read from L2
 // (Q-size synth50: its two sum MPs' 14 k messages do not fit beside the 250 union rows' table)
 template <bool PG, bool CL, bool SAVE>
+#ifdef IGN_RES_MIN_WAVES   // A/B: at least this many waves per SIMD (VGPR budget 512 / that)
+__global__ __launch_bounds__(64 * kW, IGN_RES_MIN_WAVES) void resident_forward_kernel(ResidentArgs a) {
+#else
 __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs a) {
+#endif
   static_assert(PG || !SAVE, "the training form keeps the path states in global memory (versions)");
   constexpr int H = 32, NT = 2, KS = 1, NF = 6 * NT * KS;   // U's fp16 pieces: 2 pieces x 3 gates x NT
   __shared__ h8 su[NF * 64];
