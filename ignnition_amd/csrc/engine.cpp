@@ -135,7 +135,7 @@ hipError_t upload_flush() {
 }
 
 hipError_t upload_bytes(void* dst, const void* src, size_t bytes) {
-  static const bool defer = env_flag("IGN_UPLOAD_DEFER", true);
+  const bool defer = env_flag("IGN_UPLOAD_DEFER", true);   // (read per call: tests switch it)
   UploadState& u = upload_state();
   hipStream_t us = upload_stream();
   u.n++;
@@ -1481,8 +1481,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   // the resident tables here, on the building thread, not at the first forward: a training loop's
   // builders run ahead of the step, and the step's thread would otherwise build them inside the step
   // (fresh 512 x synth50 batches: 28 -> 56 ms per step once the training forward went resident)
-  static const bool eager = env_flag("IGN_RESIDENT_EAGER", true);
-  if (eager && (rc = resident_tables(p, b.get()))) return rc;
+  if (env_flag("IGN_RESIDENT_EAGER", true) && (rc = resident_tables(p, b.get()))) return rc;
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // every clear has landed before the batch is used
   HIP_TRY(upload_flush());                           // (and every staged copy)
   *out = b.release();

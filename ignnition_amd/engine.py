@@ -701,8 +701,9 @@ class Batch:
         check(lib.ign_backward(self.engine.handle, self.handle, _ptr(dpred), _ptr(grads)))
 
     def resident_info(self) -> dict:
-        """The graph-resident forward of this batch (decided at its first forward): whether it
-        runs, its form and LDS, and the per-launch cost model (ign_batch_resident_info)."""
+        """The graph-resident forward of this batch (decided when the batch is built; at its first
+        forward under IGN_RESIDENT_EAGER=0): whether it runs, its form and LDS, and the per-launch
+        cost model (ign_batch_resident_info)."""
         r = _lib.ResidentInfo()
         if not hasattr(lib, "ign_batch_resident_info"):   # an A/B build of an older tree (IGN_AB_LIB=1)
             return {"active": 0}

@@ -257,8 +257,10 @@ int  ign_batch_create(ign_plan* plan, const ign_batch_desc* desc, ign_batch** ou
 void ign_batch_destroy(ign_batch* batch);
 int  ign_batch_info(const ign_batch* batch, ign_batch_info_t* out);
 
-/* The graph-resident forward of a batch (ABI 11): decided at the batch's first
- * ign_forward (before it, active = 0), with the per-launch cost model of its one launch. */
+/* The graph-resident forward of a batch (ABI 11): decided by ign_batch_create (with
+ * IGN_RESIDENT_EAGER=0 at the batch's first ign_forward or ign_forward_train, active = 0 before it),
+ * with the per-launch cost model of its one launch.  The training forward (ign_forward_train) runs
+ * the same form, saving what the backward reads (IGN_RESIDENT_TRAIN=0: per-MP launches). */
 typedef struct {
   int32_t active;                  /* 1: ign_forward runs the whole MP loop as one launch */
   int32_t form;                    /* 0: every state in LDS; 1: path states in HBM / L2; 2: ... and the

@@ -659,6 +659,31 @@ def test_resident_forward_batch_invariance(monkeypatch, pg):
     np.testing.assert_array_equal(mixed[:res.size], res)
 
 
+@pytest.mark.parametrize("eager,defer", [("0", "1"), ("1", "0"), ("0", "0")])
+def test_batch_build_switches_give_the_same_bits(monkeypatch, eager, defer):
+    """The batch builder's round-5 defaults -- resident tables built in ign_batch_create
+    (IGN_RESIDENT_EAGER=1) and host copies staged and waited for once per builder call
+    (IGN_UPLOAD_DEFER=1) -- against building the tables at the first forward and waiting for every
+    copy: predictions and the resident cost model identical, for RouteNet and Q-size batches."""
+    for kind in ("routenet", "qsize"):
+        desc, dims, mi, graphs, _ = workloads.make_batch_inputs(kind, "nsfnet", 3)
+        plan = MPPlan.from_model_info(mi)
+        prm = plan.init_params(4, bias_scale=0.1)
+        outs, infos = [], []
+        for e, d in (("1", "1"), (eager, defer)):
+            monkeypatch.setenv("IGN_RESIDENT_EAGER", e)
+            monkeypatch.setenv("IGN_UPLOAD_DEFER", d)
+            eng = Engine(plan, 0)
+            eng.set_params(prm)
+            b = Batch(eng, graphs)
+            outs.append(b.forward().reshape(-1))
+            infos.append(b.resident_info())
+            b.close()
+            eng.close()
+        np.testing.assert_array_equal(outs[0], outs[1])
+        assert infos[0] == infos[1] and infos[0]["active"] == 1, infos
+
+
 def test_timing_kinds_mask(monkeypatch):
     monkeypatch.setenv("IGN_RESIDENT", "0")   # the batched launches (the resident forward is one kind)
     desc, dims, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2)
