@@ -324,14 +324,10 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         const f4 v = ldp4<PG>(hPi + rl * SPP + 16 * t + 4 * g);
         h[t] = valid ? v : f4{0, 0, 0, 0};
       }
-      int hb = 0;   // SAVE: the position's first hs_save row, the state before the sequence
-      if constexpr (SAVE) {
-        hb = a.hsb[pt0 + 16 * k + j];
-        if (valid) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) gst4(hsv + (int64_t)hb * H + 16 * t + 4 * g, h[t]);
-        }
-      }
+      // SAVE: the position's first hs_save row, the state before the sequence -- not saved: it is the
+      // path version this iteration read, and the backward reads it there (as the final row, below)
+      int hb = 0;
+      if constexpr (SAVE) hb = a.hsb[pt0 + 16 * k + j];
       f4 x[3][NT];
       auto load_x = [&](uint32_t code, f4 (&xx)[3][NT]) __attribute__((always_inline)) {
         const float* p = tab + (int64_t)code * ST + 4 * g;

@@ -719,8 +719,9 @@ static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
   *done = false;
   int sum_mp[kResidentMaxSrc] = {-1, -1}, S = 0;
   // the resident form computes the ordered update with seq_gru_h16's arithmetic and leaves each
-  // sequence's final state row unsaved: only under the backward that recomputes those gates and never
-  // reads that row (the fused split-fp16 one; the unfused one contracts every hs row)
+  // sequence's first and final state rows unsaved (the path versions hold them): only under the
+  // backward that recomputes those gates and reads neither row (the fused split-fp16 one; the unfused
+  // one contracts every hs row)
   if (!p->resident_train || !resident_sum_mps(p, sum_mp, &S) || train_seq_variant(p, 32) != 6) return IGN_OK;
   int rc = resident_tables(p, b);
   if (rc || !b->resident) return rc;
@@ -971,6 +972,7 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
       SeqBwdArgs a{mt.hs[rec.it], mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
                    t->ga, t->gu, mb.n_dst};
+      a.h_in = t->ver[dst][rec.v_in];
       a.hdr = mt.hdrb;
       if (p->bwd_fuse && seq_bwd_fused_supported(H)) {
         // dU and both bias gradients (column sums of da and du) inside the kernel

@@ -21,6 +21,7 @@ struct SeqBwdArgs {
   float* gu;                 // [n_steps + n_dst][3H] dLoss/d(h.U + b_rec), rows aligned with hs
                              // (the kernel zeroes each sequence's final-state row); unused when fused
   int64_t n_dst;
+  const float* h_in = nullptr;   // [rows][H] the state before the MP (h_prev of every sequence's step 0)
   // fused form (part != nullptr, H 16 / 32): dU += sum h_prev^T du, db_rec += sum du and
   // db_in += sum da are formed in the kernel (per-wave partials in part, reduced in a fixed order);
   // gu is not written

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
     f4 h0[NT];   // H16: the tile's first states, for the forward's tile scale
     if constexpr (H16) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) h0[t] = ld4(a.hs + hbase * H + 16 * t + 4 * g);
+      for (int t = 0; t < NT; ++t) h0[t] = ld4(a.h_in + (int64_t)row * H + 16 * t + 4 * g);
     }
     // positions are sorted by length, descending: lane 0 (position tile * 16) is the longest
     const int Lmax = __builtin_amdgcn_readfirstlane(L);
@@ -171,9 +171,12 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
     // first loaded step, Lmax - 1: its own last step; masked either way).  Step codes are loaded
     // two steps ahead, so a step's row loads never wait for its code.
     f4 hp[NT], x[3][NT];
+    // a step's h_prev; step 0's is the state before the MP, read from that state version (h_in): the
+    // resident training forward does not save it as hs row hbase (the batched one does; same bits)
     auto load_rows = [&](int64_t hr, uint32_t code) __attribute__((always_inline)) {
+      const float* hsrc = hr == hbase ? a.h_in + (int64_t)row * H : a.hs + hr * H;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) hp[t] = ld4(a.hs + hr * H + 16 * t + 4 * g);
+      for (int t = 0; t < NT; ++t) hp[t] = ld4(hsrc + 16 * t + 4 * g);
 #pragma unroll
       for (int G = 0; G < 3; ++G)
 #pragma unroll
@@ -1249,6 +1252,7 @@ hipError_t launch_seq_bwd_hdr(const int32_t* fwd_hdr, const uint32_t* step_code,
 
 hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
   if (a.n_dst == 0) return hipSuccess;
+  if (!a.h_in) return hipErrorInvalidValue;
   if (a.part) {   // fused dU / b_rec(h) gradients
     if (!a.dU || !a.db_rec || !a.db_in || !a.scratch) return hipErrorInvalidValue;
     if (h == 16) return seq_bwd_fused<16, 0>(a, st);
