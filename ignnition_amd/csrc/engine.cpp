@@ -863,7 +863,7 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     }
     const int32_t pad = (int32_t)(lcode.size() - c0);
     lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)U);
-    for (int64_t k = n; k < np; ++k) {   // padding: row -1, length 0, hole codes, hs_save's pad row
+    for (int64_t k = n; k < np; ++k) {   // padding: row -1, length 0, hole codes, hs_save's pad row (unwritten)
       hsb.push_back((int32_t)(ma.n_steps + ND));
       hdr.push_back(-1);
       hdr.push_back(0);

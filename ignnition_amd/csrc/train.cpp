@@ -321,7 +321,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       mt.hs_rows = mb.n_steps + mb.n_dst;
       for (int it = 0; it < p->T; ++it) {
         float* f = nullptr;
-        // + one pad row: the resident training forward's padding lanes store there (resident.hip)
+        // + one pad row: the resident training forward's tile headers point padding positions there
+        // (resident.hip, hsb; its stores skip them, so the row stays unwritten)
         if ((rc = talloc(t.get(), &f, (mt.hs_rows + 1) * H))) return rc;
         mt.hs.push_back(f);
       }
@@ -792,6 +793,7 @@ int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* gra
   HIP_TRY(hipMemsetAsync(grads, 0, p->n_params * sizeof(float), st));
   t->grads = grads;
   t->l2_scale = l2_scale;
+  for (auto& d : t->defer) d.used = 0;   // (a backward that failed part-way leaves no stale partials)
   t->dcur.assign(E, 0);
   for (int e = 0; e < E; ++e)   // owned and halo rows (edge-cut: peers' gradients arrive in the owned rows)
     HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, (b->rows[e] + b->halo[e]) * p->ents[e].hidden_dim * sizeof(float), st));
