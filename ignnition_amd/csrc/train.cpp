@@ -96,6 +96,12 @@ struct TrainState {
     int64_t cap, used;   // chunk slots (plus the reduction's scratch after cap)
   };
   std::vector<DeferredGrad> defer;
+  struct DeferredSeq {   // the fused ordered backward's per-wave dU / bias partials, per cell
+    int cell, H;
+    float* part;
+    int64_t cap, used;   // partial slots (plus the reduction's scratch after cap)
+  };
+  std::vector<DeferredSeq> defer_seq;
   int b_ri = -1;
   bool b_open = false;
   hvec<int> dcur;                          // backward: current gradient buffer per entity
@@ -153,7 +159,19 @@ int tsgemm_deferred(TrainState* t, const float* A, int lda, const float* B, int 
   return IGN_OK;
 }
 
-int tsgemm_deferred_flush(TrainState* t, hipStream_t st) {
+int tsgemm_deferred_flush(const ign_plan* p, TrainState* t, hipStream_t st) {
+  for (auto& d : t->defer_seq)
+    if (d.used) {
+      const CellP& cp = p->cells[d.cell];
+      SeqBwdArgs a{};
+      a.part = d.part;
+      a.scratch = t->bsum;
+      a.dU = t->grads + cp.off_rk;
+      a.db_rec = t->grads + cp.off_b + 3 * cp.H;
+      a.db_in = t->grads + cp.off_b;
+      HIP_TRY(launch_seq_bwd_reduce(a, d.used, d.H, st));
+      d.used = 0;
+    }
   for (auto& d : t->defer)
     if (d.used) {
       HIP_TRY(launch_partials_reduce_add(d.part, d.used, d.M, d.N, d.ones, t->grads + d.off_c,
@@ -554,6 +572,19 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         add(cp.off_rk, cp.off_b + H3, H, H3, mb.n_dst);
       }
     }
+    for (size_t mi = 0; mi < p->mps.size(); ++mi) {   // the fused ordered backward's partials
+      const MPP& mp = p->mps[mi];
+      const CellP& cp = p->cells[mp.cell];
+      if (!mp.sorted || !p->bwd_fuse || !seq_bwd_fused_supported(cp.H)) continue;
+      const int64_t tiles = (b->mp[mi].n_dst + 15) / 16;
+      const int64_t waves = std::min<int64_t>((tiles + 3) / 4 * 4, kBwdPartialWaves) * p->T;   // upper bound
+      bool found = false;
+      for (auto& d : t->defer_seq)
+        if (d.cell == mp.cell) { d.cap += waves; found = true; }
+      if (!found) t->defer_seq.push_back({mp.cell, cp.H, nullptr, waves, 0});
+    }
+    for (auto& d : t->defer_seq)
+      if ((rc = talloc(t.get(), &d.part, (d.cap + kTsReduceSegs) * (int64_t)(d.H + 2) * 3 * d.H))) return rc;
     for (auto& w : want) {
       TrainState::DeferredGrad d{w.c, w.cb, w.M, w.N, w.ones, nullptr, w.chunks, 0};
       if ((rc = talloc(t.get(), &d.part, (w.chunks + kTsReduceSegs) * (int64_t)(w.M + w.ones) * w.N))) return rc;
@@ -794,6 +825,7 @@ int ign_backward_begin(ign_plan* p, ign_batch* b, const float* dpred, float* gra
   t->grads = grads;
   t->l2_scale = l2_scale;
   for (auto& d : t->defer) d.used = 0;   // (a backward that failed part-way leaves no stale partials)
+  for (auto& d : t->defer_seq) d.used = 0;
   t->dcur.assign(E, 0);
   for (int e = 0; e < E; ++e)   // owned and halo rows (edge-cut: peers' gradients arrive in the owned rows)
     HIP_TRY(hipMemsetAsync(t->dS[0][e], 0, (b->rows[e] + b->halo[e]) * p->ents[e].hidden_dim * sizeof(float), st));
@@ -991,6 +1023,15 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
           a.Uth = p->d_packed + cp.pk_uth;
         }
         else if (p->bwd_bf && H == 32 && cp.pk_ubf >= 0 && train_seq_variant(p, H) == 4) a.Ubf = p->d_packed + cp.pk_ubf;
+        // the partials stay for one reduction per backward (ign_backward_end) where the cell has room
+        const int64_t waves = seq_bwd_fused_waves(a, H);
+        for (auto& d : t->defer_seq)
+          if (d.cell == mp.cell && d.used + waves <= d.cap) {
+            a.part = d.part + d.used * (int64_t)(H + 2) * H3;
+            a.defer_reduce = true;
+            d.used += waves;
+            break;
+          }
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
       } else {
         HIP_TRY(launch_seq_gru_bwd(a, H, st));
@@ -1084,7 +1125,7 @@ int ign_backward_end(ign_plan* p, ign_batch* b) {
   t->b_open = false;
   hipStream_t st = p->stream;
   float* grads = t->grads;
-  if ((rc = tsgemm_deferred_flush(t, st))) return rc;
+  if ((rc = tsgemm_deferred_flush(p, t, st))) return rc;
   for (auto& mp : p->mps)   // message-network l2 terms (AUX:833-834), once per step
     for (auto& nn : mp.nn)
       for (size_t l = 0; l < nn.layers.size(); ++l) {

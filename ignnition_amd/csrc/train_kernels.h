@@ -35,6 +35,7 @@ struct SeqBwdArgs {
   const void* Uth = nullptr; // with Uh: U's scaled fp16 pieces as dh = du . U^T's A operand (pack_ut_f16)
   const int32_t* hdr = nullptr;   // per order position, padded to whole tiles: {row, len, step_ptr,
                                   // the code of the last step} (launch_seq_bwd_hdr)
+  bool defer_reduce = false;   // fused: leave the per-wave partials in part (launch_seq_bwd_reduce later)
 };
 
 // Backward of the sum update (AUX:752-765): one GRU step per destination row.
@@ -62,6 +63,10 @@ hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st);
 hipError_t launch_seq_bwd_hdr(const int32_t* fwd_hdr, const uint32_t* step_code, int64_t n_pos, int32_t* out,
                               hipStream_t st);
 bool seq_bwd_fused_supported(int h);
+// fused form: the per-wave partial slots one launch writes, and their reduction into dU / db_rec /
+// db_in (part may hold the partials of several launches, waves = their total)
+int64_t seq_bwd_fused_waves(const SeqBwdArgs& a, int h);
+hipError_t launch_seq_bwd_reduce(const SeqBwdArgs& a, int64_t waves, int h, hipStream_t st);
 int64_t seq_bwd_partial_floats(int h);
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);
 // out[r][:cols] (+)= sum over k in [ptr[r], ptr[r+1]) of in[idx[k]][:cols]   (cols % 4 == 0)
@@ -108,6 +113,7 @@ hipError_t launch_partials_reduce_add(float* part, int64_t nchunks, int M, int N
                                       hipStream_t st);
 // the reduction of partial tiles uses this many chunk slots after the partials as scratch
 constexpr int kTsReduceSegs = 64;
+constexpr int kBwdPartialWaves = 4096;   // the fused ordered backward's partial slots per launch (at most)
 // the contraction's partial tiles only (tsgemm_chunks of them at part), for a reduction later
 int64_t tsgemm_chunks(int64_t n_rows, int M, int N, int ones);
 hipError_t launch_tsgemm_partials(const float* A, int lda, const float* B, int ldb, int64_t n_rows, int M, int N,

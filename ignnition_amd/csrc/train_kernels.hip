@@ -911,7 +911,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __rest
 // iteration (32 loads in flight), and writes its partial tile.  Chunks are sized so the grid
 // holds ~8k waves; two reduction passes (segments, then final) sum the partials in a fixed order.
 constexpr int kTsWaves = 8192;
-constexpr int kBwdMaxWaves = 4096;   // fused ordered backward: partial slots
+constexpr int kBwdMaxWaves = kBwdPartialWaves;   // fused ordered backward: partial slots
 constexpr int kTsSegs = kTsReduceSegs;
 
 struct TsPlan {
@@ -1216,7 +1216,7 @@ bool seq_bwd_fused_supported(int h) { return h == 16 || h == 32; }
 int64_t seq_bwd_partial_floats(int h) { return (int64_t)(kBwdMaxWaves + kTsSegs) * (h + 2) * 3 * h; }
 
 template <int H, int RC>
-static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
+static int64_t seq_bwd_fused_blocks(int64_t n_dst) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1228,15 +1228,32 @@ static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, seq_gru_bwd_kernel<H, true, RC>, 256, 0) != hipSuccess ||
       per_cu <= 0)
     per_cu = 1;
-  const int64_t tiles = (a.n_dst + 15) / 16;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>({(tiles + 3) / 4, (int64_t)per_cu * cus, kBwdMaxWaves / 4}));
+  const int64_t tiles = (n_dst + 15) / 16;
+  return std::max<int64_t>(1, std::min<int64_t>({(tiles + 3) / 4, (int64_t)per_cu * cus, kBwdMaxWaves / 4}));
+}
+
+template <int H, int RC>
+static hipError_t seq_bwd_fused(const SeqBwdArgs& a, hipStream_t st) {
+  const int64_t blocks = seq_bwd_fused_blocks<H, RC>(a.n_dst);
   hipLaunchKernelGGL((seq_gru_bwd_kernel<H, true, RC>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || a.defer_reduce) return e;   // (deferred: launch_seq_bwd_reduce later)
+  return launch_seq_bwd_reduce(a, blocks * 4, H, st);
+}
+
+int64_t seq_bwd_fused_waves(const SeqBwdArgs& a, int h) {
+  if (h == 16) return 4 * seq_bwd_fused_blocks<16, 0>(a.n_dst);
+  if (h == 32)
+    return 4 * (a.Uh ? seq_bwd_fused_blocks<32, 2>(a.n_dst) : a.Ubf ? seq_bwd_fused_blocks<32, 1>(a.n_dst)
+                                                                   : seq_bwd_fused_blocks<32, 0>(a.n_dst));
+  return 0;
+}
+
+hipError_t launch_seq_bwd_reduce(const SeqBwdArgs& a, int64_t waves, int H, hipStream_t st) {
   // rows 0..H (dU, da sums) into scratch, row H + 1 (du sums) straight into db_rec
-  e = hipMemsetAsync(a.scratch, 0, (size_t)(H + 1) * 3 * H * sizeof(float), st);
+  hipError_t e = hipMemsetAsync(a.scratch, 0, (size_t)(H + 1) * 3 * H * sizeof(float), st);
   if (e != hipSuccess) return e;
-  if ((e = launch_partials_reduce_add(a.part, blocks * 4, H + 1, 3 * H, 1, a.scratch, a.db_rec, st)) != hipSuccess)
+  if ((e = launch_partials_reduce_add(a.part, waves, H + 1, 3 * H, 1, a.scratch, a.db_rec, st)) != hipSuccess)
     return e;
   if ((e = launch_axpy(a.dU, a.scratch, 1.f, (int64_t)H * 3 * H, st)) != hipSuccess) return e;
   return launch_axpy(a.db_in, a.scratch + (int64_t)H * 3 * H, 1.f, 3 * H, st);
