@@ -267,6 +267,7 @@ struct ign_plan {
   bool bwd_bf = true;             // ordered backward's gate recompute on split-bf16 (IGN_BWD_BF=0: f32 MFMA)
   bool train_seq_h16 = true;      // training forward's ordered update on split-fp16 (IGN_TRAIN_SEQ_H16=0: bf16)
   bool bwd_fuse = true;           // ordered backward forms dU in the kernel (IGN_BWD_FUSE=0: tsgemm)
+  bool sum_bwd_fuse = true;       // sum backward forms dW / dU in the kernel (IGN_SUM_BWD_FUSE=0: tsgemm)
   bool resident = true;           // graph-resident forward for small RouteNet-shaped graphs (IGN_RESIDENT=0: off)
   bool resident_pg = true;        // ... with the path states in global memory where they do not fit LDS (IGN_RESIDENT_PG)
   bool resident_path_global = false;   // IGN_RESIDENT=2: that form for every eligible batch (tests)

@@ -550,9 +550,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     // per (gradient tensor, shape), room for every instance of a backward
     struct Want { int64_t c, cb; int M, N, ones; int64_t chunks; };
     std::vector<Want> want;
-    auto add = [&](int64_t c, int64_t cb, int M, int N, int64_t rows) {
+    auto add = [&](int64_t c, int64_t cb, int M, int N, int64_t rows, int64_t min_slots = 0) {
       const int ones = cb >= 0;
-      const int64_t ch = tsgemm_chunks(rows, M, N, ones) * p->T;
+      const int64_t ch = std::max(tsgemm_chunks(rows, M, N, ones), min_slots) * p->T;
       for (auto& w : want)
         if (w.c == c && w.cb == cb && w.M == M && w.N == N) { w.chunks += ch; return; }
       want.push_back({c, cb, M, N, ones, ch});
@@ -568,8 +568,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       if (mp.sorted) {
         for (size_t s2 = 0; s2 < mp.src.size(); ++s2) add(cp.off_k, -1, DIN, H3, t->mp[mi].trows[s2]);
       } else if (mp.aggr == IGN_AGGR_SUM) {
-        add(cp.off_k, cp.off_b, DIN, H3, mb.n_dst);
-        add(cp.off_rk, cp.off_b + H3, H, H3, mb.n_dst);
+        const int64_t fw = sum_bwd_fused_waves(mb.n_dst, DIN, H);   // the fused sum backward's partials
+        add(cp.off_k, cp.off_b, DIN, H3, mb.n_dst, fw);
+        add(cp.off_rk, cp.off_b + H3, H, H3, mb.n_dst, fw);
       }
     }
     for (size_t mi = 0; mi < p->mps.size(); ++mi) {   // the fused ordered backward's partials
@@ -1060,10 +1061,26 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
       const float* hin = t->ver[dst][rec.v_in];
       SumBwdArgs a{mt.xs[rec.it], hin, p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b,
                    p->d_packed + cp.pk_wt, p->d_packed + cp.pk_ut, dh_in, dh_out, t->dx, t->ga, t->gu, mb.n_dst};
-      HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
-      if ((rc = tsgemm_deferred(t, mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, gk, gb, st)) ||
-          (rc = tsgemm_deferred(t, hin, H, t->gu, H3, mb.n_dst, H, H3, grk, gb + H3, st)))
-        return rc;
+      // plain sums at DIN = H = 32: dW / dU formed in the backward kernel, its partials into the
+      // deferred slots (IGN_SUM_BWD_FUSE=0: da / du written, then the two row contractions)
+      TrainState::DeferredGrad* dw = nullptr;
+      TrainState::DeferredGrad* du = nullptr;
+      const int64_t fw = mp.aggr == IGN_AGGR_SUM && p->sum_bwd_fuse ? sum_bwd_fused_waves(mb.n_dst, DIN, H) : 0;
+      for (auto& d : t->defer) {
+        if (fw && d.off_c == cp.off_k && d.off_cb == cp.off_b && d.M == DIN && d.N == H3 && d.used + fw <= d.cap) dw = &d;
+        if (fw && d.off_c == cp.off_rk && d.off_cb == cp.off_b + H3 && d.M == H && d.N == H3 && d.used + fw <= d.cap) du = &d;
+      }
+      if (dw && du) {
+        HIP_TRY(launch_sum_gru_bwd_fused(a, DIN, H, dw->part + dw->used * (int64_t)(DIN + 1) * H3,
+                                         du->part + du->used * (int64_t)(H + 1) * H3, st));
+        dw->used += fw;
+        du->used += fw;
+      } else {
+        HIP_TRY(launch_sum_gru_bwd(a, DIN, H, st));
+        if ((rc = tsgemm_deferred(t, mt.xs[rec.it], DIN, t->ga, H3, mb.n_dst, DIN, H3, gk, gb, st)) ||
+            (rc = tsgemm_deferred(t, hin, H, t->gu, H3, mb.n_dst, H, H3, grk, gb + H3, st)))
+          return rc;
+      }
       if (mp.aggr == IGN_AGGR_ATTENTION) {   // AUX:287-343 (see train_kernels.hip)
         if ((rc = attention_weights(p, b, mp, mb, srcs, hin, st))) return rc;   // this instance's weights
         const int F = DIN;

@@ -69,6 +69,12 @@ int64_t seq_bwd_fused_waves(const SeqBwdArgs& a, int h);
 hipError_t launch_seq_bwd_reduce(const SeqBwdArgs& a, int64_t waves, int h, hipStream_t st);
 int64_t seq_bwd_partial_floats(int h);
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st);
+// the same with the weight gradients formed in the kernel (din = h = 32; ga / gu unused): per-wave
+// partials of dW (+ db_in row) at part_w and of dU (+ db_rec row) at part_u, sum_bwd_fused_waves of
+// each, in launch_partials_reduce_add's layout (M = din / h, N = 3h, ones)
+int64_t sum_bwd_fused_waves(int64_t n_dst, int din, int h);
+hipError_t launch_sum_gru_bwd_fused(const SumBwdArgs& a, int din, int h, float* part_w, float* part_u,
+                                    hipStream_t st);
 // out[r][:cols] (+)= sum over k in [ptr[r], ptr[r+1]) of in[idx[k]][:cols]   (cols % 4 == 0)
 // attention backward (AUX:287-343; see train_kernels.hip): per-message dw / dv, then per source row
 // and per destination the state gradients and the score-vector gradients ds; then the weights

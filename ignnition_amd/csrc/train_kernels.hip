@@ -1285,6 +1285,225 @@ hipError_t launch_seq_gru_bwd(const SeqBwdArgs& a, int h, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Sum update backward with its weight gradients formed in the kernel (DIN = H = 32: the RouteNet /
+// Q-size sum MPs).  Persistent waves take 16-row tiles in a static order and, besides dh and dx
+// (sum_gru_bwd_kernel's arithmetic), accumulate dW = sum x^T da and dU = sum h^T du on the f32 MFMA
+// through a per-wave transpose tile (seq_gru_bwd_kernel's FUSE scheme: rows on the k axis) and the
+// bias sums on the VALU.  Each wave writes one partial of dW plus the db_in row and one of dU plus
+// the db_rec row, in launch_partials_reduce_add's layout, so da and du never go to memory and the
+// two row contractions over them (tsgemm) are gone.  Rows past n_dst have dh = 0, so da = du = 0.
+template <int DIN, int H>
+__global__ __launch_bounds__(256, 2) void sum_gru_bwd_fused_kernel(SumBwdArgs a, float* __restrict__ part_w,
+                                                                float* __restrict__ part_u) {
+  constexpr int NC = DIN / 16, NT = H / 16, KX = DIN / 4, KH = H / 4, K3 = 3 * H / 4;
+  constexpr int UNITS = DIN + 5 * H;   // transposed: x, h, dz, dr, dc (= da_h), dc r (= du_h)
+  __shared__ float sT[4][UNITS * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  float* R = sT[wave];
+  // transpose-tile offsets (seq_gru_bwd_kernel): write (unit 16t + 4g + q, row j); read (unit 16x + j,
+  // rows 4g .. 4g + 3)
+  const int wofs = j ^ (4 * g), rofs = j * 16 + 4 * (g ^ ((j >> 2) & 3));
+  f4 dW[NC][3 * NT], dU[NT][3 * NT], bz[NT], br[NT], bc[NT], bu[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    bz[t] = br[t] = bc[t] = bu[t] = f4{0, 0, 0, 0};
+#pragma unroll
+    for (int nt = 0; nt < 3 * NT; ++nt) dU[t][nt] = f4{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int nt = 0; nt < 3 * NT; ++nt) dW[c][nt] = f4{0, 0, 0, 0};
+  const int64_t n_tiles = (a.n_dst + 15) / 16;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row = tile * 16 + j;
+    const bool valid = row < a.n_dst;
+    const int64_t rr0 = valid ? row : 0;
+    f4 x[NC], h[NT], dh[NT];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = ld4(a.x + rr0 * DIN + 16 * c + 4 * g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      h[t] = ld4(a.h + rr0 * H + 16 * t + 4 * g);
+      dh[t] = valid ? ld4(a.dh_in + rr0 * H + 16 * t + 4 * g) : f4{0, 0, 0, 0};
+    }
+    f4 az[NT], ar[NT], ax[NT], ah[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      az[t] = ld4(a.bias + 0 * H + 16 * t + 4 * g);
+      ar[t] = ld4(a.bias + 1 * H + 16 * t + 4 * g);
+      ax[t] = ld4(a.bias + 2 * H + 16 * t + 4 * g);
+      ah[t] = ld4(a.bias + 3 * H + 16 * t + 4 * g);
+    }
+    int lofs = lane;   // opaque: the fragment reads stay inside the tile loop (registers)
+    asm volatile("" : "+v"(lofs));
+#pragma unroll
+    for (int s = 0; s < KX; ++s) {
+      const float xb = x[s >> 2][s & 3];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        az[t] = MFMA(a.Wp[frag_idx(0 * NT + t, s, KX, lofs)], xb, az[t]);
+        ar[t] = MFMA(a.Wp[frag_idx(1 * NT + t, s, KX, lofs)], xb, ar[t]);
+        ax[t] = MFMA(a.Wp[frag_idx(2 * NT + t, s, KX, lofs)], xb, ax[t]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      const float hb = h[s >> 2][s & 3];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        az[t] = MFMA(a.Up[frag_idx(0 * NT + t, s, KH, lofs)], hb, az[t]);
+        ar[t] = MFMA(a.Up[frag_idx(1 * NT + t, s, KH, lofs)], hb, ar[t]);
+        ah[t] = MFMA(a.Up[frag_idx(2 * NT + t, s, KH, lofs)], hb, ah[t]);
+      }
+    }
+    f4 gz[NT], gr[NT], gh[NT], guh[NT], acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = sig2_(az[t][r]);
+        const float rr = sig2_(ar[t][r]);
+        const float c = tanh2_(ax[t][r] + rr * ah[t][r]);
+        const float uh = ah[t][r] * kInv2Log2e;
+        const float d = dh[t][r];
+        const float dzp = d * (h[t][r] - c) * z * (1.f - z);
+        const float dcp = d * (1.f - z) * (1.f - c * c);
+        const float drp = dcp * uh * rr * (1.f - rr);
+        gz[t][r] = dzp;
+        gr[t][r] = drp;
+        gh[t][r] = dcp;
+        guh[t][r] = dcp * rr;
+        acc[t][r] = d * z;
+      }
+    }
+    f4 dxa[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dxa[c] = f4{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < K3; ++s) {
+      const int gt = s >> 2, G = gt / NT, t2 = gt % NT;
+      const float ba = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : gh[t2][s & 3];
+      const float bv = G == 0 ? gz[t2][s & 3] : G == 1 ? gr[t2][s & 3] : guh[t2][s & 3];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dxa[c] = MFMA(a.Wt[frag_idx(c, s, K3, lofs)], ba, dxa[c]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = MFMA(a.Ut[frag_idx(t, s, K3, lofs)], bv, acc[t]);
+    }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) st4(a.dh_out + row * H + 16 * t + 4 * g, acc[t]);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) st4(a.dx + row * DIN + 16 * c + 4 * g, dxa[c]);
+    }
+    // the tile's x, h, da and du through the transpose tile, rows on the MFMA k axis
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) R[(16 * c + 4 * g + q) * 16 + wofs] = x[c][q];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        R[(DIN + 16 * t + 4 * g + q) * 16 + wofs] = h[t][q];
+        R[(DIN + H + 16 * t + 4 * g + q) * 16 + wofs] = gz[t][q];
+        R[(DIN + 2 * H + 16 * t + 4 * g + q) * 16 + wofs] = gr[t][q];
+        R[(DIN + 3 * H + 16 * t + 4 * g + q) * 16 + wofs] = gh[t][q];
+        R[(DIN + 4 * H + 16 * t + 4 * g + q) * 16 + wofs] = guh[t][q];
+      }
+    }
+    f4 axT[NC], ahT[NT];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) axT[c] = ld4(R + c * 256 + rofs);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ahT[t] = ld4(R + (DIN / 16 + t) * 256 + rofs);
+#pragma unroll
+    for (int nt = 0; nt < 3 * NT; ++nt) {
+      const int gate = nt / NT, t2 = nt % NT;
+      const f4 bda = ld4(R + ((DIN + H) / 16 + nt) * 256 + rofs);   // dz, dr, dc
+      const f4 bdu = gate < 2 ? bda : ld4(R + ((DIN + 4 * H) / 16 + t2) * 256 + rofs);   // dz, dr, dc r
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) dW[c][nt] = MFMA(axT[c][ks], bda[ks], dW[c][nt]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) dU[t][nt] = MFMA(ahT[t][ks], bdu[ks], dU[t][nt]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      bz[t] += gz[t];
+      br[t] += gr[t];
+      bc[t] += gh[t];
+      bu[t] += guh[t];
+    }
+  }
+  // this wave's partials: rows 0..DIN-1 / 0..H-1 = dW / dU (lane: D[16m + 4g + q][16nt + j]), then the
+  // bias row [sum dz, sum dr, sum dc] (db_in) / [sum dz, sum dr, sum dc r] (db_rec)
+  const int64_t wv = (int64_t)blockIdx.x * 4 + wave;
+  float* Pw = part_w + wv * (DIN + 1) * (3 * H);
+  float* Pu = part_u + wv * (H + 1) * (3 * H);
+#pragma unroll
+  for (int nt = 0; nt < 3 * NT; ++nt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) Pw[(16 * c + 4 * g + q) * (3 * H) + 16 * nt + j] = dW[c][nt][q];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) Pu[(16 * t + 4 * g + q) * (3 * H) + 16 * nt + j] = dU[t][nt][q];
+    }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float sz = bz[t][q], sr = br[t][q], sc = bc[t][q], su = bu[t][q];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {   // over the 16 rows j of group g
+        sz += __shfl_xor(sz, o);
+        sr += __shfl_xor(sr, o);
+        sc += __shfl_xor(sc, o);
+        su += __shfl_xor(su, o);
+      }
+      if (j == 0) {
+        const int u = 16 * t + 4 * g + q;
+        Pw[DIN * (3 * H) + u] = sz;
+        Pw[DIN * (3 * H) + H + u] = sr;
+        Pw[DIN * (3 * H) + 2 * H + u] = sc;
+        Pu[H * (3 * H) + u] = sz;
+        Pu[H * (3 * H) + H + u] = sr;
+        Pu[H * (3 * H) + 2 * H + u] = su;
+      }
+    }
+}
+
+static int64_t sum_bwd_fused_blocks(int64_t n_dst) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sum_gru_bwd_fused_kernel<32, 32>, 256, 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  const int64_t tiles = (n_dst + 15) / 16;
+  return std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, (int64_t)per_cu * cus));
+}
+
+int64_t sum_bwd_fused_waves(int64_t n_dst, int din, int h) {
+  return (din == 32 && h == 32 && n_dst > 0) ? 4 * sum_bwd_fused_blocks(n_dst) : 0;
+}
+
+hipError_t launch_sum_gru_bwd_fused(const SumBwdArgs& a, int din, int h, float* part_w, float* part_u,
+                                    hipStream_t st) {
+  if (a.n_dst == 0) return hipSuccess;
+  if (din != 32 || h != 32 || !part_w || !part_u) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((sum_gru_bwd_fused_kernel<32, 32>), dim3((unsigned)sum_bwd_fused_blocks(a.n_dst)), dim3(256), 0,
+                     st, a, part_w, part_u);
+  return hipGetLastError();
+}
+
 hipError_t launch_sum_gru_bwd(const SumBwdArgs& a, int din, int h, hipStream_t st) {
   if (a.n_dst == 0) return hipSuccess;
   dim3 grid((unsigned)((a.n_dst + 63) / 64));

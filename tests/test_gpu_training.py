@@ -199,6 +199,28 @@ def test_deferred_weight_gradient_reduction(monkeypatch):
     assert _rel_err_vs_oracle(desc, dims, graphs, labels, prm, got["1"], eng.layout) <= GTOL
 
 
+@pytest.mark.parametrize("kind", ["routenet", "qsize"])
+def test_fused_sum_backward_weight_gradients(monkeypatch, kind):
+    """The 32-wide sum MPs' backward forms dW = x^T da and dU = h^T du in the kernel (f32 MFMA through a
+    per-wave transpose tile, IGN_SUM_BWD_FUSE=1, default) instead of writing da / du for two split-bf16
+    row contractions (=0): every gradient within fp32 reassociation of the other form, bitwise
+    deterministic, and within the autograd tolerance."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, "nsfnet", 3)
+    prm = MPPlan.from_model_info(mi).init_params(14, bias_scale=0.1)
+    got = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("IGN_SUM_BWD_FUSE", v)
+        eng, _, _, _, _, g = _engine_grads(desc, dims, graphs, labels, prm)
+        got[v] = g.cpu().numpy()
+        if v == "1":
+            np.testing.assert_array_equal(got[v], _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy())
+    named = {v: {n: got[v][off:off + int(np.prod(sh))] for n, sh, off in eng.layout} for v in got}
+    for n in named["0"]:
+        ref = np.linalg.norm(named["0"][n].astype(np.float64))
+        assert np.linalg.norm(named["1"][n].astype(np.float64) - named["0"][n]) <= 1e-6 * ref + 1e-12, n
+    assert _rel_err_vs_oracle(desc, dims, graphs, labels, prm, got["1"], eng.layout) <= GTOL
+
+
 def test_training_reduces_loss():
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "nsfnet", 4)
     prm = MPPlan.from_model_info(mi).init_params(0)
