@@ -333,6 +333,7 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   }
   if (const char* v = getenv("IGN_RESIDENT_PG")) p->resident_pg = atoi(v) != 0;
   if (const char* v = getenv("IGN_RESIDENT_TRAIN")) p->resident_train = atoi(v) != 0;
+  if (const char* v = getenv("IGN_RESIDENT_SAVE_TABLE")) p->resident_save_table = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_BWD_FUSE")) p->sum_bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_DENSE_BF")) p->train_dense_bf = atoi(v) != 0;
@@ -1980,6 +1981,9 @@ extern "C++" int ign::resident_launch(ign_plan* p, ign_batch* b, const ResidentS
     r.path_ver = save->path_ver;
     r.hs_save = save->hs_save;
     r.hsb = b->d_res_hsb;
+    r.tab_save = save->tab_save;
+    r.tab_hole = b->mp[0].zero_row;
+    for (int s = 0; s < sh.n_src; ++s) r.tab_off[s] = b->mp[0].src_off[s];
     for (int s = 0; s < sh.n_src; ++s) {
       r.src_ver[s] = save->src_ver[s];
       r.x_save[s] = save->x_save[s];

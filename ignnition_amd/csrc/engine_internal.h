@@ -272,6 +272,7 @@ struct ign_plan {
   bool resident_pg = true;        // ... with the path states in global memory where they do not fit LDS (IGN_RESIDENT_PG)
   bool resident_path_global = false;   // IGN_RESIDENT=2: that form for every eligible batch (tests)
   bool resident_train = true;     // the training forward on the resident form's SAVE variant (IGN_RESIDENT_TRAIN=0: off)
+  bool resident_save_table = true;   // ... which also saves the ordered MP's tables (IGN_RESIDENT_SAVE_TABLE=0: recompute)
   int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
                                   // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
                                   // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);
@@ -364,6 +365,7 @@ struct ResidentSave {
   float* const* src_ver[kResidentMaxSrc];    // [T + 1] per source entity of the ordered MP
   float* const* hs_save;                     // [T] the ordered MP's per-step states
   float* const* x_save[kResidentMaxSrc];     // [T] per source entity: its sum MP's message sums
+  float* const* tab_save = nullptr;          // [T] optional: the ordered MP's projected table per iteration
 };
 int resident_tables(ign_plan* p, ign_batch* b);   // once per batch; leaves b->resident false if not eligible
 int resident_launch(ign_plan* p, ign_batch* b, const ResidentSave* save);

@@ -225,6 +225,10 @@ struct ResidentArgs {
   float* const* hs_save;
   float* const* x_save[kResidentMaxSrc];
   const int32_t* hsb;         // [headers] the position's first hs_save row (step_ptr + order position)
+  float* const* tab_save;     // SAVE, optional: [T] the ordered MP's projected table per iteration, in
+                              // the batched layout (the backward's table; build_table is skipped)
+  int64_t tab_off[kResidentMaxSrc];   // table row of each source entity's row 0 (MPB::src_off)
+  int64_t tab_hole;           // the table's zero row (a hole: the bias alone)
 };
 // the kernels' dynamic-LDS limit, once per device: call before any launch or stream capture
 hipError_t resident_prepare_device();

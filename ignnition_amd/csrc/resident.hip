@@ -62,6 +62,10 @@ __device__ __forceinline__ void lds4w(float* p, f4 v) { *reinterpret_cast<f4*>(p
 __device__ __forceinline__ float* in_global(float* p) {
   return (float*)(__attribute__((address_space(1))) float*)p;
 }
+// the batched table row of local union row ll (source entity 0's rows, then entity 1's)
+__device__ __forceinline__ int64_t tab_row(const ResidentArgs& a, int64_t ll, int64_t L0, int64_t s00, int64_t s10) {
+  return ll >= L0 ? a.tab_off[1] + s10 + (ll - L0) : a.tab_off[0] + s00 + ll;
+}
 __device__ __forceinline__ void gst4(float* p, f4 v) { *(__attribute__((address_space(1))) f4*)p = v; }
 // the path states: global memory (PG) or LDS
 template <bool G> __device__ __forceinline__ f4 ldp4(const float* p) {
@@ -121,7 +125,7 @@ __device__ __forceinline__ void project_row(const ResidentArgs& a, const f4 (&hn
 // the iteration-0 projected row as project_kernel computes it (f32 MFMA, x.W' over k-steps of 1 on
 // the bias) so the resident forward reproduces the batched forward's bits
 __device__ __forceinline__ void project_row_f32(const ResidentArgs& a, const f4 (&xv)[2], float* tab, int ll,
-                                                bool valid, int lane, int g) {
+                                                bool valid, int lane, int g, float* gsave = nullptr) {
   int lofs = lane;
   asm volatile("" : "+v"(lofs));
   constexpr int H = 32, NT = 2, KX = 32 / 4;
@@ -142,7 +146,10 @@ __device__ __forceinline__ void project_row_f32(const ResidentArgs& a, const f4 
 #pragma unroll
     for (int G = 0; G < 3; ++G)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) lds4w(tab + (int64_t)ll * ST + G * H + 16 * t + 4 * g, acc[G][t]);
+      for (int t = 0; t < NT; ++t) {
+        lds4w(tab + (int64_t)ll * ST + G * H + 16 * t + 4 * g, acc[G][t]);
+        if (gsave) gst4(gsave + G * H + 16 * t + 4 * g, acc[G][t]);   // (the training form's saved table)
+      }
   }
 }
 
@@ -277,8 +284,14 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
     f4 h[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) h[t] = valid ? lds4(hL + (int64_t)ll * SP + 16 * t + 4 * g) : f4{0, 0, 0, 0};
-    project_row_f32(a, h, tab, ll, valid, lane, g);
+    float* gs = nullptr;   // SAVE: the table of iteration 0, row of this union row
+    if constexpr (SAVE)
+      if (a.tab_save) gs = in_global(a.tab_save[0]) + tab_row(a, ll, L0, s00, s10) * 96;
+    project_row_f32(a, h, tab, ll, valid, lane, g, gs);
   }
+  if constexpr (SAVE)   // every saved table's hole row: the bias alone (one workgroup writes them)
+    if (a.tab_save && gph == 0)
+      for (int i = tid; i < a.T * 96; i += 64 * kW) in_global(a.tab_save[i / 96])[a.tab_hole * 96 + i % 96] = a.proj_b[i % 96];
   __syncthreads();
 #ifdef IGN_RES_STAMP
   IGN_STAMP(t_a);
@@ -612,7 +625,11 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
         }
       }
       if (!last) {
-        if constexpr (SAVE) project_row_f32(a, hn, tab, ll, valid, lane, g);   // build_table's projection
+        if constexpr (SAVE) {   // build_table's projection (and the next iteration's saved table)
+          float* gs = nullptr;
+          if (a.tab_save && it + 1 < a.T) gs = in_global(a.tab_save[it + 1]) + tab_row(a, ll, L0, s00, s10) * 96;
+          project_row_f32(a, hn, tab, ll, valid, lane, g, gs);
+        }
         else project_row(a, hn, tab, ll, valid, lane, g);
       }
     }

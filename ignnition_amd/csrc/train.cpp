@@ -87,6 +87,8 @@ struct TrainState {
   int f_it = 0, f_mi = 0;
   bool f_open = false;
   float** res_ptrs = nullptr;   // the graph-resident training forward's version / save pointer arrays
+  std::vector<float*> tsave;    // its saved projected tables of the ordered MP, per iteration
+  bool tab_saved = false;       // this forward saved them (the backward skips build_table)
   // weight gradients formed once per MP instance (T of them per backward) keep their partial tiles
   // here and are reduced once, at ign_backward_end, in instance order (IGN_DEFER_WGRAD=0: per instance)
   struct DeferredGrad {
@@ -610,6 +612,7 @@ int ign_forward_train_begin(ign_plan* p, ign_batch* b) {
     t->cur[e] = 0;
   }
   t->recs.clear();
+  t->tab_saved = false;
   t->f_it = t->f_mi = 0;
   t->f_open = true;
   t->forward_done = false;
@@ -765,9 +768,17 @@ static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
   if ((int)t->ver[path].size() != T + 1) return IGN_OK;
   for (int s = 0; s < S; ++s)
     if ((int)t->ver[src_ent[s]].size() != T + 1) return IGN_OK;
-  // pointer arrays: path versions [T + 1] | per source: versions [T + 1] | hs_save [T] | per source: x_save [T]
-  const int64_t n_ptr = (T + 1) * (1 + S) + T * (1 + S);
+  // pointer arrays: path versions [T + 1] | per source: versions [T + 1] | hs_save [T] | per source:
+  // x_save [T] | the ordered MP's projected tables [T] (saved for the backward: no recompute)
+  const int64_t n_ptr = (T + 1) * (1 + S) + T * (1 + S) + T;
+  const MPB& m0 = b->mp[0];
+  const bool save_tab = p->resident_save_table && m0.n_multi == 0;
   if (!t->res_ptrs) {
+    for (int k = 0; k < T && save_tab; ++k) {
+      float* f = nullptr;
+      if ((rc = talloc(t, &f, (m0.zero_row + 1) * 3 * p->cells[p->mps[0].cell].H))) return rc;
+      t->tsave.push_back(f);
+    }
     hvec<float*> v;
     for (int k = 0; k <= T; ++k) v.push_back(t->ver[path][k]);
     for (int s = 0; s < S; ++s)
@@ -775,6 +786,7 @@ static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
     for (int k = 0; k < T; ++k) v.push_back(t->mp[0].hs[k]);
     for (int s = 0; s < S; ++s)
       for (int k = 0; k < T; ++k) v.push_back(t->mp[sum_mp[s]].xs[k]);
+    for (int k = 0; k < T; ++k) v.push_back(save_tab ? t->tsave[k] : nullptr);
     if ((int64_t)v.size() != n_ptr) return fail(IGN_ERR_RUNTIME, "resident training pointers");
     if ((rc = tupload(t, &t->res_ptrs, v))) return rc;
   }
@@ -783,7 +795,9 @@ static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
   for (int s = 0; s < S; ++s) sv.src_ver[s] = t->res_ptrs + (T + 1) * (1 + s);
   sv.hs_save = t->res_ptrs + (T + 1) * (1 + S);
   for (int s = 0; s < S; ++s) sv.x_save[s] = t->res_ptrs + (T + 1) * (1 + S) + T * (1 + s);
+  if (!t->tsave.empty()) sv.tab_save = t->res_ptrs + (T + 1) * (1 + S) + T * (1 + S);
   if ((rc = resident_launch(p, b, &sv))) return rc;
+  t->tab_saved = !t->tsave.empty();
   // the records ign_forward_train_mp would have left (GM:404-603 order)
   for (int it = 0; it < T; ++it)
     for (int mi = 0; mi < (int)p->mps.size(); ++mi) {
@@ -1003,8 +1017,10 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
     float* grk = grads + cp.off_rk;
     float* gb = grads + cp.off_b;
     if (mp.sorted) {
-      if ((rc = build_table(p, mp, mb, cp, srcs))) return rc;
-      SeqBwdArgs a{mt.hs[rec.it], mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
+      // the forward's table of this instance: saved by the resident training forward, else recomputed
+      const bool saved = t->tab_saved && rec.mi == 0 && rec.it < (int)t->tsave.size();
+      if (!saved && (rc = build_table(p, mp, mb, cp, srcs))) return rc;
+      SeqBwdArgs a{mt.hs[rec.it], saved ? t->tsave[rec.it] : mb.d_table, mb.d_order, mb.d_len, mb.d_step_ptr, mb.d_step_code,
                    p->d_packed + cp.pk_u, p->d_packed + cp.pk_b, p->d_packed + cp.pk_ut, dh_in, dh_out,
                    t->ga, t->gu, mb.n_dst};
       a.h_in = t->ver[dst][rec.v_in];
