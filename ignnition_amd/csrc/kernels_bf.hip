@@ -2108,6 +2108,12 @@ hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float
 }
 
 bool dense_bf_supported(int K, int M) {
+  // whole stages of G 16-unit tiles: G <= 8 for K < 256; K = 256 stages two tiles (NP = 2) or one,
+  // so the readout's first-layer input gradient (K = 256 -> M = 32, RouteNet's state width) runs
+  // here instead of on row_gemm_t's f32 MFMA
+#ifndef IGN_DENSE_BF_M128
+  if (K == 256) return M > 0 && M % 32 == 0;
+#endif
   return (K == 32 || K == 64 || K == 128 || K == 256) && M % 128 == 0 && M > 0;
 }
 
