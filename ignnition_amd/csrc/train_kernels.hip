@@ -644,9 +644,7 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
     f4 acc = accumulate ? ld4(out + r * cols + c) : f4{0, 0, 0, 0};
     const int k1 = ptr[r + 1];
     int k = ptr[r];
-    // eight (then four) rows in flight; the additions keep the CSR order (bitwise the same as one
-    // at a time)
-#ifndef IGN_GATHER4   // A/B: four rows in flight only
+    // eight rows in flight; the additions keep the CSR order (bitwise the same as one at a time)
     for (; k + 8 <= k1; k += 8) {
       int i8[8];
 #pragma unroll
@@ -656,6 +654,23 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
       for (int u = 0; u < 8; ++u) v8[u] = ld4(in + (int64_t)i8[u] * cols + c);
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += v8[u];
+    }
+#ifndef IGN_GATHER_SERIAL_TAIL
+    // the rest (< 8) as one batch too: indices clamped to the row's last entry (a cached re-read),
+    // additions masked.  A RouteNet path (~7 links) was a 4-batch and three dependent idx -> row
+    // round trips: the link-update backward's gather 114 -> 98 us, 16.60 -> 16.43 ms per training
+    // step (same box, tools/gpu_calls/r05_c54.sh)
+    if (k < k1) {
+      int i8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) i8[u] = idx[min(k + u, k1 - 1)];
+      f4 v8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v8[u] = ld4(in + (int64_t)i8[u] * cols + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < k1) acc += v8[u];
+      k = k1;
     }
 #endif
     for (; k + 4 <= k1; k += 4) {
