@@ -633,57 +633,43 @@ __global__ __launch_bounds__(256) void sum_gru_bwd_kernel(SumBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// V: 4-float vectors per thread (cols % (4 V) == 0); each thread walks its row's list in batches
+// of eight entries, the last (< 8) batch with indices clamped to the list's last entry (a cached
+// re-read) and masked additions; the additions keep the CSR order (bitwise one at a time).  The
+// batched tail: a RouteNet path (~3 links) was a 4-batch and single rows, each a dependent
+// idx -> row round trip; the link-update backward's gather 114 -> 98 us, 16.60 -> 16.43 ms per
+// training step (same box, tools/gpu_calls/r05_c54.sh)
+template <int V>
 __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, const int32_t* __restrict__ ptr,
                                       const int32_t* __restrict__ idx, const float* __restrict__ in, int cols,
                                       int accumulate) {
-  const int q = cols >> 2;
+  const int q = cols / (4 * V);
   const int64_t total = n_rows * q;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = e / q;
-    const int c = (int)(e - r * q) * 4;
-    f4 acc = accumulate ? ld4(out + r * cols + c) : f4{0, 0, 0, 0};
+    const int c = (int)(e - r * q) * 4 * V;
+    f4 acc[V];
+#pragma unroll
+    for (int w = 0; w < V; ++w) acc[w] = accumulate ? ld4(out + r * cols + c + 4 * w) : f4{0, 0, 0, 0};
     const int k1 = ptr[r + 1];
-    int k = ptr[r];
-    // eight rows in flight; the additions keep the CSR order (bitwise the same as one at a time)
-    for (; k + 8 <= k1; k += 8) {
-      int i8[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) i8[u] = idx[k + u];
-      f4 v8[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v8[u] = ld4(in + (int64_t)i8[u] * cols + c);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v8[u];
-    }
-#ifndef IGN_GATHER_SERIAL_TAIL
-    // the rest (< 8) as one batch too: indices clamped to the row's last entry (a cached re-read),
-    // additions masked.  A RouteNet path (~7 links) was a 4-batch and three dependent idx -> row
-    // round trips: the link-update backward's gather 114 -> 98 us, 16.60 -> 16.43 ms per training
-    // step (same box, tools/gpu_calls/r05_c54.sh)
-    if (k < k1) {
+    for (int k = ptr[r]; k < k1; k += 8) {
       int i8[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) i8[u] = idx[min(k + u, k1 - 1)];
-      f4 v8[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v8[u] = ld4(in + (int64_t)i8[u] * cols + c);
+      f4 v8[8][V];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (k + u < k1) acc += v8[u];
-      k = k1;
+#pragma unroll
+        for (int w = 0; w < V; ++w) v8[u][w] = ld4(in + (int64_t)i8[u] * cols + c + 4 * w);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < k1) {
+#pragma unroll
+          for (int w = 0; w < V; ++w) acc[w] += v8[u][w];
+        }
     }
-#endif
-    for (; k + 4 <= k1; k += 4) {
-      const int i0 = idx[k], i1 = idx[k + 1], i2 = idx[k + 2], i3 = idx[k + 3];
-      const f4 v0 = ld4(in + (int64_t)i0 * cols + c), v1 = ld4(in + (int64_t)i1 * cols + c);
-      const f4 v2 = ld4(in + (int64_t)i2 * cols + c), v3 = ld4(in + (int64_t)i3 * cols + c);
-      acc += v0;
-      acc += v1;
-      acc += v2;
-      acc += v3;
-    }
-    for (; k < k1; ++k) acc += ld4(in + (int64_t)idx[k] * cols + c);
-    st4(out + r * cols + c, acc);
+#pragma unroll
+    for (int w = 0; w < V; ++w) st4(out + r * cols + c + 4 * w, acc[w]);
   }
 }
 
@@ -1589,8 +1575,10 @@ hipError_t launch_csr_gather_add(float* out, int64_t n_rows, const int32_t* ptr,
                                  int cols, int accumulate, hipStream_t st) {
   if (n_rows == 0) return hipSuccess;
   if (cols % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(csr_gather_add_kernel, dim3(blocks_for(n_rows * (cols / 4))), dim3(256), 0, st, out, n_rows, ptr,
-                     idx, in, cols, accumulate);
+  // V = 2 (8 columns per thread) for the ordered update's 96-column table gradient measured slower:
+  // 305 -> 330 us per launch, 16.41 -> 16.58 ms per training step (tools/gpu_calls/r05_c57.sh)
+  hipLaunchKernelGGL(csr_gather_add_kernel<1>, dim3(blocks_for(n_rows * (cols / 4))), dim3(256), 0, st, out, n_rows,
+                     ptr, idx, in, cols, accumulate);
   return hipGetLastError();
 }
 
