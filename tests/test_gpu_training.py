@@ -405,7 +405,8 @@ def test_split_bf16_backward_matches_f32(monkeypatch, switch):
     """The split-bf16 weight-gradient contractions (tsgemm_bf) against their f32-MFMA form, and the training
     Dense layers' split-fp16 row GEMMs (IGN_TRAIN_DENSE_H16, forward and backward) against their
     split-bf16 form: bitwise deterministic, and equal to fp32 reassociation (relative L2 <= 1e-5)
-    on 24 synth50 graphs."""
+    on 24 synth50 graphs.  IGN_TRAIN_DENSE_BF=0 also puts the readout's first-layer input gradient
+    (256 -> 32, on dense_bf since round 5) back on row_gemm_t's f32 MFMA."""
     desc, dims, mi, graphs, labels = workloads.make_batch_inputs("routenet", "synth50", 24)
     prm = MPPlan.from_model_info(mi).init_params(13, bias_scale=0.1)
     monkeypatch.setenv(switch, "1")
