@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void sum_gru_bwd_kernel(SumBwdArgs a) {
 // batched tail: a RouteNet path (~3 links) was a 4-batch and single rows, each a dependent
 // idx -> row round trip; the link-update backward's gather 114 -> 98 us, 16.60 -> 16.43 ms per
 // training step (same box, tools/gpu_calls/r05_c54.sh)
-template <int V>
+template <int V, bool NT = false>
 __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, const int32_t* __restrict__ ptr,
                                       const int32_t* __restrict__ idx, const float* __restrict__ in, int cols,
                                       int accumulate) {
@@ -660,7 +660,10 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
-        for (int w = 0; w < V; ++w) v8[u][w] = ld4(in + (int64_t)i8[u] * cols + c + 4 * w);
+        for (int w = 0; w < V; ++w) {
+          const float* pv = in + (int64_t)i8[u] * cols + c + 4 * w;
+          v8[u][w] = NT ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(pv)) : ld4(pv);
+        }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (k + u < k1) {
@@ -1577,6 +1580,16 @@ hipError_t launch_csr_gather_add(float* out, int64_t n_rows, const int32_t* ptr,
   if (cols % 4) return hipErrorInvalidValue;
   // V = 2 (8 columns per thread) for the ordered update's 96-column table gradient measured slower:
   // 305 -> 330 us per launch, 16.41 -> 16.58 ms per training step (tools/gpu_calls/r05_c57.sh)
+#ifndef IGN_GATHER_TEMPORAL
+  // the wide gather (the ordered update's ga rows, 1.4 GB read once per MP instance) loads its rows
+  // non-temporally, so they do not push the other kernels' data out of L2 / MALL: 16.49 -> 16.20 ms
+  // per training step, same box (tools/gpu_calls/r05_c59.sh); the same bits
+  if (cols >= 64) {
+    hipLaunchKernelGGL((csr_gather_add_kernel<1, true>), dim3(blocks_for(n_rows * (cols / 4))), dim3(256), 0, st, out,
+                       n_rows, ptr, idx, in, cols, accumulate);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL(csr_gather_add_kernel<1>, dim3(blocks_for(n_rows * (cols / 4))), dim3(256), 0, st, out, n_rows,
                      ptr, idx, in, cols, accumulate);
   return hipGetLastError();
