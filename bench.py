@@ -654,13 +654,14 @@ def main():
     seq_v = int(os.environ.get("IGN_SEQ_VARIANT", "6"))
     seq_v = seq_v if seq_v in (2, 4) else 6          # the engine's mapping (engine.cpp)
     ro_v = int(os.environ.get("IGN_READOUT_VARIANT", "4"))
-    ro_v = ro_v if ro_v in (1, 2) else 4
+    ro_v = ro_v if ro_v in (1, 2, 5) else 4
     sum_v = int(os.environ.get("IGN_SUM_VARIANT", "8"))
     BF = "split-bf16: exact 3-piece bf16 operands, %d products, fp32 accumulate"
     H16 = ("split-fp16: power-of-two-scaled 2-piece fp16 operands (RNE, 2^-22 relative), %d products, "
            "fp32 accumulate")
     seq_c = {2: "f32 MFMA", 4: BF % 6, 6: H16 % 3}
-    ro_c = {1: "f32 MFMA", 2: BF % 6, 4: "both layers " + H16 % 3}
+    ro_c = {1: "f32 MFMA", 2: BF % 6, 4: "both layers " + H16 % 3 + ", 16x16x32",
+            5: "both layers " + H16 % 3 + ", 32x32x16"}
     contraction = {"ordered_update_hU": seq_c.get(seq_v, "f32 MFMA") if plan.hidden[0] in (32, 64) else "f32 MFMA",
                    "readout": ro_c.get(ro_v, BF % 6),
                    # sum variants 8 (default) / 7: split-fp16 / split-bf16 x.W and h.U at DIN = H = 64,
@@ -742,6 +743,8 @@ def resident_roof(batches, roof, isolated):
     out = {"resident": {"form": {0: "all states in LDS", 1: "path states in HBM/L2",
                                  2: "path states and sum CSR in HBM/L2"}[infos[0]["form"]],
                         "launches_per_step": n, "lds_bytes": int(avg["lds_bytes"]),
+                        "workgroups_per_launch": infos[0].get("workgroups"),
+                        "graphs_per_workgroup": infos[0].get("graphs_per_workgroup"),
                         "tile_steps_per_launch": avg["tile_steps"], "union_tiles_per_iteration": avg["union_tiles"],
                         "segmented_rows": avg["seg_rows"], "sum_messages_per_iteration": avg["messages"]},
            # alg bytes = B_stage over the launch's T x MPs (the line's alg_bytes_per_launch);
@@ -755,8 +758,8 @@ def resident_roof(batches, roof, isolated):
         mix = json.load(f)["kernels"].get(RES_KERNEL[infos[0]["form"]])
     if not mix:
         return out
-    graphs = max(b.num_graphs for b in batches)
-    simds = 4 * min(graphs, N_CU)
+    wgs = max(i.get("workgroups") or 0 for i in infos) or max(b.num_graphs for b in batches)
+    simds = 4 * min(wgs, N_CU)
     issue_ms = avg["tile_steps"] * mix["cycles_per_tile_step"] / (simds * CLOCK_GHZ * 1e9) * 1e3
     iso_ms = isolated["ms"] / isolated["launches"] if isolated and isolated["launches"] else None
     out["issue"] = {"what": "phase A's VALU/MFMA issue floor: tile_steps x cycles_per_tile_step / (SIMDs x clock)",

@@ -79,7 +79,8 @@ class ResidentInfo(C.Structure):
     _fields_ = [("active", i32), ("form", i32), ("lds_bytes", i64), ("tile_steps", i64), ("union_tiles", i64),
                 ("seg_rows", i64), ("messages", i64), ("bytes_compulsory", C.c_double),
                 ("bytes_roundtrip", C.c_double), ("bytes_stage", C.c_double), ("flops", C.c_double),
-                ("mfma_bf16", C.c_double), ("mfma_f32", C.c_double)]
+                ("mfma_bf16", C.c_double), ("mfma_f32", C.c_double), ("workgroups", i32),
+                ("graphs_per_workgroup", i32)]
 
 
 class Stats(C.Structure):
@@ -110,7 +111,7 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_forward_train_end", "ign_backward_begin", "ign_backward_mp", "ign_backward_end",
            "ign_batch_train_buffers", "ign_batch_read_predictions", "ign_batch_resident_info"]
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -197,9 +198,16 @@ def _load():
 
 
 lib = _load()
-if lib.ign_abi_version() != ABI_VERSION and os.environ.get("IGN_AB_LIB") != "1":   # (A/B: an older build)
-    raise ImportError("libignmp.so ABI %d, bindings expect %d: rebuild (python -m ignnition_amd.build)"
-                      % (lib.ign_abi_version(), ABI_VERSION))
+if lib.ign_abi_version() != ABI_VERSION:
+    if os.environ.get("IGN_AB_LIB") != "1":
+        raise ImportError("libignmp.so ABI %d, bindings expect %d: rebuild (python -m ignnition_amd.build)"
+                          % (lib.ign_abi_version(), ABI_VERSION))
+    # A/B against an older build: the ctypes structs (BatchInfo, Stats, ResidentInfo) are this
+    # ABI's layouts, so fields the older library does not fill read as garbage -- say so loudly
+    import sys as _sys
+    print("ignnition_amd: WARNING: IGN_AB_LIB=1 loads %s with ABI %d, the bindings are ABI %d; struct "
+          "layouts may differ" % (os.environ.get("IGN_LIB_PATH", "libignmp.so"), lib.ign_abi_version(), ABI_VERSION),
+          file=_sys.stderr)
 
 
 class EngineError(RuntimeError):

@@ -17,9 +17,10 @@ OUT = os.path.join(HERE, "libignmp.so")
 # the resident kernel's phase-A instruction mix (tools/isa_mix.py), read by bench.py's roofline.issue
 ISA_MIX = os.path.join(HERE, "isa_mix.json")
 SOURCES = ["engine.cpp", "devpool.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "plan_json.cpp", "kernels.hip", "kernels_bf.hip",
-           "train_kernels.hip", "readout_kernels.hip", "resident.hip"]
+           "train_kernels.hip", "readout_kernels.hip", "resident.hip", "readout_h32.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
-EXTRA = {"kernels_bf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "resident.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+EXTRA = {"kernels_bf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "resident.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+         "readout_h32.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def needs_build() -> bool:
@@ -61,6 +62,15 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
 
 def write_isa_mix(hipcc: str) -> None:
+    """bench.py's roofline.issue input.  A diagnostic: a failure here (an asm or parser change, no
+    hipcc) warns instead of failing build() -- bench.py runs without the file."""
+    try:
+        _write_isa_mix(hipcc)
+    except Exception as e:   # noqa: BLE001
+        print("ignnition_amd.build: warning: isa_mix.json not written (%s)" % e, file=sys.stderr)
+
+
+def _write_isa_mix(hipcc: str) -> None:
     tool = os.path.join(HERE, "..", "tools", "isa_mix.py")
     if not os.path.exists(tool):
         return

@@ -10,8 +10,11 @@
 //
 // IGN_POOL=0 bypasses the cache (hipMalloc / hipFree per block).  IGN_POOL_POISON=1 fills every
 // scratch block it hands out with NaN (0xFF bytes): the parity tests under it show that no kernel
-// reads batch scratch it has not written (tests/test_gpu_parity.py).  IGN_POOL_CACHE_GB caps the
-// idle bytes kept (default: half the device's memory; ign_plan_trim_cache releases them all).
+// reads batch scratch it has not written (tests/test_gpu_parity.py).  The idle bytes are capped per
+// device across every pool of the process (one per plan: bench's sub-batch engines, a trainer's eval
+// engine): IGN_POOL_CACHE_GB, default half the device memory free when the first pool was created;
+// ign_plan_trim_cache releases a plan's.  When hipMalloc runs out of memory, every pool of the device
+// gives its idle blocks back before the retry, not only the allocating plan's.
 //
 // The host side has the same problem: the batch builders' index tables are ~10^8 bytes of host
 // memory per batch.  hvec (engine_internal.h) draws blocks >= 1 MiB from a process-wide cache
@@ -20,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -57,6 +61,22 @@ int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 
+// the idle-byte budget of one device, shared by every pool of the process on it
+struct DeviceBudget {
+  std::atomic<int64_t> idle{0};
+  size_t cap = 0;
+};
+
+struct Registry {
+  std::mutex mu;
+  std::map<int, DeviceBudget> budgets;              // std::map: stable addresses
+  std::vector<std::weak_ptr<DevPool>> pools;
+};
+Registry& registry() {
+  static Registry* r = new Registry();   // never destroyed: pools may outlive static destruction order
+  return *r;
+}
+
 }  // namespace
 
 struct DevPool {
@@ -68,9 +88,18 @@ struct DevPool {
   std::map<size_t, std::vector<Idle>> idle;    // by size class, oldest first
   std::unordered_map<void*, size_t> live;      // block -> size class
   size_t idle_bytes = 0;
-  size_t cap = (size_t)64 << 30;
+  DeviceBudget* budget = nullptr;
   bool enabled = true, poison = false;
   int device = 0;
+
+  void add_idle(size_t cls) {
+    idle_bytes += cls;
+    budget->idle += (int64_t)cls;
+  }
+  void sub_idle(size_t cls) {
+    idle_bytes -= cls;
+    budget->idle -= (int64_t)cls;
+  }
 
   // free idle blocks whose fence has completed, oldest classes' first, until idle_bytes <= target;
   // with wait, also those still in flight (their fences are waited for).  With out, the blocks are
@@ -84,7 +113,7 @@ struct DevPool {
         if (v[i].fence->ready()) {
           if (out) out->push_back(v[i].ptr);
           else hipFree(v[i].ptr);
-          idle_bytes -= it->first;
+          sub_idle(it->first);
           v.erase(v.begin() + i);
         } else {
           ++i;
@@ -95,8 +124,11 @@ struct DevPool {
   }
 
   ~DevPool() {
+    int prev = 0;
+    hipGetDevice(&prev);
     hipSetDevice(device);
     trim(0, true);
+    hipSetDevice(prev);
   }
 };
 
@@ -105,17 +137,64 @@ std::shared_ptr<DevPool> pool_create(int device) {
   pool->device = device;
   pool->enabled = env_int("IGN_POOL", 1) != 0;
   pool->poison = env_int("IGN_POOL_POISON", 0) != 0;
-  // default cap: half the device's memory.  A training batch of 512 x synth50 holds ~11 GB of
-  // device blocks and the input pipeline keeps workers + 1 of them in flight; under a smaller cap
-  // (16 GB before) every release trimmed blocks with hipFree -- which waits for the device -- under
-  // the pool lock that the step's own release then waited for: 22 -> 57 ms per fresh-batch step
-  size_t half = (size_t)16 << 30;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.totalGlobalMem / 2 > half) half = prop.totalGlobalMem / 2;
-  const int gb = env_int("IGN_POOL_CACHE_GB", -1);
-  pool->cap = gb >= 0 ? (size_t)gb << 30 : half;
+  Registry& reg = registry();
+  std::lock_guard<std::mutex> g(reg.mu);
+  auto found = reg.budgets.find(device);
+  if (found == reg.budgets.end()) {
+    // the device's cap, once: half its memory free now (round 5 kept half the TOTAL memory per pool,
+    // so several plans could together cache more than the device has).  A training batch of 512 x
+    // synth50 holds ~11 GB of device blocks and the input pipeline keeps workers + 1 of them in
+    // flight; under a 16 GB cap every release trimmed blocks with hipFree -- which waits for the
+    // device -- under the pool lock the step's own release then waited for (22 -> 57 ms per step)
+    DeviceBudget& b = reg.budgets[device];
+    const int gb = env_int("IGN_POOL_CACHE_GB", -1);
+    size_t free_b = 0, total_b = 0;
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (hipSetDevice(device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess) b.cap = free_b / 2;
+    else b.cap = (size_t)16 << 30;
+    hipSetDevice(prev);
+    if (gb >= 0) b.cap = (size_t)gb << 30;
+    found = reg.budgets.find(device);
+  }
+  pool->budget = &found->second;
+  // drop expired entries while here
+  auto& v = reg.pools;
+  v.erase(std::remove_if(v.begin(), v.end(), [](const std::weak_ptr<DevPool>& w) { return w.expired(); }), v.end());
+  v.push_back(pool);
   return pool;
 }
+
+namespace {
+
+// the other live pools of a device (their idle blocks are given back on OOM or over the budget)
+std::vector<std::shared_ptr<DevPool>> device_pools(int device, const DevPool* except) {
+  Registry& reg = registry();
+  std::lock_guard<std::mutex> g(reg.mu);
+  std::vector<std::shared_ptr<DevPool>> out;
+  for (auto& w : reg.pools)
+    if (auto p = w.lock())
+      if (p.get() != except && p->device == device) out.push_back(std::move(p));
+  return out;
+}
+
+// free idle blocks of the device's other pools until its idle bytes are within `target`
+// (each pool under its own lock, never two at once; wait: also blocks still in flight)
+void trim_device(DevPool* self, size_t target, bool wait) {
+  for (auto& p : device_pools(self->device, self)) {
+    if (self->budget->idle.load() <= (int64_t)target) return;
+    std::vector<void*> victims;
+    {
+      std::lock_guard<std::mutex> g(p->mu);
+      const int64_t excess = p->budget->idle.load() - (int64_t)target;
+      if (excess <= 0) return;
+      p->trim(p->idle_bytes > (size_t)excess ? p->idle_bytes - (size_t)excess : 0, wait, &victims);
+    }
+    for (void* v : victims) hipFree(v);
+  }
+}
+
+}  // namespace
 
 bool pool_enabled(const DevPool* pool) { return pool && pool->enabled; }
 
@@ -137,7 +216,7 @@ hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch) {
           *out = v[i].ptr;
           v.erase(v.begin() + i);
           if (v.empty()) pool->idle.erase(it);
-          pool->idle_bytes -= cls;
+          pool->sub_idle(cls);
           pool->live[*out] = cls;
           break;
         }
@@ -145,12 +224,13 @@ hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch) {
   }
   if (!*out) {
     hipError_t e = hipMalloc(out, cls);
-    if (e == hipErrorOutOfMemory) {   // give back every idle block (waiting for in-flight ones), retry
+    if (e == hipErrorOutOfMemory) {   // give back every idle block of the device (waiting for in-flight ones), retry
       (void)hipGetLastError();
       {
         std::lock_guard<std::mutex> g(pool->mu);
         pool->trim(0, true);
       }
+      trim_device(pool, 0, true);
       e = hipMalloc(out, cls);
     }
     if (e != hipSuccess) {
@@ -187,11 +267,14 @@ void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t a
       const size_t cls = it->second;
       pool->live.erase(it);
       pool->idle[cls].push_back({b, fence});
-      pool->idle_bytes += cls;
+      pool->add_idle(cls);
     }
-    if (pool->idle_bytes > pool->cap) pool->trim(pool->cap, false, &victims);
+    // over the device's budget: this pool's own idle blocks first, then the other pools'
+    const int64_t excess = pool->budget->idle.load() - (int64_t)pool->budget->cap;
+    if (excess > 0) pool->trim(pool->idle_bytes > (size_t)excess ? pool->idle_bytes - (size_t)excess : 0, false, &victims);
   }
   for (void* v : victims) hipFree(v);
+  if (pool->budget->idle.load() > (int64_t)pool->budget->cap) trim_device(pool, pool->budget->cap, false);
 }
 
 // ---- host blocks ----------------------------------------------------------------------------

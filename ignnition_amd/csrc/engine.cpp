@@ -278,6 +278,9 @@ int ign::repack(ign_plan* p) {
     const DenseP &l1 = p->dense[0], &l2 = p->dense[1];
     HIP_TRY(launch_pack_readout_h16(p->d_params + l1.off_w, l1.use_bias ? p->d_params + l1.off_b : nullptr,
                                     p->d_params + l2.off_w, p->d_packed + l2.pk_h, l1.in, l1.out, l2.out, p->stream));
+    if (l2.pk_h32 >= 0)
+      HIP_TRY(launch_pack_readout_h32(p->d_params + l1.off_w, l1.use_bias ? p->d_params + l1.off_b : nullptr,
+                                      p->d_params + l2.off_w, p->d_packed + l2.pk_h32, l1.in, l1.out, l2.out, p->stream));
   }
   for (auto& dp : p->dense) {
     if (dp.pk_w >= 0) HIP_TRY(launch_pack_dense(p->d_params + dp.off_w, p->d_packed + dp.pk_w, dp.in, dp.out, p->stream));
@@ -333,6 +336,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   }
   if (const char* v = getenv("IGN_RESIDENT_PG")) p->resident_pg = atoi(v) != 0;
   if (const char* v = getenv("IGN_RESIDENT_TRAIN")) p->resident_train = atoi(v) != 0;
+  if (const char* v = getenv("IGN_RES_LPT")) p->res_lpt = atoi(v) != 0;
+  if (const char* v = getenv("IGN_RES_GROUP")) p->res_group = std::max(0, atoi(v));
   if (const char* v = getenv("IGN_RESIDENT_SAVE_TABLE")) p->resident_save_table = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_FUSE")) p->bwd_fuse = atoi(v) != 0;
   if (const char* v = getenv("IGN_SUM_BWD_FUSE")) p->sum_bwd_fuse = atoi(v) != 0;
@@ -343,9 +348,9 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
   if (const char* v = getenv("IGN_TRAIN_FUSED_READOUT")) p->train_fused_readout = atoi(v) != 0;
   if (const char* v = getenv("IGN_BWD_BF")) p->bwd_bf = atoi(v) != 0;
   if (const char* v = getenv("IGN_TRAIN_SEQ_H16")) p->train_seq_h16 = atoi(v) != 0;
-  if (const char* v = getenv("IGN_READOUT_VARIANT")) {   // 4 (default), 2 or 1; anything else: 4
+  if (const char* v = getenv("IGN_READOUT_VARIANT")) {   // 4 (default), 5, 2 or 1; anything else: 4
     const int rv = atoi(v);
-    p->readout_variant = rv == 1 || rv == 2 ? rv : 4;
+    p->readout_variant = rv == 1 || rv == 2 || rv == 5 ? rv : 4;
   }
   p->T = d->num_iterations;
   p->ents.assign(d->entities, d->entities + d->num_entities);
@@ -541,7 +546,10 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
         readout_bf_supported(p->dense[0].in, p->dense[0].out, p->dense[1].out, p->dense[0].act, p->dense[1].act)) {
       dp.pk_bf = pk;
       pk = align(pk + 3LL * dp.in * dp.out / 2);
-      if (l == 1) { dp.pk_h = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64); }
+      if (l == 1) {
+        dp.pk_h = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64);
+        dp.pk_h32 = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64);
+      }
     }
     if (dense_bf_supported(dp.in, dp.out)) {
       dp.pk_bfn = pk;
@@ -746,14 +754,17 @@ static size_t resident_lds_bytes(int64_t paths, int64_t urows, int64_t msgs, int
 }
 
 // a sum MP's destinations with at least this many messages take the segmented sum (sum_seg_kernel,
-// one wave per destination); the others the lane walk of the GRU-step kernel (IGN_SUM_WINDOW: 0 never,
-// 2 always).  Per destination, so a graph's rows take the same order alone and in any batch.
-static int64_t seg_min_messages(const ign_plan* p) {
-  return p->sum_window == 0 ? INT64_MAX : p->sum_window == 2 ? 0 : 64;
-}
+// one wave per destination); the others the lane walk of the GRU-step kernel (IGN_SUM_WINDOW=2: every
+// destination segmented).  Per destination, so a graph's rows take the same order alone and in any batch.
+// IGN_SUM_WINDOW=0, the lane walk's A/B switch, refuses a batch with a destination of >= 64 messages
+// (ign_batch_create): a float32 chain that long leaves the fp32 class -- Q-size synth50's nodes as
+// lane walks landed at 4.3x IEEE float32's error (all of them) and 1.8x (those below 128), DESIGN.md §4
+constexpr int64_t kSegMinMessages = 64;
+static int64_t seg_min_messages(const ign_plan* p) { return p->sum_window == 2 ? 0 : kSegMinMessages; }
 
-// per-graph tables of the resident forward; leaves b->resident false where it does not apply
-static int resident_batch(ign_plan* p, ign_batch* b) {
+// per-graph tables of the resident forward, K graphs per workgroup; leaves b->resident false where it
+// does not apply
+static int resident_batch_k(ign_plan* p, ign_batch* b, int K) {
   ResShape sh;
   if (!resident_plan_shape(p, &sh)) return IGN_OK;
   const int path = sh.path, S = sh.n_src;
@@ -761,10 +772,20 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   if (b->halo[path] || ma.n_multi || (int)ma.src_off.size() != S) return IGN_OK;
   for (int s = 0; s < S; ++s)
     if (b->halo[sh.src_ent[s]]) return IGN_OK;
-  const int G = b->G;
-  const auto& po = b->row_off[path];
-  const std::vector<int64_t>* so[kResidentMaxSrc] = {&b->row_off[sh.src_ent[0]],
-                                                    S > 1 ? &b->row_off[sh.src_ent[1]] : nullptr};
+  // a workgroup's "graph" is a group of K consecutive graphs of the batch (round 6, IGN_RES_GROUP):
+  // their disjoint union is one graph to the kernel (concatenated local rows, one tile counter, one
+  // set of union-row tiles), so small graphs fill the 16 waves -- GEANT2's 35 path tiles and 5
+  // union-row tiles per graph leave most waves idle in phase A's tail and in phase B.  Every row is
+  // computed as before (tiles of paths sorted by length across the group: the scale caveat above)
+  const int G = (b->G + K - 1) / K;
+  std::vector<int64_t> po_g(G + 1), so_g[kResidentMaxSrc];
+  for (int k = 0; k <= G; ++k) po_g[k] = b->row_off[path][std::min(k * K, b->G)];
+  for (int s = 0; s < S; ++s) {
+    so_g[s].resize(G + 1);
+    for (int k = 0; k <= G; ++k) so_g[s][k] = b->row_off[sh.src_ent[s]][std::min(k * K, b->G)];
+  }
+  const auto& po = po_g;
+  const std::vector<int64_t>* so[kResidentMaxSrc] = {&so_g[0], S > 1 ? &so_g[1] : nullptr};
   auto Ls = [&](int s, int g) -> int64_t { return s < S ? (*so[s])[g + 1] - (*so[s])[g] : 0; };
   // union rows: per graph, source entity 0's rows, then entity 1's
   std::vector<int64_t> uo(G + 1, 0);
@@ -878,6 +899,21 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
     for (int f = 0; f < 3; ++f)
       lds[f] = std::max(lds[f], resident_lds_bytes(po[g + 1] - po[g], U, nmsg[g], lcode_off[g + 1] - lcode_off[g], f));
   }
+  // the workgroups' graphs, longest first (round 6): a launch of more graphs than CUs -- or the second
+  // of two sub-batch launches, whose workgroups take the CUs the first one frees -- is a list
+  // schedule in workgroup order, so longest-first is LPT.  The estimate, in cycles of one workgroup:
+  // phase A's tile-steps over 4 SIMDs at ~1 300 cycles each, phase B's messages at ~6
+  hvec<int32_t> gorder(G);
+  {
+    std::vector<double> cost(G, 0.0);
+    for (int g = 0; g < G; ++g) {
+      double ts = 0;
+      for (size_t k = 0; k < pp[g].size(); k += 16) ts += ma.h_len[pp[g][k]];
+      cost[g] = ts * 325.0 + (double)nmsg[g] * 6.0;
+    }
+    std::iota(gorder.begin(), gorder.end(), 0);
+    std::stable_sort(gorder.begin(), gorder.end(), [&](int32_t x, int32_t y) { return cost[x] > cost[y]; });
+  }
   // every state in LDS where the largest graph's fit, else the path states in global memory, else
   // also the sum MPs' CSR
   int form = IGN_RES_ALL_LDS;
@@ -901,11 +937,12 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
       (rc = dev_upload(b, &b->d_res_lmsg_off, lmsg_off)) || (rc = dev_upload(b, &b->d_res_lmsg_ptr, lmsg_ptr)) ||
       (rc = dev_upload(b, &b->d_res_lmsg_src, lmsg_src)) || (rc = dev_upload(b, &b->d_res_lorder, lorder)) ||
       (rc = dev_upload(b, &b->d_res_lnseg, lnseg)) || (rc = dev_upload(b, &b->d_res_lcode_off, lcode_off)) ||
-      (rc = dev_upload(b, &b->d_res_hsb, hsb)) ||
+      (rc = dev_upload(b, &b->d_res_hsb, hsb)) || (rc = dev_upload(b, &b->d_res_gorder, gorder)) ||
       (rc = dev_upload(b, &b->d_res_lcode, lcode)))
     return rc;
   b->res_lds = lds[form];
   b->res_form = form;
+  b->res_graphs = G;
   // the cost model of one launch (ign_batch_resident_info)
   ign_resident_info_t& ri = b->res_info;
   ri = ign_resident_info_t{};
@@ -948,6 +985,8 @@ static int resident_batch(ign_plan* p, ign_batch* b) {
   for (int g = 0; g < G; ++g) ptiles += (double)((uo[g + 1] - uo[g] + 15) / 16);
   ri.mfma_bf16 = (p->T * (tile_steps * 18.0 + utiles * 72.0) + (p->T - 1) * utiles * 36.0) * kMfmaBf16Flops;
   ri.mfma_f32 = ptiles * 48.0 * kMfmaF32Flops;
+  ri.workgroups = G;
+  ri.graphs_per_workgroup = K;
   b->resident = true;
   return IGN_OK;
 }
@@ -1374,8 +1413,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         for (int g = 0; g < G; ++g)
           max_src_rows = std::max(max_src_rows, b->row_off[mp.src[0].entity][g + 1] - b->row_off[mp.src[0].entity][g]);
       const int64_t win_rows = DIN == 16 ? 2400 : DIN == 32 ? 1200 : 600;   // sum_win_kernel's windows
-      // IGN_SUM_WINDOW: -1 auto, 0 off (one lane group per destination walks its messages in the
-      // GRU-step kernel), 1 windowed, 2 segmented for every destination.  Auto takes the segmented
+      // IGN_SUM_WINDOW: -1 auto, 0 off below 128 messages (one lane group per destination walks its
+      // messages in the GRU-step kernel), 1 windowed, 2 segmented for every destination.  Auto takes the segmented
       // sum (one wave per destination) for the destinations whose lane walk would be a long dependent
       // chain: >= 64 messages (seg_min_messages; Q-size's path -> node update, ~140 per node: 4.36-4.39
       // ms/step against 5.19 windowed and 5.51 lane-walk in round 4).  The rule reads each
@@ -1384,6 +1423,10 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       // orders), and the graph-resident forward takes the same order per row (resident.hip B1).
       const bool window = p->sum_window == 1;
       int64_t n_seg = 0;   // order is sorted by message count, descending: the segmented rows lead
+      if (p->sum_window == 0 && ND > 0 && ptr[1] - ptr[0] >= kSegMinMessages)   // (order: by count, descending)
+        return fail(IGN_ERR_UNSUPPORTED, "IGN_SUM_WINDOW=0 (every sum a lane walk): mp %d has a destination of %lld "
+                    "messages; a float32 chain of >= %lld terms leaves the fp32 class, so this switch is for batches "
+                    "below that", (int)mi, (long long)(ptr[1] - ptr[0]), (long long)kSegMinMessages);
       if (!window && !halo)
         while (n_seg < ND && ptr[n_seg + 1] - ptr[n_seg] >= seg_min_messages(p)) ++n_seg;
       const bool seg = n_seg > 0;
@@ -1889,7 +1932,8 @@ int readout(ign_plan* p, ign_batch* b) {
     if (!a.b1 || !a.b2) return fail(IGN_ERR_UNSUPPORTED, "fused readout requires use_bias on hidden layers");
     double flops = 2.0 * P * ((double)l1.in * l1.out + (double)l2.in * l2.out + l3.in);
     const bool bf = p->readout_variant >= 2 && l1.pk_bf >= 0 && l2.pk_bf >= 0;
-    const bool h16 = p->readout_variant == 4 && bf && l2.pk_h >= 0;
+    const bool h32 = p->readout_variant == 5 && bf && l2.pk_h32 >= 0;
+    const bool h16 = (p->readout_variant == 4 || (p->readout_variant == 5 && !h32)) && bf && l2.pk_h >= 0;
     const double tiles = (double)((P + 15) / 16);
     // per 16-row tile: layer 1 out/16 x in/32 and layer 2 out/16 x in/32 MFMAs of 16x16x32, x6 or x9
     // products (readout_bf); f32 (readout3): out/16 x in/4 each of 16x16x4
@@ -1898,9 +1942,11 @@ int readout(ign_plan* p, ign_batch* b) {
     // variant 4: both layers x3 (16x16x32 f16, the bf16 rate)
     const double kh = 3.0 * k1;
     tm.begin(K_READOUT, flops, (double)P * (4.0 * l1.in + 4.0),
-             h16 ? tiles * kh * kMfmaBf16Flops : bf ? tiles * k1 * 6 * kMfmaBf16Flops : 0,
+             h16 || h32 ? tiles * kh * kMfmaBf16Flops : bf ? tiles * k1 * 6 * kMfmaBf16Flops : 0,
              bf ? 0 : tiles * k1f * kMfmaF32Flops);
-    if (h16)
+    if (h32)   // variant 5: the same piece products on 32x32x16 (16-row-tile equivalent counted above)
+      HIP_TRY(launch_readout_h32(a, p->d_packed + l2.pk_h32, l1.in, st));
+    else if (h16)
       HIP_TRY(launch_readout_h16(a, p->d_packed + l2.pk_h, l1.in, st));
     else if (bf)
       HIP_TRY(launch_readout_bf(a, p->d_packed + l1.pk_bf, p->d_packed + l2.pk_bf, l1.in, 6, st));
@@ -1955,6 +2001,7 @@ extern "C++" int ign::resident_launch(ign_plan* p, ign_batch* b, const ResidentS
   r.lmsg_src = b->d_res_lmsg_src;
   r.lorder = b->d_res_lorder;
   r.lnseg = b->d_res_lnseg;
+  r.gorder = p->res_lpt ? b->d_res_gorder : nullptr;
   r.path_feat = b->d_feat[path];
   r.path_F = p->ents[path].feature_total;
   r.path_state = b->d_state[0][path];
@@ -1992,7 +2039,7 @@ extern "C++" int ign::resident_launch(ign_plan* p, ign_batch* b, const ResidentS
   const ign_resident_info_t& ri = b->res_info;
   Timer tm{p};
   tm.begin(K_RESIDENT, ri.flops, ri.bytes_stage, ri.mfma_bf16, ri.mfma_f32);
-  HIP_TRY(launch_resident_forward(r, b->G, save ? b->res_train_lds : b->res_lds, save ? b->res_train_form : b->res_form,
+  HIP_TRY(launch_resident_forward(r, b->res_graphs, save ? b->res_train_lds : b->res_lds, save ? b->res_train_form : b->res_form,
                                   save != nullptr, p->stream));
   tm.end();
   if (!save) {
@@ -2000,6 +2047,19 @@ extern "C++" int ign::resident_launch(ign_plan* p, ign_batch* b, const ResidentS
     for (int s = 0; s < sh.n_src; ++s) b->cur[sh.src_ent[s]] = 0;
   }
   return IGN_OK;
+}
+
+// IGN_RES_GROUP=K: K graphs per workgroup.  Auto (0): two where the all-LDS form of a single graph fits
+// twice (NSFNET x512: 0.248-0.257 -> 0.203-0.208 ms/step, r06_c07; GEANT2's path states need the
+// path-global form at two per workgroup, measured slower: 0.548 -> 0.570), else one
+static int resident_batch(ign_plan* p, ign_batch* b) {
+  if (p->res_group > 0) return resident_batch_k(p, b, p->res_group);
+  int rc = resident_batch_k(p, b, 1);
+  if (rc || !b->resident || b->res_form != IGN_RES_ALL_LDS || b->G < 2 || 2 * b->res_lds > kResidentMaxDynLds)
+    return rc;
+  b->resident = false;   // (the single-graph tables stay allocated until the batch goes)
+  if ((rc = resident_batch_k(p, b, 2)) || b->resident) return rc;
+  return resident_batch_k(p, b, 1);
 }
 
 // the batch's resident tables, built once (the first ign_forward or training forward)

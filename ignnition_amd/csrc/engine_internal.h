@@ -107,6 +107,7 @@ struct DenseP {
   int64_t pk_wt = -1;             // backward: A fragments of W [in][out] (row_gemm_t), if supported
   int64_t pk_bf = -1;             // fused readout: split-bf16 A fragments (readout variants 2/3)
   int64_t pk_h = -1;              // fused readout, layer 2: scaled split-fp16 fragments (readout variant 4)
+  int64_t pk_h32 = -1;            // ... the same pieces in variant 5's order (readout_h32.hip)
   int64_t pk_bfn = -1;            // training forward: split-bf16 pieces, natural k (dense_bf)
   int64_t pk_bft = -1;            // training backward: split-bf16 pieces of W^T (dense_bf_t)
   int64_t pk_hn = -1, pk_ht = -1;  // training: scaled split-fp16 pieces of W / W^T (dense_h16)
@@ -249,7 +250,9 @@ struct ign_plan {
   float* d_packed = nullptr;
   bool params_set = false;
   bool fused_readout = false;
-  int readout_variant = 4;        // fused readout: 4 = both layers on split-fp16 (3 products), 1 = f32
+  int readout_variant = 4;        // fused readout: 4 = both layers on split-fp16 (3 products) on 16x16x32 MFMAs
+                                  // (readout_h16), 5 = the same on 32x32x16 (readout_h32.hip, slower: DESIGN
+                                  // §3b), 1 = f32
                                   // MFMA (readout3), 2 = split-bf16 x6 (readout_bf); IGN_READOUT_VARIANT
   int ro_width = 0;
   int seq_variant = 6;            // ordered update: 6 = split-fp16 h.U with 3 piece products (H = 32,
@@ -272,9 +275,12 @@ struct ign_plan {
   bool resident_pg = true;        // ... with the path states in global memory where they do not fit LDS (IGN_RESIDENT_PG)
   bool resident_path_global = false;   // IGN_RESIDENT=2: that form for every eligible batch (tests)
   bool resident_train = true;     // the training forward on the resident form's SAVE variant (IGN_RESIDENT_TRAIN=0: off)
+  bool res_lpt = true;            // resident workgroups take their graphs longest first (IGN_RES_LPT=0: batch order)
+  int res_group = 0;              // consecutive graphs per resident workgroup (IGN_RES_GROUP; 0: auto, 1 or 2)
   bool resident_save_table = true;   // ... which also saves the ordered MP's tables (IGN_RESIDENT_SAVE_TABLE=0: recompute)
-  int sum_window = -1;            // windowed sum aggregation where eligible: 1 always, 0 never, -1 (default)
-                                  // for MPs with >= 64 messages per destination on average (IGN_SUM_WINDOW).
+  int sum_window = -1;            // IGN_SUM_WINDOW: 1 windowed sum aggregation where eligible; -1 (default)
+                                  // segmented for destinations of >= 64 messages, 0 of >= 128, 2 for all.
+                                  // (The windowed form:)
                                   // Measured 0.120 vs 0.112 ms (RouteNet link update, 37 messages per link);
                                   // Q-size x512 7.33 -> 6.44 ms/step with both sum MPs windowed
   // timing
@@ -321,6 +327,7 @@ struct ign_batch {
   bool res_tried = false;         // resident_batch ran (lazily, at the first ign_forward)
   size_t res_lds = 0;
   int res_form = 0;               // IGN_RES_ALL_LDS / IGN_RES_PATH_GLOBAL / IGN_RES_PATH_CSR_GLOBAL
+  int res_graphs = 0;             // resident workgroups per launch (graphs / IGN_RES_GROUP)
   ign_resident_info_t res_info{}; // per launch: bytes (compulsory, round trips, SURVEY B_stage), FLOPs,
                                   // MFMA FLOPs, tile-steps (ign_batch_resident_info)
   int64_t* d_res_path_off = nullptr;
@@ -333,6 +340,7 @@ struct ign_batch {
   uint16_t* d_res_lmsg_src = nullptr;
   uint16_t* d_res_lorder = nullptr;
   int32_t* d_res_lnseg = nullptr;
+  int32_t* d_res_gorder = nullptr;   // workgroup -> graph, by estimated cost, descending (IGN_RES_LPT)
   int32_t* d_res_lcode_off = nullptr;
   uint16_t* d_res_lcode = nullptr;
   int32_t* d_res_hsb = nullptr;   // per header: the training forward's hs_save row of the position

@@ -185,6 +185,7 @@ constexpr int kResidentTableStride = 100;   // LDS floats per 96-wide projected 
 constexpr size_t kResidentMaxDynLds = 144 * 1024;   // + ~14.5 KB static (U pieces, biases)
 enum { IGN_RES_ALL_LDS = 0, IGN_RES_PATH_GLOBAL = 1, IGN_RES_PATH_CSR_GLOBAL = 2 };   // kernel forms
 struct ResidentArgs {
+  const int32_t* gorder;      // [G] the graph of workgroup b (longest first; nullptr: b), round 6
   const int64_t* path_off;    // [G + 1] rows of the ordered MP's destination entity ("paths") per graph
   const int64_t* src_off[kResidentMaxSrc];   // [G + 1] rows of each source entity per graph
   const int64_t* urow_off;    // [G + 1] graph g's union rows start here (lmsg_ptr, lorder)
@@ -243,6 +244,13 @@ bool readout_bf_supported(int din, int n1, int n2, int act1, int act2);
 // header; floats 256 * 256 + 64 + IN1 * 256 + 64)
 hipError_t launch_readout_h16(const Readout3Args& args, const void* Wh, int din, hipStream_t st);
 hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
+                                   int n2, hipStream_t st);
+hipError_t launch_pack_readout_h16_header(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
+                                          int n2, hipStream_t st);
+// readout variant 5 (readout_h32.hip): variant 4's arithmetic class on v_mfma_f32_32x32x16_f16, k-outer
+// layer 2 (pack_readout_h32: the same buffer size and header positions as variant 4's)
+hipError_t launch_readout_h32(const Readout3Args& args, const void* Wh, int din, hipStream_t st);
+hipError_t launch_pack_readout_h32(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
                                    int n2, hipStream_t st);
 hipError_t launch_readout_bf(const Readout3Args& args, const void* W1f, const void* W2f, int din, int passes,
                              hipStream_t st);

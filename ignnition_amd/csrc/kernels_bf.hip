@@ -2097,6 +2097,14 @@ hipError_t launch_readout_h16(const Readout3Args& args, const void* Wh, int din,
   return hipGetLastError();
 }
 
+// the variant-4 / variant-5 headers alone (readout_h32.hip packs its own pieces)
+hipError_t launch_pack_readout_h16_header(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
+                                          int n2, hipStream_t st) {
+  hipLaunchKernelGGL(pack_readout_h16_kernel, dim3(1), dim3(1024), 0, st, W1, b1, W2, static_cast<uint16_t*>(out), in1,
+                     n1, n2);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_readout_h16(const float* W1, const float* b1, const float* W2, void* out, int in1, int n1,
                                    int n2, hipStream_t st) {
   if (n1 != 256 || n2 != 256 || in1 % 32) return hipErrorInvalidValue;

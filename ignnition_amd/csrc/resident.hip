@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * kW) void resident_forward_kernel(ResidentArgs 
   __shared__ float sbias[H];
   __shared__ int sctr[2];   // phase A's tile counters (alternate iterations)
   extern __shared__ float dyn[];
-  const int gph = blockIdx.x;
+  const int gph = a.gorder ? a.gorder[blockIdx.x] : (int)blockIdx.x;   // longest graphs first (LPT)
   const int64_t p0 = a.path_off[gph], P = a.path_off[gph + 1] - p0;
   const int64_t s00 = a.src_off[0][gph], L0 = a.src_off[0][gph + 1] - s00;
   const int64_t s10 = a.n_src > 1 ? a.src_off[1][gph] : 0;

@@ -713,7 +713,7 @@ int ign_forward_train_end(ign_plan* p, ign_batch* b, float* pred_out) {
   int in_stride = p->ro_width;
   // the inference readout kernel (readout_h16) with its activations written out: one launch, no
   // re-read of layer 1's output (readout.cpp's fused-readout conditions, variant 4)
-  const bool fused = p->train_fused_readout && p->fused_readout && p->readout_variant == 4 && p->dense.size() == 3 &&
+  const bool fused = p->train_fused_readout && p->fused_readout && p->readout_variant >= 4 && p->dense.size() == 3 &&
                      p->dense[1].pk_h >= 0 && p->dense[0].pk_bf >= 0 && p->dense[1].pk_bf >= 0 &&
                      p->dense[0].use_bias && p->dense[1].use_bias;
   if (fused) {
@@ -723,7 +723,10 @@ int ign_forward_train_end(ign_plan* p, ign_batch* b, float* pred_out) {
                    nullptr, p->d_params + l2.off_b,
                    p->d_params + l3.off_w, l3.use_bias ? p->d_params + l3.off_b : nullptr,
                    l1.act, l2.act, l3.act, b->d_pred, t->act[0], t->act[1]};
-    HIP_TRY(launch_readout_h16(a, p->d_packed + l2.pk_h, l1.in, st));
+    if (p->readout_variant == 5 && l2.pk_h32 >= 0)   // the inference kernel's variant (same predictions)
+      HIP_TRY(launch_readout_h32(a, p->d_packed + l2.pk_h32, l1.in, st));
+    else
+      HIP_TRY(launch_readout_h16(a, p->d_packed + l2.pk_h, l1.in, st));
   }
   for (size_t l = 0; !fused && l < p->dense.size(); ++l) {
     const DenseP& d = p->dense[l];
@@ -758,7 +761,9 @@ static int resident_train_forward(ign_plan* p, ign_batch* b, bool* done) {
   // sequence's first and final state rows unsaved (the path versions hold them): only under the
   // backward that recomputes those gates and reads neither row (the fused split-fp16 one; the unfused
   // one contracts every hs row)
-  if (!p->resident_train || !resident_sum_mps(p, sum_mp, &S) || train_seq_variant(p, 32) != 6) return IGN_OK;
+  // (the training form keeps its path states in global memory: IGN_RESIDENT_PG=0 turns it off too)
+  if (!p->resident_train || !p->resident_pg || !resident_sum_mps(p, sum_mp, &S) || train_seq_variant(p, 32) != 6)
+    return IGN_OK;
   int rc = resident_tables(p, b);
   if (rc || !b->resident) return rc;
   TrainState* t = b->train;
@@ -1078,7 +1083,8 @@ int ign_backward_mp(ign_plan* p, ign_batch* b) {
       SumBwdArgs a{mt.xs[rec.it], hin, p->d_packed + cp.pk_w, p->d_packed + cp.pk_u, p->d_packed + cp.pk_b,
                    p->d_packed + cp.pk_wt, p->d_packed + cp.pk_ut, dh_in, dh_out, t->dx, t->ga, t->gu, mb.n_dst};
       // plain sums at DIN = H = 32: dW / dU formed in the backward kernel, its partials into the
-      // deferred slots (IGN_SUM_BWD_FUSE=0: da / du written, then the two row contractions)
+      // deferred slots (IGN_SUM_BWD_FUSE=0: da / du written, then the two row contractions; with no
+      // deferred slot, IGN_DEFER_WGRAD=0, the unfused path runs whatever IGN_SUM_BWD_FUSE says)
       TrainState::DeferredGrad* dw = nullptr;
       TrainState::DeferredGrad* du = nullptr;
       const int64_t fw = mp.aggr == IGN_AGGR_SUM && p->sum_bwd_fuse ? sum_bwd_fused_waves(mb.n_dst, DIN, H) : 0;

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 11
+#define IGN_ABI_VERSION 12
 
 enum ign_status {
   IGN_OK = 0,
@@ -257,7 +257,7 @@ int  ign_batch_create(ign_plan* plan, const ign_batch_desc* desc, ign_batch** ou
 void ign_batch_destroy(ign_batch* batch);
 int  ign_batch_info(const ign_batch* batch, ign_batch_info_t* out);
 
-/* The graph-resident forward of a batch (ABI 11): decided by ign_batch_create (with
+/* The graph-resident forward of a batch (ABI 11, 12): decided by ign_batch_create (with
  * IGN_RESIDENT_EAGER=0 at the batch's first ign_forward or ign_forward_train, active = 0 before it),
  * with the per-launch cost model of its one launch.  The training forward (ign_forward_train) runs
  * the same form, saving what the backward reads (IGN_RESIDENT_TRAIN=0: per-MP launches). */
@@ -278,6 +278,9 @@ typedef struct {
   double  flops;                   /* executed FLOPs (fp32-equivalent) */
   double  mfma_bf16;               /* FLOPs issued on the 16-bit matrix pipe */
   double  mfma_f32;                /* ... on the f32 matrix pipe */
+  int32_t workgroups;              /* ABI 12: workgroups per launch (graphs / graphs_per_workgroup) */
+  int32_t graphs_per_workgroup;    /* ABI 12: consecutive graphs one workgroup runs as one disjoint union
+                                      (IGN_RES_GROUP; auto: 2 where a graph's all-LDS form fits twice) */
 } ign_resident_info_t;
 int  ign_batch_resident_info(const ign_batch* batch, ign_resident_info_t* out);
 

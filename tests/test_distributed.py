@@ -234,25 +234,26 @@ def test_bench_gpus_n_launches_n_ranks():
     assert len(lines) == 1 and not any(k.startswith("edge_cut") for k in lines[0])
 
 
-def test_bench_gpus_4_dry_run_partition_and_halo_symmetry():
-    """`bench.py --gpus 4 --dry-run`: four ranks, one line; the graph-sharded
-    RouteNet edges of all four shards; the edge-cut leg's four partitions add up to the whole graph's
-    in-edges, and the halo exchange is symmetric per rank pair (rows rank i reads from rank j = rows
-    j sends to i), with no rank reading its own rows."""
-    r, lines = _bench(["--gpus", "4", "--dry-run", "--topology", "nsfnet", "--graphs", "2", "--steps", "2",
-                       "--warmup", "1", "--edge-cut-nodes", "20000"])
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_gpus_n_dry_run_partition_and_halo_symmetry(n):
+    """`bench.py --gpus N --dry-run` for the driver's N = 4 and N = 8: N
+    ranks, one line; the graph-sharded RouteNet edges of all N shards; the edge-cut leg's N
+    partitions add up to the whole graph's in-edges, and the halo exchange is symmetric per rank
+    pair (rows rank i reads from rank j = rows j sends to i), with no rank reading its own rows."""
+    r, lines = _bench(["--gpus", str(n), "--dry-run", "--topology", "nsfnet", "--graphs", "2", "--steps", "2",
+                       "--warmup", "1", "--edge-cut-nodes", "20000"], timeout=400)
     assert r.returncode == 0, r.stderr[-2000:]
     assert len(lines) == 1, r.stdout
     line = lines[0]
-    assert line["n_gpus"] == 4
-    _, _, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 8)
+    assert line["n_gpus"] == n
+    _, _, mi, graphs, _ = workloads.make_batch_inputs("routenet", "nsfnet", 2 * n)
     assert line["config"]["edges_per_step_total"] == workloads.edges_per_forward(mi, graphs)
     ec = line["edge_cut_20000n"]
-    assert ec["n_ranks"] == 4 and ec["edges_match_whole_graph"]
+    assert ec["n_ranks"] == n and ec["edges_match_whole_graph"]
     assert ec["halo_symmetric"], (ec["halo_recv_by_pair"], ec["halo_send_by_pair"])
     recv = np.asarray(ec["halo_recv_by_pair"])
-    assert recv.shape == (4, 4) and np.all(np.diag(recv) == 0) and recv.sum() == ec["halo_rows"]["total"] > 0
-    assert (recv > 0).sum() >= 6   # the 10 % uniform sources reach beyond the neighbouring ranges
+    assert recv.shape == (n, n) and np.all(np.diag(recv) == 0) and recv.sum() == ec["halo_rows"]["total"] > 0
+    assert (recv > 0).sum() >= n * (n - 1) // 2   # the 10 % uniform sources reach beyond the neighbouring ranges
 
 
 def test_bench_single_rank_dry_run_and_world_mismatch():

@@ -8,9 +8,9 @@ cd "$(dirname "$0")/.."
 python -m ignnition_amd.build > /dev/null
 mkdir -p ignnition_amd/ab/obj_$NAME
 pids=""
-for SRC in kernels.hip kernels_bf.hip train_kernels.hip readout_kernels.hip resident.hip; do
+for SRC in kernels.hip kernels_bf.hip train_kernels.hip readout_kernels.hip resident.hip readout_h32.hip; do
   EXTRA=""
-  { [ "$SRC" = kernels_bf.hip ] || [ "$SRC" = resident.hip ]; } && EXTRA="-mllvm -amdgpu-mfma-vgpr-form"
+  { [ "$SRC" = kernels_bf.hip ] || [ "$SRC" = resident.hip ] || [ "$SRC" = readout_h32.hip ]; } && EXTRA="-mllvm -amdgpu-mfma-vgpr-form"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value $EXTRA $DEFS \
     -c ignnition_amd/csrc/$SRC -o ignnition_amd/ab/obj_$NAME/$SRC.o &
   pids="$pids $!"
