@@ -579,17 +579,19 @@ def main():
     barrier_sync()
     dt = time.perf_counter() - t0
     stats = stats_all()
-    isolated = None
+    isolated = isolated_all = None
     if len(subs) > 1 and not args.no_timing and not args.train:
         # isolated leg, after the timed region: sub-batch 0 alone on the chip, its dominant kernel's
-        # launches timed (in the timed region the sub-batches' kernels co-run, so there a launch's
-        # duration is its share of a chip it does not have to itself)
+        # and the readout's launches timed (in the timed region the sub-batches' kernels co-run, so
+        # there a launch's duration is its share of a chip it does not have to itself)
         set_timing(False)
-        engines[0].set_timing(True, kinds=[dom])
+        kinds = [dom] + (["readout"] if dom != "readout" else [])
+        engines[0].set_timing(True, kinds=kinds)
         for _ in range(3):
             subs[0].forward(to_host=False)
         engines[0].synchronize()
-        isolated = engines[0].stats()[dom]
+        isolated_all = engines[0].stats()
+        isolated = isolated_all[dom]
     for fn in cleanup:
         fn()
     dev = None
@@ -685,6 +687,8 @@ def main():
                             "mfma_pipe": pipe(isolated)}
     if roof is not None and dom == "mp_resident":
         roof.update(resident_roof(batches, roof, isolated))
+    if roof is not None and isolated_all is not None:
+        roof.update(step_account(isolated_all, dom, len(subs), dt / args.steps * 1e3, pipe))
     if roof is not None:
         roof["contraction"] = contraction[{"seq_gru": "ordered_update_hU", "readout": "readout",
                                            "mp_resident": "mp_resident"}.get(dom, "sum_update")]
@@ -724,6 +728,32 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def step_account(iso, dom, parts, ms_step, pipe):
+    """the step's kernels timed alone (sub-batch 0 on an idle chip, after the timed
+    region) against the measured step: the readout's launch time and its 16-bit pipe fraction, and
+    the sum of every sub-batch's isolated dominant + readout launches beside ms_per_step (the
+    difference is what co-running the sub-batches hides, or loses)."""
+    out = {}
+    ro = iso.get("readout")
+    per = {}
+    for k in (dom, "readout"):
+        v = iso.get(k)
+        if v and v["launches"]:
+            per[k] = v["ms"] / v["launches"]
+    if ro and ro["launches"]:
+        out["readout_isolated"] = {"avg_launch_ms": round(per["readout"], 4), "launches": ro["launches"],
+                                   "mfma_pipe": pipe(ro),
+                                   "what": "sub-batch 0's readout (fused Dense 256 -> 256 -> 1) alone on the chip"}
+    if per:
+        total = parts * sum(per.values())
+        out["step_account"] = {"what": "every sub-batch's isolated launches summed, against ms_per_step",
+                               "sub_batches": parts,
+                               "per_sub_batch_ms": {k: round(v, 4) for k, v in per.items()},
+                               "sum_isolated_ms": round(total, 4), "ms_per_step": round(ms_step, 4),
+                               "co_run_gain_ms": round(total - ms_step, 4)}
+    return out
 
 
 def resident_roof(batches, roof, isolated):

@@ -315,6 +315,14 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float z, rr, c, uh;
+#ifdef IGN_BWD_ABL_NOGATE   // timing-only ablation (wrong gradients): no transcendental gate recompute
+          if constexpr (H16) {
+            z = fmaf(az[t][r], cS, x[0][t][r]);
+            rr = fmaf(ar[t][r], cS, x[1][t][r]);
+            c = fmaf(rr, ah[t][r], x[2][t][r]);
+            uh = ah[t][r] * cS * kInv2Log2e;
+          } else
+#endif
           if constexpr (H16) {   // seq_gru_h16's gate arithmetic on the scaled accumulators
             z = rcpf_(1.0f + __builtin_amdgcn_exp2f(fmaf(az[t][r], cS, x[0][t][r])));
             const float rc = rcpf_(fmaf(__builtin_amdgcn_exp2f(fmaf(ar[t][r], cS, x[1][t][r])), SS, SS));
@@ -347,7 +355,9 @@ __global__ __launch_bounds__(256, 2) void seq_gru_bwd_kernel(SeqBwdArgs a) {
 #pragma unroll
         for (int mt = 0; mt < NT; ++mt) af[mt] = ld4(R + mt * 256 + rofs);
       }
+#ifndef IGN_BWD_ABL_NOLOAD   // timing-only ablation (wrong gradients): every step reuses the first step's rows
       if (step > 0) load_rows(hbase + (step - 1 < L ? step - 1 : 0), code_next);
+#endif
       // FUSE: every lane stores, so no branch skips the stores and the step's closing wait for the
       // prefetched rows can leave them in flight (a conditional store block made the compiler merge
       // its two paths into vmcnt(0): each step waited for its ga stores to reach memory).  A lane past
