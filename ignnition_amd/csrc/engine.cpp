@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
@@ -27,6 +28,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ignmp.h"
@@ -216,6 +218,27 @@ int act_ok(int a) { return a >= IGN_ACT_LINEAR && a <= IGN_ACT_TANH; }
 // equal length; the longest sequences start first).  Measured faster than per-graph orders with
 // XCD-aware tiles for both the ordered and the sum updates (profiles/r02/seq_experiments).  A
 // counting sort (counts are small): O(n), the same order as std::stable_sort.
+// f(lo, hi) over [0, n) in contiguous chunks on up to IGN_BUILD_THREADS threads (default 2: a
+// training loop already runs several builders), at least min_per items each; the caller's thread
+// takes the first chunk
+template <class F>
+void parallel_ranges(int64_t n, int64_t min_per, F&& f) {
+  static const int T = [] {
+    const char* v = std::getenv("IGN_BUILD_THREADS");
+    return v && *v ? std::max(1, std::atoi(v)) : 2;
+  }();
+  const int nt = (int)std::min<int64_t>(T, std::max<int64_t>(1, n / std::max<int64_t>(1, min_per)));
+  if (nt <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (int t = 1; t < nt; ++t) th.emplace_back([&f, n, nt, t] { f(n * t / nt, n * (t + 1) / nt); });
+  f(0, n / nt);
+  for (auto& x : th) x.join();
+}
+
 void sort_order(hvec<int32_t>& order, const hvec<int64_t>& cnt) {
   const int64_t n = (int64_t)order.size();
   int64_t mx = 0;
@@ -849,56 +872,90 @@ static int resident_batch_k(ign_plan* p, ign_batch* b, int K) {
   // ordered MP: each graph's positions in the batch's length-sorted order (stable, so still sorted
   // by length, descending), padded to whole tiles; their step codes as local union rows (U_g: the
   // hole), then max_len + 8 hole codes (the tile loop reads codes past a row's end)
-  std::vector<std::vector<int32_t>> pp(G);
+  // (positions by graph: a counting sort keyed by a row -> graph table, the batch order kept)
   const int64_t ND = (int64_t)ma.h_order.size();
-  for (int64_t i = 0; i < ND; ++i) pp[graph_of(po, ma.h_order[i])].push_back((int32_t)i);
-  hvec<int32_t> ptile_off(G + 1, 0), hdr, hsb, lcode_off(G + 1, 0);
-  double tile_steps = 0;
-  hvec<uint16_t> lcode;
-  size_t lds[3] = {0, 0, 0};
-  for (int g = 0; g < G; ++g) {
-    const int64_t U = uo[g + 1] - uo[g];
-    const int64_t n = (int64_t)pp[g].size(), np = (n + 15) / 16 * 16;
-    const size_t c0 = lcode.size();
-    int32_t maxl = 0;
-    for (int64_t k = 0; k < n; ++k) {
-      const int64_t i = pp[g][k];
-      const int32_t len = ma.h_len[i], sp = ma.h_step_ptr[i];
-      hdr.push_back((int32_t)(ma.h_order[i] - po[g]));
-      hdr.push_back(len);
-      hsb.push_back(sp + (int32_t)i);   // the training forward's hs_save rows of position i
-      hdr.push_back((int32_t)(lcode.size() - c0));
-      for (int32_t t = 0; t < len; ++t) {
-        const uint32_t c = ma.h_step_code[sp + t];
-        uint16_t code = (uint16_t)U;   // the zero row: a hole
-        if (c < (uint32_t)ma.zero_row) {
-          const int s = S > 1 && (int64_t)c >= ma.src_off[1] ? 1 : 0;
-          const int64_t lr = (int64_t)c - ma.src_off[s] - (*so[s])[g];
-          if (lr < 0 || lr >= Ls(s, g)) return IGN_OK;   // another graph's row: not resident
-          code = (uint16_t)((s ? Ls(0, g) : 0) + lr);
-        } else if (c != (uint32_t)ma.zero_row) {
-          return IGN_OK;   // a multi-message row (n_multi == 0: unreachable)
-        }
-        lcode.push_back(code);
-      }
-      hdr.push_back(len > 0 ? lcode[c0 + hdr[hdr.size() - 1]] : (int32_t)U);
-      maxl = std::max(maxl, len);
-    }
-    const int32_t pad = (int32_t)(lcode.size() - c0);
-    lcode.insert(lcode.end(), (size_t)maxl + 8, (uint16_t)U);
-    for (int64_t k = n; k < np; ++k) {   // padding: row -1, length 0, hole codes, hs_save's pad row (unwritten)
-      hsb.push_back((int32_t)(ma.n_steps + ND));
-      hdr.push_back(-1);
-      hdr.push_back(0);
-      hdr.push_back(pad);
-      hdr.push_back((int32_t)U);
-    }
-    ptile_off[g + 1] = ptile_off[g] + (int32_t)np;
-    for (int64_t k = 0; k < n; k += 16) tile_steps += ma.h_len[pp[g][k]];   // a tile's first row is its longest
-    lcode_off[g + 1] = (int32_t)lcode.size();
-    for (int f = 0; f < 3; ++f)
-      lds[f] = std::max(lds[f], resident_lds_bytes(po[g + 1] - po[g], U, nmsg[g], lcode_off[g + 1] - lcode_off[g], f));
+  hvec<int32_t> pstart(G + 1, 0), plist(std::max<int64_t>(ND, 1));
+  {
+    hvec<int32_t> gid(std::max<int64_t>(po[G], 1));
+    for (int g = 0; g < G; ++g)
+      for (int64_t r = po[g]; r < po[g + 1]; ++r) gid[r] = g;
+    for (int64_t i = 0; i < ND; ++i) pstart[gid[ma.h_order[i]] + 1]++;
+    for (int g = 0; g < G; ++g) pstart[g + 1] += pstart[g];
+    hvec<int32_t> fill(pstart.begin(), pstart.end() - 1);
+    for (int64_t i = 0; i < ND; ++i) plist[fill[gid[ma.h_order[i]]]++] = (int32_t)i;
   }
+  // two passes over the graphs, the second on IGN_BUILD_THREADS threads (the tables are ~10^7
+  // entries for 512 synth50 graphs, ~20 ms on one builder thread): each graph's sizes, their
+  // prefix sums, then every graph fills its own ranges
+  std::vector<int64_t> npad(G), ncode(G), maxl_g(G, 0);
+  hvec<int32_t> ptile_off(G + 1, 0), lcode_off(G + 1, 0);
+  double tile_steps = 0;
+  for (int g = 0; g < G; ++g) {
+    const int64_t n = pstart[g + 1] - pstart[g];
+    npad[g] = (n + 15) / 16 * 16;
+    int64_t codes = 0, maxl = 0;
+    for (int64_t k = pstart[g]; k < pstart[g + 1]; ++k) {
+      const int32_t len = ma.h_len[plist[k]];
+      codes += len;
+      maxl = std::max<int64_t>(maxl, len);
+    }
+    for (int64_t k = pstart[g]; k < pstart[g + 1]; k += 16) tile_steps += ma.h_len[plist[k]];   // a tile's first row is its longest
+    maxl_g[g] = maxl;
+    ncode[g] = codes + maxl + 8;
+    ptile_off[g + 1] = ptile_off[g] + (int32_t)npad[g];
+    if ((int64_t)lcode_off[g] + ncode[g] >= INT32_MAX) return IGN_OK;
+    lcode_off[g + 1] = lcode_off[g] + (int32_t)ncode[g];
+  }
+  hvec<int32_t> hdr((size_t)4 * ptile_off[G]), hsb((size_t)ptile_off[G]);
+  hvec<uint16_t> lcode((size_t)lcode_off[G]);
+  std::atomic<bool> foreign{false};   // a code of another graph's row or a multi-message row: not resident
+  parallel_ranges(G, 16, [&](int64_t g0, int64_t g1) {
+    for (int64_t g = g0; g < g1 && !foreign.load(std::memory_order_relaxed); ++g) {
+      const int64_t U = uo[g + 1] - uo[g];
+      int32_t* h = hdr.data() + (size_t)4 * ptile_off[g];
+      int32_t* hs = hsb.data() + ptile_off[g];
+      uint16_t* lc = lcode.data() + lcode_off[g];
+      int32_t c = 0;   // the graph's next local code
+      for (int64_t k = pstart[g]; k < pstart[g + 1]; ++k) {
+        const int64_t i = plist[k];
+        const int32_t len = ma.h_len[i], sp = ma.h_step_ptr[i];
+        *h++ = (int32_t)(ma.h_order[i] - po[g]);
+        *h++ = len;
+        *hs++ = sp + (int32_t)i;   // the training forward's hs_save rows of position i
+        *h++ = c;
+        const int32_t c_first = c;
+        for (int32_t t = 0; t < len; ++t) {
+          const uint32_t cd = ma.h_step_code[sp + t];
+          uint16_t code = (uint16_t)U;   // the zero row: a hole
+          if (cd < (uint32_t)ma.zero_row) {
+            const int s = S > 1 && (int64_t)cd >= ma.src_off[1] ? 1 : 0;
+            const int64_t lr = (int64_t)cd - ma.src_off[s] - (*so[s])[g];
+            if (lr < 0 || lr >= Ls(s, (int)g)) { foreign = true; return; }
+            code = (uint16_t)((s ? Ls(0, (int)g) : 0) + lr);
+          } else if (cd != (uint32_t)ma.zero_row) {
+            foreign = true;   // a multi-message row (n_multi == 0: unreachable)
+            return;
+          }
+          lc[c++] = code;
+        }
+        *h++ = len > 0 ? lc[c_first] : (int32_t)U;
+      }
+      const int32_t pad = c;
+      for (int64_t q = 0; q < maxl_g[g] + 8; ++q) lc[c++] = (uint16_t)U;
+      for (int64_t k = pstart[g + 1] - pstart[g]; k < npad[g]; ++k) {   // padding: row -1, length 0, hole codes, hs_save's pad row (unwritten)
+        *hs++ = (int32_t)(ma.n_steps + ND);
+        *h++ = -1;
+        *h++ = 0;
+        *h++ = pad;
+        *h++ = (int32_t)U;
+      }
+    }
+  });
+  if (foreign) return IGN_OK;
+  size_t lds[3] = {0, 0, 0};
+  for (int g = 0; g < G; ++g)
+    for (int f = 0; f < 3; ++f)
+      lds[f] = std::max(lds[f], resident_lds_bytes(po[g + 1] - po[g], uo[g + 1] - uo[g], nmsg[g], ncode[g], f));
   // the workgroups' graphs, longest first (round 6): a launch of more graphs than CUs -- or the second
   // of two sub-batch launches, whose workgroups take the CUs the first one frees -- is a list
   // schedule in workgroup order, so longest-first is LPT.  The estimate, in cycles of one workgroup:
@@ -908,7 +965,7 @@ static int resident_batch_k(ign_plan* p, ign_batch* b, int K) {
     std::vector<double> cost(G, 0.0);
     for (int g = 0; g < G; ++g) {
       double ts = 0;
-      for (size_t k = 0; k < pp[g].size(); k += 16) ts += ma.h_len[pp[g][k]];
+      for (int64_t k = pstart[g]; k < pstart[g + 1]; k += 16) ts += ma.h_len[plist[k]];
       cost[g] = ts * 325.0 + (double)nmsg[g] * 6.0;
     }
     std::iota(gorder.begin(), gorder.end(), 0);
@@ -1064,7 +1121,11 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   }
 
   // per-MP CSR / step tables
+  static const bool build_prof = env_flag("IGN_BUILD_PROF", false);
+  std::vector<double> t_mp;   // IGN_BUILD_PROF: the time up to the end of each MP's tables
+  const double t_mp0 = build_prof ? now_ms() : 0.0;
   for (size_t mi = 0; mi < p->mps.size(); ++mi) {
+    if (build_prof && mi > 0) t_mp.push_back(now_ms());
     const MPP& mp = p->mps[mi];
     const int S = (int)mp.src.size();
     const int dst = mp.dst;
@@ -1526,7 +1587,18 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   // the resident tables here, on the building thread, not at the first forward: a training loop's
   // builders run ahead of the step, and the step's thread would otherwise build them inside the step
   // (fresh 512 x synth50 batches: 28 -> 56 ms per step once the training forward went resident)
+  const double t_res0 = build_prof ? now_ms() : 0.0;
   if (env_flag("IGN_RESIDENT_EAGER", true) && (rc = resident_tables(p, b.get()))) return rc;
+  if (build_prof) {
+    std::string s;
+    double prev = t_mp0;
+    for (size_t i = 0; i < t_mp.size(); ++i) {
+      s += " mp" + std::to_string(i) + " " + std::to_string(t_mp[i] - prev).substr(0, 6);
+      prev = t_mp[i];
+    }
+    fprintf(stderr, "[ign-build] batch sections:%s mp%zu+readout %.2f, resident tables %.2f ms\n", s.c_str(),
+            t_mp.size(), t_res0 - prev, now_ms() - t_res0);
+  }
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // every clear has landed before the batch is used
   HIP_TRY(upload_flush());                           // (and every staged copy)
   *out = b.release();

@@ -278,8 +278,11 @@ def train_and_evaluate(model, dist=None, device: int = 0, log_every: int = 10):
     # the next batches are read and built on worker threads while the GPU runs the current step
     try:
         for step in range(1, train_steps + 1):
-            out = trainer.train_prepared(*next(prepared))
-            if rank == 0 and (step % log_every == 0 or step == 1):
+            logged = step % log_every == 0 or step == 1
+            # the loss reaches the host only on the logged steps: the others are enqueued without a
+            # wait, so the next batch's host work overlaps this step on the GPU
+            out = trainer.train_prepared(*next(prepared), want_loss=logged)
+            if rank == 0 and logged:
                 log.warning("IGNNITION: step %d  Loss %.6g  Regularization loss %.6g  Total loss %.6g", step,
                             out["loss"], out["regularization_loss"], out["total_loss"])
             if time.time() - last_save >= save_secs:

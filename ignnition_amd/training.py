@@ -123,18 +123,25 @@ class Trainer:
         """One optimizer step on a batch of graphs (model_fn TRAIN, GM:712-830)."""
         return self.train_prepared(*self.prepare(features, labels))
 
-    def train_prepared(self, b, y) -> dict:
-        """One optimizer step on a batch made by ``prepare`` (closed here)."""
+    def train_prepared(self, b, y, want_loss: bool = True) -> dict:
+        """One optimizer step on a batch made by ``prepare`` (closed here).  ``want_loss=False``: the
+        step is only enqueued -- no host wait for the loss or the regularisation term (the returned
+        dict has None for them), so the next step's host work overlaps this one on the GPU; the
+        training loop asks for them on the steps it logs (tf.estimator computes the loss every step
+        but only the logged steps reach the host)."""
         prof = self.step_prof
         tick = time.perf_counter if prof is not None else None
         t0 = tick() if tick else 0.0
+        # y was made on a builder's stream: without a host wait in this step, its memory must not
+        # return to that stream's pool before the step has read it
+        y.record_stream(self.torch.cuda.current_stream(y.device))
         try:
             b.forward_train(to_host=False)
             if tick:
                 t1 = tick()
                 prof["forward_enqueue"] += t1 - t0
             dpred = self.torch.empty_like(y)
-            loss = self.engine.mse_loss(b.predictions_ptr(), y, dpred)
+            loss = self.engine.mse_loss(b.predictions_ptr(), y, dpred, want_loss=want_loss)
             if tick:
                 t2 = tick()
                 prof["loss_wait"] += t2 - t1
@@ -160,12 +167,12 @@ class Trainer:
             if tick:
                 t5 = tick()
                 prof["close"] += t5 - t4
-        reg = self.engine.l2_loss()
+        reg = self.engine.l2_loss() if want_loss else None
         if tick:
             prof["l2_wait"] += tick() - t5
             prof["steps"] += 1
-        return {"loss": loss, "regularization_loss": reg, "total_loss": loss + reg, "learning_rate": lr,
-                "step": self.iterations}
+        return {"loss": loss, "regularization_loss": reg, "total_loss": loss + reg if want_loss else None,
+                "learning_rate": lr, "step": self.iterations}
 
     def _denorm(self, v):
         if self.output_denorm is None or str(self.output_denorm) == "None":
@@ -268,6 +275,9 @@ class BatchPrefetcher:
                     raise job
                 features, labels = self.load(job) if self.load is not None else job
                 res = self.trainer.prepare(features, labels)
+                # the gathered arrays are copied into the batch: drop them now, so that the native
+                # reader's buffers go back to its pool before this worker's next gather
+                del features, labels
             except BaseException as e:   # handed to the consumer
                 res = e
             with self.cv:

@@ -141,6 +141,37 @@ def test_concurrent_batches_equal_serial(tmp_path):
     ds.close()
 
 
+def test_recycled_gather_buffers_equal_fresh(tmp_path, monkeypatch):
+    """Destroyed batches hand their concatenation buffers back to the dataset's pool; batches of
+    other sizes and orders gathered into them (larger, smaller, repeated) hold exactly what an
+    unpooled dataset (IGN_GATHER_POOL=0) gathers, and a batch may outlive its dataset's handle."""
+    import gc
+    desc, dims, mi = workloads.model("qsize")
+    synthetic.write_tar_dataset(synthetic.dataset("nsfnet", 12, qsize=True), str(tmp_path), per_file=5)
+    pooled = NativeDataset.for_model(str(tmp_path), mi)
+    monkeypatch.setenv("IGN_GATHER_POOL", "0")
+    fresh = NativeDataset.for_model(str(tmp_path), mi)
+    keys = plan_keys(MPPlan.from_model_info(mi))
+    rng = np.random.default_rng(3)
+    for size in (3, 12, 2, 7, 12, 1, 5):
+        ids = rng.choice(12, size=size, replace=False)
+        a, ya = pooled.batch(ids, keys)
+        b, yb = fresh.batch(ids, keys)
+        np.testing.assert_array_equal(ya[0], yb[0])
+        for k in keys:
+            np.testing.assert_array_equal(a.get(k)[0], b.get(k)[0])
+            np.testing.assert_array_equal(a.get(k)[1], b.get(k)[1])
+        del a, b
+        gc.collect()
+    last, _ = pooled.batch([4, 0, 9], keys)
+    pooled.close()
+    fresh.close()
+    ref = {k: np.array(last.get(k)[0]) for k in keys}
+    del last   # destroyed after the dataset: its buffers go to the pool the batch still holds
+    gc.collect()
+    assert all(v.size for v in ref.values())
+
+
 class _FakeBatch:
     def __init__(self, v):
         self.v, self.closed = v, False
