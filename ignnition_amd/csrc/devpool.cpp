@@ -13,8 +13,10 @@
 // reads batch scratch it has not written (tests/test_gpu_parity.py).  The idle bytes are capped per
 // device across every pool of the process (one per plan: bench's sub-batch engines, a trainer's eval
 // engine): IGN_POOL_CACHE_GB, default half the device memory free when the first pool was created;
-// ign_plan_trim_cache releases a plan's.  When hipMalloc runs out of memory, every pool of the device
-// gives its idle blocks back before the retry, not only the allocating plan's.
+// ign_plan_trim_cache releases a plan's.  The cache is trimmed to the cap by the allocating threads
+// (a training loop's batch builders), never by a release: hipFree waits for the device, and a
+// release is the training step's own Batch.close.  When hipMalloc runs out of memory, every pool of
+// the device gives its idle blocks back before the retry, not only the allocating plan's.
 //
 // The host side has the same problem: the batch builders' index tables are ~10^8 bytes of host
 // memory per batch.  hvec (engine_internal.h) draws blocks >= 1 MiB from a process-wide cache
@@ -24,6 +26,7 @@
 #include <sys/mman.h>
 
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -144,8 +147,10 @@ std::shared_ptr<DevPool> pool_create(int device) {
     // the device's cap, once: half its memory free now (round 5 kept half the TOTAL memory per pool,
     // so several plans could together cache more than the device has).  A training batch of 512 x
     // synth50 holds ~11 GB of device blocks and the input pipeline keeps workers + 1 of them in
-    // flight; under a 16 GB cap every release trimmed blocks with hipFree -- which waits for the
-    // device -- under the pool lock the step's own release then waited for (22 -> 57 ms per step)
+    // flight.  Under a 16 GB cap every release trimmed blocks with hipFree -- which waits for the
+    // device -- in the step's own Batch.close (22 -> 57 ms per step, round 5); a quarter of the free
+    // memory still did once the cache had filled (close 17 ms per step at 8 input workers, 62 at 12,
+    // r06_c15).  Releases no longer trim (pool_alloc does)
     DeviceBudget& b = reg.budgets[device];
     const int gb = env_int("IGN_POOL_CACHE_GB", -1);
     size_t free_b = 0, total_b = 0;
@@ -207,30 +212,52 @@ hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch) {
   }
   const size_t cls = size_class(bytes);
   {
+    // a ready block of this size class or of the next two (<= 1.5x the request): batches of one
+    // workload differ a little in size, and blocks stranded one class up would fill the cache
     std::lock_guard<std::mutex> g(pool->mu);
-    auto it = pool->idle.find(cls);
-    if (it != pool->idle.end()) {
+    auto it = pool->idle.lower_bound(cls);
+    for (int tried = 0; !*out && it != pool->idle.end() && tried < 3 && it->first * 2 <= cls * 3; ++tried) {
       auto& v = it->second;
       for (size_t i = 0; i < v.size(); ++i)
         if (v[i].fence->ready()) {
           *out = v[i].ptr;
           v.erase(v.begin() + i);
-          if (v.empty()) pool->idle.erase(it);
-          pool->sub_idle(cls);
-          pool->live[*out] = cls;
+          pool->sub_idle(it->first);
+          pool->live[*out] = it->first;
           break;
         }
+      it = v.empty() ? pool->idle.erase(it) : std::next(it);
     }
   }
   if (!*out) {
     hipError_t e = hipMalloc(out, cls);
-    if (e == hipErrorOutOfMemory) {   // give back every idle block of the device (waiting for in-flight ones), retry
+    // out of memory: give back the device's idle blocks and retry -- first those whose fence has
+    // completed, then (still short) every one, waiting for the in-flight fences.  The blocks are freed
+    // after the lock is dropped: the step's own release takes this lock, and hipFree / the fence waits
+    // under it stalled the step for the whole trim (10-12 ms per step with 10-12 input workers, r06_c11)
+    for (int pass = 0; e == hipErrorOutOfMemory && pass < 2; ++pass) {
       (void)hipGetLastError();
+      static const bool prof = env_int("IGN_BUILD_PROF", 0) != 0;
+      if (prof)
+        fprintf(stderr, "[ign-pool] out of memory for a %.1f MB block: trimming the device's idle blocks (%s)\n",
+                cls / 1048576.0, pass ? "waiting for in-flight ones" : "completed ones");
+      std::vector<void*> victims;
+      if (pass == 1) {   // the in-flight fences, waited for outside the lock
+        std::vector<std::shared_ptr<Fence>> fences;
+        {
+          std::lock_guard<std::mutex> g(pool->mu);
+          for (auto& kv : pool->idle)
+            for (auto& b : kv.second)
+              if (!b.fence->done && b.fence->ev) fences.push_back(b.fence);
+        }
+        for (auto& f : fences) hipEventSynchronize(f->ev);
+      }
       {
         std::lock_guard<std::mutex> g(pool->mu);
-        pool->trim(0, true);
+        pool->trim(0, false, &victims);
       }
-      trim_device(pool, 0, true);
+      for (void* v : victims) hipFree(v);
+      trim_device(pool, 0, pass == 1);
       e = hipMalloc(out, cls);
     }
     if (e != hipSuccess) {
@@ -239,6 +266,18 @@ hipError_t pool_alloc(DevPool* pool, void** out, size_t bytes, bool scratch) {
     }
     std::lock_guard<std::mutex> g(pool->mu);
     pool->live[*out] = cls;
+  }
+  // over the device's budget: this pool's own idle blocks first, then the other pools' (completed
+  // fences only; freed here, on the allocating thread, outside the lock)
+  if (pool->budget->idle.load() > (int64_t)pool->budget->cap) {
+    std::vector<void*> victims;
+    {
+      std::lock_guard<std::mutex> g(pool->mu);
+      const int64_t excess = pool->budget->idle.load() - (int64_t)pool->budget->cap;
+      if (excess > 0) pool->trim(pool->idle_bytes > (size_t)excess ? pool->idle_bytes - (size_t)excess : 0, false, &victims);
+    }
+    for (void* v : victims) hipFree(v);
+    if (pool->budget->idle.load() > (int64_t)pool->budget->cap) trim_device(pool, pool->budget->cap, false);
   }
   if (scratch && pool->poison) return hipMemsetAsync(*out, 0xFF, bytes, upload_stream());
   return hipSuccess;
@@ -258,7 +297,6 @@ void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t a
     fence->ev = nullptr;
     if (after) hipStreamSynchronize(after);
   }
-  std::vector<void*> victims;
   {
     std::lock_guard<std::mutex> g(pool->mu);
     for (void* b : blocks) {
@@ -269,12 +307,7 @@ void pool_release(DevPool* pool, const std::vector<void*>& blocks, hipStream_t a
       pool->idle[cls].push_back({b, fence});
       pool->add_idle(cls);
     }
-    // over the device's budget: this pool's own idle blocks first, then the other pools'
-    const int64_t excess = pool->budget->idle.load() - (int64_t)pool->budget->cap;
-    if (excess > 0) pool->trim(pool->idle_bytes > (size_t)excess ? pool->idle_bytes - (size_t)excess : 0, false, &victims);
   }
-  for (void* v : victims) hipFree(v);
-  if (pool->budget->idle.load() > (int64_t)pool->budget->cap) trim_device(pool, pool->budget->cap, false);
 }
 
 // ---- host blocks ----------------------------------------------------------------------------
