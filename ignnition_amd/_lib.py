@@ -59,7 +59,8 @@ class BatchDesc(C.Structure):
                 ("adj_edges", C.POINTER(i64)), ("adj_src", C.POINTER(C.POINTER(i64))),
                 ("adj_dst", C.POINTER(C.POINTER(i64))), ("adj_seq", C.POINTER(C.POINTER(i64))),
                 ("interleave_len", C.POINTER(i64)), ("interleave_idx", C.POINTER(C.POINTER(i64))),
-                ("halo_rows", C.POINTER(i64)), ("adj_params", C.POINTER(C.POINTER(f32)))]
+                ("halo_rows", C.POINTER(i64)), ("adj_params", C.POINTER(C.POINTER(f32))),
+                ("index_bytes", i32)]   # ABI 13: 0/8 int64 index arrays, 4 int32
 
 
 class DatasetDesc(C.Structure):
@@ -107,11 +108,11 @@ SYMBOLS = ["ign_abi_version", "ign_last_error", "ign_device_count", "ign_plan_cr
            "ign_batch_enable_training", "ign_forward_train", "ign_backward", "ign_mse_loss", "ign_l2_loss",
            "ign_adam_step", "ign_plan_get_params", "ign_dataset_open", "ign_dataset_close", "ign_dataset_size",
            "ign_dataset_error", "ign_dataset_gather", "ign_dataset_get", "ign_dataset_batch_create",
-           "ign_dataset_batch_get", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json", "ign_forward_train_begin", "ign_forward_train_mp",
+           "ign_dataset_batch_get", "ign_dataset_batch_get_narrow", "ign_dataset_batch_destroy", "ign_plan_create_json", "ign_plan_describe_json", "ign_forward_train_begin", "ign_forward_train_mp",
            "ign_forward_train_end", "ign_backward_begin", "ign_backward_mp", "ign_backward_end",
            "ign_batch_train_buffers", "ign_batch_read_predictions", "ign_batch_resident_info"]
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 PART = {"all": 0, "interior": 1, "boundary": 2}
 
 
@@ -172,6 +173,7 @@ def _load():
         "ign_dataset_get": (C.c_int, [VP, C.c_char_p, P(i32), P(VP), P(i64), P(P(i64))]),
         "ign_dataset_batch_create": (C.c_int, [VP, P(i64), i32, P(VP)]),
         "ign_dataset_batch_get": (C.c_int, [VP, C.c_char_p, P(i32), P(VP), P(i64), P(P(i64))]),
+        "ign_dataset_batch_get_narrow": (C.c_int, [VP, C.c_char_p, P(i32), P(VP), P(i64), P(P(i64))]),
         "ign_dataset_batch_destroy": (None, [VP]),
         "ign_plan_create_json": (C.c_int, [C.c_char_p, C.c_char_p, i32, P(VP)]),
         "ign_plan_describe_json": (C.c_int, [VP, C.c_char_p, i64, P(i64)]),

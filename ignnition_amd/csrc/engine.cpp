@@ -1049,6 +1049,27 @@ static int resident_batch_k(ign_plan* p, ign_batch* b, int K) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// ign_batch_create's message lists for one (graph, source) of a plain MP (no interleave, attention or
+// axis-2 concat), T the desc's index type: false when an index is out of range (the caller's checked
+// loop then reports the first one)
+extern "C++" template <class T>
+static bool plain_messages(const T* __restrict as, const T* __restrict ad, const T* __restrict aq, int64_t n,
+                           int64_t nsrc, int64_t ndst, int64_t rd, int64_t rs, int64_t slot_off, uint32_t sb, bool net,
+                           int64_t e0, hvec<int32_t>& mdst, hvec<int32_t>& mpos, hvec<uint32_t>& mcode,
+                           int64_t* __restrict fl) {
+  bool bad = false;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t si = as[k], di = ad[k];
+    bad |= (uint64_t)si >= (uint64_t)nsrc || (uint64_t)di >= (uint64_t)ndst;
+    const int64_t dc = bad ? 0 : di;   // (no store outside the graph's flen range before the report)
+    mdst.push_back((int32_t)(rd + dc));
+    mpos.push_back((int32_t)(slot_off + (int64_t)aq[k]));
+    mcode.push_back(sb | (uint32_t)(net ? e0 + k : rs + si));
+    fl[dc] += 1;
+  }
+  return !bad;
+}
+
 int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   if (!p || !d || !out) return fail(IGN_ERR_INVALID, "null argument");
   *out = nullptr;
@@ -1097,6 +1118,15 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       if (n < 0) return fail(IGN_ERR_INVALID, "negative edge count");
       eoff[a][g + 1] = eoff[a][g] + n;
     }
+  std::vector<IdxArr> asrc(p->n_adj), adst(p->n_adj), aseq(p->n_adj), ilx(p->n_il);   // ABI 13: int32 or int64
+  if (d->index_bytes != 0 && d->index_bytes != 4 && d->index_bytes != 8)
+    return fail(IGN_ERR_INVALID, "index_bytes %d (0 / 8: int64 index arrays, 4: int32)", (int)d->index_bytes);
+  for (int a = 0; a < p->n_adj; ++a) {
+    asrc[a] = IdxArr(d->adj_src[a], d->index_bytes);
+    adst[a] = IdxArr(d->adj_dst[a], d->index_bytes);
+    aseq[a] = IdxArr(d->adj_seq[a], d->index_bytes);
+  }
+  for (int i = 0; i < p->n_il; ++i) ilx[i] = IdxArr(d->interleave_idx[i], d->index_bytes);
   std::vector<hvec<int64_t>> ioff(p->n_il, hvec<int64_t>(G + 1, 0));
   for (int i = 0; i < p->n_il; ++i)
     for (int g = 0; g < G; ++g) ioff[i][g + 1] = ioff[i][g] + d->interleave_len[(int64_t)g * p->n_il + i];
@@ -1124,6 +1154,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
   static const bool build_prof = env_flag("IGN_BUILD_PROF", false);
   std::vector<double> t_mp;   // IGN_BUILD_PROF: the time up to the end of each MP's tables
   const double t_mp0 = build_prof ? now_ms() : 0.0;
+  BuildMarks bm(env_flag("IGN_BUILD_PROF_FINE", false));   // IGN_BUILD_PROF_FINE=1: finer sections of each MP
   for (size_t mi = 0; mi < p->mps.size(); ++mi) {
     if (build_prof && mi > 0) t_mp.push_back(now_ms());
     const MPP& mp = p->mps[mi];
@@ -1156,7 +1187,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
             return fail(IGN_ERR_INVALID, "graph %d: interleave index lists have different lengths (%lld vs %lld;"
                         " tf.stack fails, GM:518)", g, (long long)len0, (long long)n);
           len0 = n;
-          for (int64_t k = ioff[il][g]; k < ioff[il][g + 1]; ++k) ilflat.push_back(d->interleave_idx[il][k]);
+          for (int64_t k = ioff[il][g]; k < ioff[il][g + 1]; ++k) ilflat.push_back(ilx[il][k]);
         }
       }
       int64_t total_slots = 0;
@@ -1169,7 +1200,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
                       " max(seq)+1 is undefined, GM:484-490)", g, a);
         int64_t mx = -1;
         for (int64_t k = e0; k < e1; ++k) {
-          int64_t sq = d->adj_seq[a][k];
+          int64_t sq = aseq[a][k];
           if (sq < 0) return fail(IGN_ERR_INVALID, "graph %d: negative seq value", g);
           mx = std::max(mx, sq);
         }
@@ -1198,12 +1229,31 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if (mp.aggr == IGN_AGGR_ATTENTION && s > 0) {
           lens_s.assign(ndst, 0);
           for (int64_t k = e0; k < e1; ++k) {
-            const int64_t di = d->adj_dst[a][k];
+            const int64_t di = adst[a][k];
             if (di >= 0 && di < ndst) lens_s[di]++;
           }
         }
+        if (mp.aggr != IGN_AGGR_INTERLEAVE && mp.aggr != IGN_AGGR_ATTENTION && !mp.feature_concat) {
+          // the common case (sum, ordered, convolution; no axis-2 concat): the loop below without its
+          // per-message branches on the MP's kind, whose fields it reloaded on every message (the
+          // stores may alias them), reading the desc's own index width.  An index out of range
+          // reruns the checked loop, which reports the first one.
+          const int64_t rd = b->row_off[dst][g], rs = b->row_off[se][g];
+          const uint32_t sb = (uint32_t)s << IGN_SLOT_SHIFT;
+          const bool net = !mp.nn[s].layers.empty();
+          const bool ok = d->index_bytes == 4
+              ? plain_messages(static_cast<const int32_t*>(asrc[a].p) + e0, static_cast<const int32_t*>(adst[a].p) + e0,
+                               static_cast<const int32_t*>(aseq[a].p) + e0, e1 - e0, nsrc, ndst, rd, rs, slot_off, sb,
+                               net, e0, mdst, mpos, mcode, flen.data() + rd)
+              : plain_messages(d->adj_src[a] + e0, d->adj_dst[a] + e0, d->adj_seq[a] + e0, e1 - e0, nsrc, ndst, rd, rs,
+                               slot_off, sb, net, e0, mdst, mpos, mcode, flen.data() + rd);
+          if (ok) {
+            slot_off += lmax[s];
+            continue;
+          }
+        }
         for (int64_t k = e0; k < e1; ++k) {
-          int64_t si = d->adj_src[a][k], di = d->adj_dst[a][k], sq = d->adj_seq[a][k];
+          int64_t si = asrc[a][k], di = adst[a][k], sq = aseq[a][k];
           if (si < 0 || si >= nsrc) return fail(IGN_ERR_INVALID, "graph %d: src index %lld out of range [0,%lld)", g, (long long)si, (long long)nsrc);
           if (di < 0 || di >= ndst) return fail(IGN_ERR_INVALID, "graph %d: dst index %lld out of range [0,%lld)", g, (long long)di, (long long)ndst);
           int64_t pos = slot_off + sq;
@@ -1256,8 +1306,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       hvec<int32_t> es(ne), ed(ne);
       for (int g = 0; g < G; ++g)
         for (int64_t k = eoff[a][g]; k < eoff[a][g + 1]; ++k) {
-          es[k] = (int32_t)(b->row_off[se][g] + d->adj_src[a][k]);
-          ed[k] = (int32_t)(b->row_off[dst][g] + d->adj_dst[a][k]);
+          es[k] = (int32_t)(b->row_off[se][g] + asrc[a][k]);
+          ed[k] = (int32_t)(b->row_off[dst][g] + adst[a][k]);
         }
       mb.n_edges[s] = ne;
       if ((rc = dev_upload(b.get(), &mb.d_edge_src[s], es)) || (rc = dev_upload(b.get(), &mb.d_edge_dst[s], ed))) return rc;
@@ -1275,6 +1325,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         mb.d_msg_layer[s].push_back(f);
       }
     }
+    bm.mark("messages");
     mb.edges = tot;
     b->edges_per_forward += tot * p->T;
     const CellP& cp = p->cells[mp.cell];
@@ -1288,6 +1339,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
           return fail(IGN_ERR_INVALID, "destination row %lld receives no message: the reference's sorted update"
                       " gathers position -1 (AUX:793-795)", (long long)r);
       sort_order(order, flen);
+      bm.mark("sort");
       // combined projected table: source s occupies rows [src_off[s], src_off[s] + rows_s)
       int64_t trow = 0;
       for (int s = 0; s < S; ++s) {
@@ -1346,6 +1398,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
           if (slot_of[k] >= 0 && multi_of[slot_of[k]] >= 0)
             multi_rows[fill[multi_of[slot_of[k]]]++] = (uint32_t)table_row(mcode[k]);
       }
+      bm.mark("slots");
       for (int64_t i = 0; i < ND; i += 16) mb.wave_steps += len[i];   // sorted: a tile's first row is its longest
       {   // the ordered update's tile headers: one 16-B load per position, no dependent code load
         const int64_t NDp = (ND + 15) / 16 * 16;
@@ -1359,6 +1412,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         }
         if ((rc = dev_upload(b.get(), &mb.d_seq_hdr, hdr))) return rc;
       }
+      bm.mark("headers");
       if (mb.zero_row + 1 + mb.n_multi >= (int64_t)UINT32_MAX) return fail(IGN_ERR_UNSUPPORTED, "MP too large");
       mb.n_steps = steps;
       mb.n_msgs = n_msgs;
@@ -1384,6 +1438,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       mb.flops = (double)steps * (2.0 * H * 3 * H + 14.0 * H);
       mb.bytes = (double)steps * (4.0 * H + 4) + (double)ND * 8.0 * H + 4.0 * (ND + 1);
       b->gru_steps += steps * p->T;
+      bm.mark("uploads");
     } else {
       sort_order(order, flen);
       // edge-cut partitions: destinations reading a halo row go last (they wait for the exchange)
@@ -1400,6 +1455,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
         if ((int64_t)(c & IGN_ROW_MASK) >= b->rows[se]) bnd[mdst[k]] = 1;
       }
       std::stable_partition(order.begin(), order.end(), [&](int32_t r) { return !bnd[r]; });
+      bm.mark("sort");
       mb.n_interior = std::count(bnd.begin(), bnd.end(), 0);
       hvec<int32_t> where(ND);
       for (int64_t i = 0; i < ND; ++i) where[order[i]] = (int32_t)i;
@@ -1482,6 +1538,7 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
       // destination's own in-degree, a property of its graph, so a graph's predictions stay bitwise
       // the same alone and in any batch (the two kernels add a destination's messages in different
       // orders), and the graph-resident forward takes the same order per row (resident.hip B1).
+      bm.mark("csr");
       const bool window = p->sum_window == 1;
       int64_t n_seg = 0;   // order is sorted by message count, descending: the segmented rows lead
       if (p->sum_window == 0 && ND > 0 && ptr[1] - ptr[0] >= kSegMinMessages)   // (order: by count, descending)
@@ -1571,7 +1628,9 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
 
   // readout buffers (the resident forward's tables are built by the first ign_forward: a batch that
   // only trains or steps MP by MP never pays for them)
+  bm.mark("mp-rest");
   if ((rc = readout_batch(p, b.get(), d))) return rc;
+  bm.mark("readout");
   const int64_t P = space_rows(p, b.get(), p->ro_t[p->ro_in[0]]);
   b->n_pred = P;
   b->out_units = p->dense.back().out;
@@ -1599,6 +1658,8 @@ int ign_batch_create(ign_plan* p, const ign_batch_desc* d, ign_batch** out) {
     fprintf(stderr, "[ign-build] batch sections:%s mp%zu+readout %.2f, resident tables %.2f ms\n", s.c_str(),
             t_mp.size(), t_res0 - prev, now_ms() - t_res0);
   }
+  bm.mark("alloc+resident");
+  bm.print("ign_batch_create fine");
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // every clear has landed before the batch is used
   HIP_TRY(upload_flush());                           // (and every staged copy)
   *out = b.release();

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdint>
@@ -414,6 +416,40 @@ hipStream_t upload_stream();
 hipError_t upload_bytes(void* dst, const void* src, size_t bytes);
 void host_cache_stats(int64_t* live, int64_t* idle, int64_t* maps, int64_t* unmaps);
 hipError_t upload_flush();   // wait for this thread's pending copies
+// one index array of an ign_batch_desc (adj_src / adj_dst / adj_seq / interleave_idx): int32
+// elements when the desc's index_bytes is 4 (ABI 13), else int64
+struct IdxArr {
+  const void* p = nullptr;
+  bool w32 = false;
+  IdxArr() = default;
+  IdxArr(const int64_t* q, int32_t index_bytes) : p(q), w32(index_bytes == 4) {}
+  int64_t operator[](int64_t k) const {
+    return w32 ? (int64_t) static_cast<const int32_t*>(p)[k] : static_cast<const int64_t*>(p)[k];
+  }
+};
+
+// IGN_BUILD_PROF=1: named host sections of one batch build (the time since the previous mark),
+// printed as one line at the end of the build
+struct BuildMarks {
+  bool on;
+  double last = 0;
+  std::string line;
+  static double now() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  explicit BuildMarks(bool enabled) : on(enabled), last(enabled ? now() : 0.0) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const double t = now();
+    char buf[96];
+    snprintf(buf, sizeof buf, " %s %.2f", what, t - last);
+    line += buf;
+    last = t;
+  }
+  void print(const char* head) const {
+    if (on) fprintf(stderr, "[ign-build] %s sections:%s\n", head, line.c_str());
+  }
+};
 struct UploadScope {
   explicit UploadScope(const char* what);
   ~UploadScope();

@@ -271,7 +271,7 @@ int readout_batch(ign_plan* p, ign_batch* b, const ign_batch_desc* d) {
         std::vector<int32_t> is(b->adj_rows[a]), id(b->adj_rows[a]);
         for (int g = 0; g < G; ++g)
           for (int64_t e = b->adj_off[a][g]; e < b->adj_off[a][g + 1]; ++e) {
-            const int64_t s = d->adj_src[a][e], t = d->adj_dst[a][e];
+            const int64_t s = IdxArr(d->adj_src[a], d->index_bytes)[e], t = IdxArr(d->adj_dst[a], d->index_bytes)[e];
             const int64_t ns = d->num_nodes[(int64_t)g * p->ents.size() + se];
             const int64_t nd = d->num_nodes[(int64_t)g * p->ents.size() + de];
             if (s < 0 || s >= ns || t < 0 || t >= nd)   // the reference logs and exits (AUX:1253-1263)

@@ -289,6 +289,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   int rc = ensure_device(p);
   if (rc) return rc;
   UploadScope scope("ign_batch_enable_training");
+  const char* fine = getenv("IGN_BUILD_PROF_FINE");
+  BuildMarks bm(fine && atoi(fine) != 0);   // IGN_BUILD_PROF_FINE=1: host sections of this build
   const int E = (int)p->ents.size();
   for (size_t c = 0; c < p->cells.size(); ++c) {
     const CellP& cp = p->cells[c];
@@ -477,6 +479,7 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         return rc;
     }
     t->mp.push_back(std::move(mt));
+    bm.mark(mi == 0 ? "mp0" : mi == 1 ? "mp1" : "mp2+");
   }
   if ((rc = talloc(t.get(), &t->ga, ga_n)) || (rc = talloc(t.get(), &t->gu, gu_n)) ||
       (rc = talloc(t.get(), &t->dx, dx_n)) || (rc = talloc(t.get(), &t->dtab, dtab_n)))
@@ -594,8 +597,11 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       t->defer.push_back(d);
     }
   }
+  bm.mark("rest");
   HIP_TRY(hipStreamSynchronize(upload_stream()));   // IGN_POOL_POISON fills have landed
   HIP_TRY(upload_flush());                           // (and every staged copy)
+  bm.mark("wait");
+  bm.print("ign_batch_enable_training fine");
   b->train = t.release();
   return IGN_OK;
 }

@@ -81,10 +81,12 @@ class NativeDataset:
         glen = np.ctypeslib.as_array(lens, shape=(max(G, 1),))[:G].copy()
         return vals.astype(np_t, copy=False), glen
 
-    def batch(self, ids, keys):
+    def batch(self, ids, keys, narrow=False):
         """BatchedGraphs holding ``keys`` for samples ``ids``, and the labels (or None).  Thread
         safe: the gather has buffers of its own (``ign_dataset_batch``), which the returned
-        arrays view without a copy and keep alive."""
+        arrays view without a copy and keep alive.  ``narrow``: integer keys as int32 arrays
+        (``ign_dataset_batch_get_narrow``; values that do not fit stay int64), half the bytes of
+        the gather and of the batch build's index reads (``ign_batch_desc.index_bytes``)."""
         ids = np.ascontiguousarray(np.asarray(ids, np.int64))
         h = C.c_void_p()
         check(lib.ign_dataset_batch_create(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), len(ids),
@@ -94,9 +96,9 @@ class NativeDataset:
 
         def get(key):
             dt, ptr, total, lens = C.c_int32(), C.c_void_p(), C.c_int64(), C.POINTER(C.c_int64)()
-            check(lib.ign_dataset_batch_get(owner.handle, key.encode(), C.byref(dt), C.byref(ptr), C.byref(total),
-                                            C.byref(lens)))
-            ctype, np_t = (C.c_float, np.float32) if dt.value == 0 else (C.c_int64, np.int64)
+            fn = lib.ign_dataset_batch_get_narrow if narrow and key != "__label__" else lib.ign_dataset_batch_get
+            check(fn(owner.handle, key.encode(), C.byref(dt), C.byref(ptr), C.byref(total), C.byref(lens)))
+            ctype, np_t = {0: (C.c_float, np.float32), 1: (C.c_int64, np.int64), 2: (C.c_int32, np.int32)}[dt.value]
             n = total.value
             if n == 0 or not ptr.value:
                 vals = np.zeros(0, np_t)

@@ -559,18 +559,23 @@ def batch_desc(p: "MPPlan", graphs, halo_rows: dict = None):
         if not (np.array_equal(ls, ld) and np.array_equal(ls, lq)):
             raise ValueError("%s/%s/%s have different lengths" % (ks, kd, kq))
         cnt[:, a] = ls
-        srcs.append(_i64(s)), dsts.append(_i64(d)), seqs.append(_i64(q))
+        srcs.append(s), dsts.append(d), seqs.append(q)
     I = len(p.il_slots)
     il_len = np.zeros((G, max(I, 1)), np.int64)
     ils = []
     for i, key in enumerate(p.il_slots):
         v, lens = bg.get(key)
         il_len[:, i] = lens
-        ils.append(_i64(v))
+        ils.append(v)
+    # index arrays: int32 as they come when every one is (the native reader's narrow gather,
+    # index_bytes = 4: no widening copy here, half the bytes the build reads), else all as int64
+    narrow = all(np.asarray(x).dtype == np.int32 for x in srcs + dsts + seqs + ils)
+    conv = (lambda x: np.ascontiguousarray(np.asarray(x).reshape(-1))) if narrow else _i64
+    srcs, dsts, seqs, ils = ([conv(x) for x in l] for l in (srcs, dsts, seqs, ils))
     fp = C.POINTER(C.c_float)
     lp = C.POINTER(C.c_int64)
     feat_ptrs = (fp * E)(*[f.ctypes.data_as(fp) if f is not None and f.size else fp() for f in feats])
-    mk = lambda arrs: (lp * max(len(arrs), 1))(*[a.ctypes.data_as(lp) for a in arrs])
+    mk = lambda arrs: (lp * max(len(arrs), 1))(*[C.cast(a.ctypes.data, lp) for a in arrs])
     prm_arrays = []
     for slot in p.adj_slots:
         key = "params_" + slot.adj
@@ -582,7 +587,7 @@ def batch_desc(p: "MPPlan", graphs, halo_rows: dict = None):
                                                                                  else fp() for a in prm_arrays]))
     desc = _lib.BatchDesc(G, num.ctypes.data_as(lp), ptrs[0], cnt.ctypes.data_as(lp), ptrs[1], ptrs[2], ptrs[3],
                           il_len.ctypes.data_as(lp), ptrs[4], halo.ctypes.data_as(lp) if halo is not None else lp(),
-                          ptrs[5])
+                          ptrs[5], 4 if narrow else 8)
     keep = (num, feats, cnt, srcs, dsts, seqs, il_len, ils, prm_arrays, halo, ptrs)
     return desc, keep, (G, E, num, cnt, halo)
 

@@ -161,7 +161,8 @@ class NativeInput:
         yield from _global_batches(id_stream(), self.batch_size, self.rank, self.world)
 
     def load(self, ids):
-        bg, labels = self.ds.batch(ids, self.keys)
+        # integer keys as int32 (the batch build reads them at that width: half the gather's bytes)
+        bg, labels = self.ds.batch(ids, self.keys, narrow=True)
         bg.sample_ids = list(ids)
         for f in self.feature_list:
             if str(f.normalization) != "None" and f.name in bg:

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define IGN_ABI_VERSION 12
+#define IGN_ABI_VERSION 13
 
 enum ign_status {
   IGN_OK = 0,
@@ -182,6 +182,10 @@ typedef struct {
   /* per adjacency: graph-concatenated params_<adj> [edges][param dim] (cast to float, GM:454-456),
    * needed by message networks that read edge_params; NULL entries / NULL array when absent */
   const float* const* adj_params;
+  /* ABI 13: the width of adj_src, adj_dst, adj_seq and interleave_idx's elements: 0 or 8 = int64_t
+   * (the pointer types above), 4 = int32_t (the pointers then point at int32_t arrays; the native
+   * reader's narrow gather, ign_dataset_batch_get_narrow, hands them over without a widening copy) */
+  int32_t index_bytes;
 }  ign_batch_desc;
 
 typedef struct {
@@ -393,7 +397,7 @@ void ign_dataset_close(ign_dataset* ds);
 int  ign_dataset_size(const ign_dataset* ds, int64_t* n_samples, int32_t* n_errors);
 const char* ign_dataset_error(const ign_dataset* ds, int32_t i);
 int  ign_dataset_gather(ign_dataset* ds, const int64_t* ids, int32_t count);
-/* dtype: 0 float32, 1 int64 */
+/* dtype: 0 float32, 1 int64 (2 int32: ign_dataset_batch_get_narrow only) */
 int  ign_dataset_get(ign_dataset* ds, const char* key, int32_t* dtype, const void** ptr, int64_t* total,
                      const int64_t** per_graph);
 /* The same gather as a batch object with its own buffers (pointers valid until it is destroyed):
@@ -403,6 +407,11 @@ typedef struct ign_dataset_batch ign_dataset_batch;
 int  ign_dataset_batch_create(const ign_dataset* ds, const int64_t* ids, int32_t count, ign_dataset_batch** out);
 int  ign_dataset_batch_get(ign_dataset_batch* batch, const char* key, int32_t* dtype, const void** ptr,
                            int64_t* total, const int64_t** per_graph);
+/* ABI 13: the same, with an integer key's values as int32 (dtype 2) when every sample's fit (the
+ * reader stores them so), else as int64 (dtype 1): half the bytes of the int64 concatenation, for
+ * ign_batch_desc.index_bytes = 4 */
+int  ign_dataset_batch_get_narrow(ign_dataset_batch* batch, const char* key, int32_t* dtype, const void** ptr,
+                                  int64_t* total, const int64_t** per_graph);
 void ign_dataset_batch_destroy(ign_dataset_batch* batch);
 
 #ifdef __cplusplus

@@ -460,6 +460,7 @@ const char* ign_oracle_last_error(void) { return g_err; }
 int ign_oracle_forward(const ign_plan_desc* p, const ign_batch_desc* d, const float* const* params, int32_t n_params,
                        float* out, int32_t threads, int32_t precision) {
   if (!p || !d || !params || !out) return err(IGN_ERR_INVALID, "null argument");
+  if (d->index_bytes == 4) return err(IGN_ERR_UNSUPPORTED, "oracle: int32 index arrays (ABI 13) are not read here");
   if (p->num_readout_ops) return err(IGN_ERR_UNSUPPORTED, "oracle: readout operations before predict are not restated in C++");
   if (p->num_readout_inputs < 1) return err(IGN_ERR_INVALID, "no predict inputs");
   Model m;

@@ -27,7 +27,7 @@ def test_every_header_symbol_exported():
 
 
 def test_abi_version_and_error_string():
-    assert _lib.lib.ign_abi_version() == _lib.ABI_VERSION == 12
+    assert _lib.lib.ign_abi_version() == _lib.ABI_VERSION == 13
     rc = _lib.lib.ign_plan_create(None, 0, None)
     assert rc == -1
     assert b"null" in _lib.lib.ign_last_error()

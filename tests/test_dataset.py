@@ -172,6 +172,32 @@ def test_recycled_gather_buffers_equal_fresh(tmp_path, monkeypatch):
     assert all(v.size for v in ref.values())
 
 
+def test_narrow_gather_equals_wide(tmp_path):
+    """``NativeDataset.batch(..., narrow=True)`` (``ign_dataset_batch_get_narrow``): the integer
+    keys as int32 with the int64 gather's values and per-graph lengths, float keys and labels
+    unchanged; the wide gather of the same batch still int64 (samples are stored narrow)."""
+    desc, dims, mi = workloads.model("qsize")
+    synthetic.write_tar_dataset(synthetic.dataset("nsfnet", 6, qsize=True), str(tmp_path), per_file=4)
+    ds = NativeDataset.for_model(str(tmp_path), mi)
+    keys = plan_keys(MPPlan.from_model_info(mi))
+    ids = [4, 0, 5, 2]
+    wide, yw = ds.batch(ids, keys)
+    nar, yn = ds.batch(ids, keys, narrow=True)
+    np.testing.assert_array_equal(yw[0], yn[0])
+    n_int = 0
+    for k in keys:
+        (vw, lw), (vn, ln) = wide.get(k), nar.get(k)
+        np.testing.assert_array_equal(lw, ln)
+        np.testing.assert_array_equal(vw, vn)
+        if vw.dtype == np.int64:
+            assert vn.dtype == np.int32, k
+            n_int += 1
+        else:
+            assert vn.dtype == vw.dtype == np.float32, k
+    assert n_int >= 6
+    ds.close()
+
+
 class _FakeBatch:
     def __init__(self, v):
         self.v, self.closed = v, False

@@ -878,3 +878,62 @@ def test_json_plan_forward_matches_python_plan(kind):
     e2.handle = h
     e2.set_params(prm)
     np.testing.assert_array_equal(Batch(e2, graphs).forward(), ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# ABI 13: int32 index arrays (ign_batch_desc.index_bytes = 4)
+def _narrowed(graphs):
+    from ignnition_amd.engine import BatchedGraphs
+    bg = BatchedGraphs.from_dicts(graphs)
+    return BatchedGraphs({k: (v.astype(np.int32) if v.dtype == np.int64 else v, lens)
+                          for k, (v, lens) in bg.arrays.items()}, bg.num_graphs)
+
+
+@pytest.mark.parametrize("case", ["routenet", "qsize", "extend_nn"])
+def test_int32_index_batches_equal_int64(case):
+    """A batch whose index arrays are int32 (index_bytes 4: the native reader's narrow gather hands
+    them over without widening) predicts bitwise what the int64 batch predicts: RouteNet, Q-size
+    (interleave indices) and a readout with extend_adjacencies (readout.cpp reads the desc too)."""
+    if case == "extend_nn":
+        ops, pin, nets = READOUT_CASES[case]
+        desc = model_examples.routenet_readout(ops, pin, nets, iterations=3)
+        _, dims, _ = workloads.model("routenet")
+        mi = Model_information(copy.deepcopy(desc), dims)
+        graphs, _ = workloads.graph_inputs(mi, [synthetic.routenet_sample("nsfnet" if g % 2 == 0 else "geant2", g)
+                                                for g in range(3)])
+    else:
+        desc, dims, mi, graphs, _ = workloads.make_batch_inputs(case, "geant2", 3)
+    plan = MPPlan.from_model_info(mi)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(5, bias_scale=0.1))
+    outs = []
+    for g in (graphs, _narrowed(graphs)):
+        b = Batch(eng, g)
+        outs.append(b.forward().reshape(-1).copy())
+        b.close()
+    eng.close()
+    assert outs[0].size > 0
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_native_narrow_gather_batches_equal_wide(tmp_path):
+    """The training input path (NativeInput.load: the native reader's narrow gather) builds batches
+    that predict bitwise what the wide (int64) gather's batches predict."""
+    from ignnition_amd.dataset import NativeDataset, plan_keys
+    desc, dims, mi = workloads.model("qsize")
+    synthetic.write_tar_dataset(synthetic.dataset("nsfnet", 5, qsize=True), str(tmp_path), per_file=3)
+    ds = NativeDataset.for_model(str(tmp_path), mi)
+    plan = MPPlan.from_model_info(mi)
+    keys = plan_keys(plan)
+    eng = Engine(plan, 0)
+    eng.set_params(plan.init_params(2, bias_scale=0.1))
+    outs = []
+    for narrow in (False, True):
+        bg, _ = ds.batch([3, 1, 4, 0], keys, narrow=narrow)
+        assert any(bg.get(k)[0].dtype == np.int32 for k in keys) == narrow
+        b = Batch(eng, bg)
+        outs.append(b.forward().reshape(-1).copy())
+        b.close()
+    eng.close()
+    ds.close()
+    np.testing.assert_array_equal(outs[0], outs[1])

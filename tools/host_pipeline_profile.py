@@ -46,7 +46,7 @@ def main():
         for rep in range(reps):
             ids = rng.permutation(n)
             t = [time.perf_counter()]
-            bg, labels = ds.batch(ids, keys)
+            bg, labels = ds.batch(ids, keys, narrow=os.environ.get("NARROW", "1") == "1")   # as NativeInput.load
             t.append(time.perf_counter())
             for f in mi.get_all_features():
                 if str(f.normalization) != "None" and f.name in bg:
