@@ -317,6 +317,7 @@ struct HostCache {
   std::mutex mu;
   std::map<size_t, std::vector<void*>> idle;   // by size class
   std::unordered_map<void*, bool> pinned;      // every live or idle block -> registered for DMA
+  std::unordered_map<void*, size_t> cls_of;    // every live or idle block -> its size class
   size_t idle_bytes = 0, live_bytes = 0;
   size_t cap = 0;
   int64_t n_map = 0, n_unmap = 0;   // IGN_BUILD_PROF: blocks mapped + pinned, and unpinned + unmapped
@@ -327,6 +328,7 @@ struct HostCache {
       if (it->second) hipHostUnregister(p);
       pinned.erase(it);
     }
+    cls_of.erase(p);
     munmap(p, cls);
     n_unmap++;
   }
@@ -348,15 +350,19 @@ void* host_block_alloc(size_t bytes) {
   HostCache& c = host_cache();
   const size_t cls = host_class(bytes);
   {
+    // an idle block of this class or of the next two (<= 1.5x): batches of one workload differ a
+    // little in size, and a miss maps and pins a new block (page faults + registration: the index
+    // tables' first MP took 12 -> 28 ms over four batches as blocks stranded one class up)
     std::lock_guard<std::mutex> g(c.mu);
-    auto it = c.idle.find(cls);
-    if (it != c.idle.end() && !it->second.empty()) {
-      void* p = it->second.back();
-      it->second.pop_back();
-      c.idle_bytes -= cls;
-      c.live_bytes += cls;
-      return p;
-    }
+    auto it = c.idle.lower_bound(cls);
+    for (int tried = 0; it != c.idle.end() && tried < 3 && it->first * 2 <= cls * 3; ++tried, ++it)
+      if (!it->second.empty()) {
+        void* p = it->second.back();
+        it->second.pop_back();
+        c.idle_bytes -= it->first;
+        c.live_bytes += it->first;
+        return p;
+      }
   }
   void* p = mmap(nullptr, cls, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (p == MAP_FAILED) return nullptr;
@@ -367,6 +373,7 @@ void* host_block_alloc(size_t bytes) {
   if (!reg) (void)hipGetLastError();
   std::lock_guard<std::mutex> g(c.mu);
   c.pinned[p] = reg;
+  c.cls_of[p] = cls;
   c.live_bytes += cls;
   c.n_map++;
   return p;
@@ -375,8 +382,9 @@ void* host_block_alloc(size_t bytes) {
 void host_block_free(void* p, size_t bytes) {
   if (!p) return;
   HostCache& c = host_cache();
-  const size_t cls = host_class(bytes);
   std::lock_guard<std::mutex> g(c.mu);
+  auto k = c.cls_of.find(p);
+  const size_t cls = k != c.cls_of.end() ? k->second : host_class(bytes);   // (a block may be one class up)
   c.idle[cls].push_back(p);
   c.idle_bytes += cls;
   c.live_bytes -= cls;

@@ -2069,7 +2069,10 @@ static void readout_h16_launch(const Readout3Args& args, const h8* w, hipStream_
 #ifndef IGN_READOUT_WAVES
 #define IGN_READOUT_WAVES 4
 #endif
-  constexpr int WAVES = IGN_READOUT_WAVES, RT = 2;   // RT = 1 (8 or 4 waves) measured slower: 0.59 / 0.69 ms
+#ifndef IGN_READOUT_RT
+#define IGN_READOUT_RT 2
+#endif
+  constexpr int WAVES = IGN_READOUT_WAVES, RT = IGN_READOUT_RT;   // RT = 1 (8 or 4 waves) measured slower: 0.59 / 0.69 ms
   auto k = args.save1 ? readout_h16_kernel<DIN, ACT, WAVES, RT, true> : readout_h16_kernel<DIN, ACT, WAVES, RT>;
   const int64_t groups = (args.n_rows + 16 * RT * WAVES - 1) / (16 * RT * WAVES);
   hipLaunchKernelGGL(k, dim3((unsigned)persistent_grid(k, groups, 64 * WAVES)), dim3(64 * WAVES), 0, st, args, w);
