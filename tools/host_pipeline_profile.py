@@ -42,6 +42,9 @@ def main():
     lock = threading.Lock()
 
     def work(seed):
+        if os.environ.get("PIN") == "1":   # this builder thread on one CPU of the process's set
+            cpus = sorted(os.sched_getaffinity(0))
+            os.sched_setaffinity(0, {cpus[seed % len(cpus)]})
         rng = np.random.default_rng(seed)
         for rep in range(reps):
             ids = rng.permutation(n)
