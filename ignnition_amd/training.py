@@ -217,6 +217,46 @@ class Trainer:
         self.model.set_params(params)
 
 
+def builder_cpus(workers: int) -> list:
+    """CPU sets for ``workers`` batch-builder threads (IGN_PIN_BUILDERS=1; default off): two CPUs each,
+    consecutive ones of the NUMA node the calling thread runs on, within the process's affinity
+    (local rank r of a multi-rank node takes the r-th slice).
+    A builder's index tables are memory-bound host work; a thread the scheduler moved across CCDs
+    and NUMA nodes between batches ran the ordered MP's message lists at 20-21 ms instead of
+    10 ms pinned (one builder, `r06_c22.sh`).  With eight builders on a shared host it measured
+    slower (24.0-26.6 against 19.0-23.9 ms per fresh-batch step, `r06_c23.sh`: the low CPUs it
+    picks are other tenants' too), hence off by default.  Empty sets (no pinning) when the switch
+    is off, the topology is unreadable, or the node has fewer than one CPU per builder."""
+    if os.environ.get("IGN_PIN_BUILDERS", "0") != "1" or not hasattr(os, "sched_getaffinity"):
+        return [set() for _ in range(workers)]
+    try:
+        allowed = os.sched_getaffinity(0)
+        with open("/proc/self/stat") as f:
+            cur = int(f.read().rsplit(")", 1)[1].split()[36])   # field 39: the CPU last run on
+        node = set(allowed)
+        for path in sorted(os.listdir("/sys/devices/system/node")):
+            if not path.startswith("node"):
+                continue
+            cpus = set()
+            with open("/sys/devices/system/node/%s/cpulist" % path) as f:
+                for part in f.read().strip().split(","):
+                    lo, _, hi = part.partition("-")
+                    cpus.update(range(int(lo), int(hi or lo) + 1))
+            if cur in cpus:
+                node = cpus & set(allowed)
+                break
+    except (OSError, ValueError, IndexError):
+        return [set() for _ in range(workers)]
+    cand = sorted(node)
+    # ranks of one node (torchrun's LOCAL_RANK) take disjoint slices; no pinning when they do not fit
+    lr = int(os.environ.get("LOCAL_RANK", "0") or 0)
+    per = 2 if len(cand) >= 2 * workers * (lr + 1) else 1 if len(cand) >= workers * (lr + 1) else 0
+    if per == 0:
+        return [set() for _ in range(workers)]
+    base = lr * workers * per
+    return [set(cand[base + per * i:base + per * i + per]) for i in range(workers)]
+
+
 class BatchPrefetcher:
     """The training input pipeline overlapped with the GPU (the role of tf.data's
     ``map(num_parallel_calls)`` + ``prefetch``, GM:181-192).  ``workers`` threads take the next
@@ -242,11 +282,17 @@ class BatchPrefetcher:
         self.end = None                       # sequence number of the end of the jobs
         self.next_out = 0
         self.stop = threading.Event()
-        self.threads = [threading.Thread(target=self._run, daemon=True) for _ in range(max(1, workers))]
+        cpus = builder_cpus(max(1, workers))
+        self.threads = [threading.Thread(target=self._run, args=(c,), daemon=True) for c in cpus]
         for t in self.threads:
             t.start()
 
-    def _run(self):
+    def _run(self, cpus=frozenset()):
+        if cpus:
+            try:
+                os.sched_setaffinity(0, cpus)   # this thread (Linux: pid 0 is the caller)
+            except OSError:
+                pass
         while True:
             while not self.slots.acquire(timeout=0.1):
                 if self.stop.is_set():

@@ -254,3 +254,26 @@ def test_batch_arrays_keep_their_buffers_alive(tmp_path):
     for _ in range(3):   # reuse the freed memory if it were freed
         ds.batch([2, 1, 0], keys)
     np.testing.assert_array_equal(arr, ref)
+
+
+def test_builder_cpus_are_disjoint_per_local_rank(monkeypatch):
+    """Batch-builder pinning (IGN_PIN_BUILDERS): each builder gets CPUs of the process's affinity,
+    local ranks take disjoint slices (or none when they do not fit), and the switch turns it off."""
+    import os
+    from ignnition_amd.training import builder_cpus
+    monkeypatch.setenv("IGN_PIN_BUILDERS", "1")
+    allowed = os.sched_getaffinity(0)
+    seen = set()
+    for lr in range(2):
+        monkeypatch.setenv("LOCAL_RANK", str(lr))
+        sets = builder_cpus(2)
+        assert len(sets) == 2
+        for c in sets:
+            assert c <= allowed
+            assert not (c & seen)
+            seen |= c
+    monkeypatch.setenv("LOCAL_RANK", "1000")
+    assert builder_cpus(2) == [set(), set()]
+    monkeypatch.setenv("IGN_PIN_BUILDERS", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    assert builder_cpus(3) == [set(), set(), set()]
