@@ -90,3 +90,30 @@ def test_compute_without_gpu_fails_loudly():
     with pytest.raises(_lib.EngineError) as ei:
         Engine(_plan("routenet")).set_params(_plan("routenet").init_params(0))
     assert ei.value.code == -3
+
+
+def test_batch_desc_index_width():
+    """ABI 13: batch_desc passes int32 index arrays through (index_bytes 4, no widening copy) when
+    every one of them is int32, and widens all of them to int64 (index_bytes 8) otherwise."""
+    import numpy as np
+    from ignnition_amd import workloads
+    from ignnition_amd.engine import BatchedGraphs, MPPlan, batch_desc
+    desc, dims, mi, graphs, _ = workloads.make_batch_inputs("qsize", "nsfnet", 2)
+    plan = MPPlan.from_model_info(mi)
+    bg = BatchedGraphs.from_dicts(graphs)
+    ints = [k for k, (v, _) in bg.arrays.items() if v.dtype == np.int64]
+    narrow = BatchedGraphs({k: (v.astype(np.int32) if k in ints else v, l) for k, (v, l) in bg.arrays.items()}, 2)
+    d8, keep8, _ = batch_desc(plan, bg)
+    d4, keep4, _ = batch_desc(plan, narrow)
+    assert d8.index_bytes == 8 and d4.index_bytes == 4
+    srcs4 = keep4[3]
+    assert srcs4 and all(a.dtype == np.int32 for a in srcs4)
+    assert all(np.shares_memory(a, narrow.get(k)[0]) for a, k in zip(srcs4, [s.keys[0] for s in plan.adj_slots]))
+    mixed = dict(narrow.arrays)
+    k0 = plan.adj_slots[0].keys[0]
+    mixed[k0] = (bg.get(k0)[0], bg.get(k0)[1])   # one int64 array among int32 ones
+    dm, keepm, _ = batch_desc(plan, BatchedGraphs(mixed, 2))
+    assert dm.index_bytes == 8
+    assert all(a.dtype == np.int64 for arrs in (keepm[3], keepm[4], keepm[5], keepm[7]) for a in arrs)
+    for a4, a8 in zip(keep4[3] + keep4[4] + keep4[5] + keep4[7], keep8[3] + keep8[4] + keep8[5] + keep8[7]):
+        np.testing.assert_array_equal(a4, a8)
