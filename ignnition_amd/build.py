@@ -17,7 +17,7 @@ OUT = os.path.join(HERE, "libignmp.so")
 # the resident kernel's phase-A instruction mix (tools/isa_mix.py), read by bench.py's roofline.issue
 ISA_MIX = os.path.join(HERE, "isa_mix.json")
 SOURCES = ["engine.cpp", "devpool.cpp", "train.cpp", "readout.cpp", "dataset.cpp", "plan_json.cpp", "kernels.hip", "kernels_bf.hip",
-           "train_kernels.hip", "readout_kernels.hip", "resident.hip", "readout_h32.hip"]
+           "train_kernels.hip", "readout_kernels.hip", "resident.hip", "readout_h32.hip", "train_csr.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-unused-value"]
 EXTRA = {"kernels_bf.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "resident.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
          "readout_h32.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}

@@ -296,3 +296,14 @@ struct MsgGatherArgs {
 };
 hipError_t launch_msg_gather(const MsgGatherArgs& a, hipStream_t st);
 hipError_t launch_pack_dense_pad(const float* W, float* Wp, int IN, int IN_pad, int OUT, hipStream_t st);
+
+// train_csr.hip: the training tables' transposed CSRs by a stable radix sort on the device
+size_t tcsr_temp_bytes(int64_t n);
+hipError_t launch_tcsr_keys_seq(const uint32_t* step_code, int64_t n_steps, uint32_t zero_row, uint32_t* keys,
+                                int32_t* vals, hipStream_t st);
+hipError_t launch_tcsr_keys_sum(const int32_t* msg_ptr, const int32_t* order, int64_t n_dst, const uint32_t* msg_src,
+                                uint32_t* keys, int32_t* vals, hipStream_t st);
+hipError_t launch_tcsr_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                            const int32_t* vals_in, int32_t* vals_out, int64_t n, uint32_t max_key, hipStream_t st);
+hipError_t launch_tcsr_ptr(const uint32_t* sorted_keys, int64_t n, uint32_t key0, int64_t rows, int32_t* ptr,
+                           hipStream_t st);

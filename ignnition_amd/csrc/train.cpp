@@ -132,6 +132,55 @@ int talloc(TrainState* t, float** out, int64_t n) {
   return IGN_OK;
 }
 
+// The transposed CSRs of MP mb on the GPU (train_csr.hip; IGN_TRAIN_CSR_GPU=0: build_csrs on the
+// host): a stable radix sort of the step (seq) or message keys on the upload stream, the same
+// arrays as the host's.  ptr[s]: row pointers of source slot s into idx, the sorted values every
+// slot shares.  The keys and the sort's scratch go back to the pool behind a fence.
+int tcsr_gpu(TrainState* t, const MPB& mb, int S, const int64_t* tkeys, bool seq, std::vector<int32_t*>& ptr,
+             int32_t*& idx) {
+  hipStream_t st = upload_stream();
+  const int64_t n = seq ? mb.n_steps : mb.n_msgs;
+  int rc;
+  float* f = nullptr;
+  if ((rc = talloc(t, &f, std::max<int64_t>(n, 1)))) return rc;
+  idx = reinterpret_cast<int32_t*>(f);
+  ptr.assign(S, nullptr);
+  for (int s = 0; s < S; ++s) {
+    if ((rc = talloc(t, &f, tkeys[s] + 1))) return rc;
+    ptr[s] = reinterpret_cast<int32_t*>(f);
+  }
+  const size_t nb = (size_t)std::max<int64_t>(n, 1) * 4, tb = tcsr_temp_bytes(std::max<int64_t>(n, 1));
+  std::vector<void*> scratch(4, nullptr);
+  for (int k = 0; k < 4; ++k) {
+    const hipError_t e = pool_alloc(t->pool, &scratch[k], k < 3 ? nb : std::max<size_t>(tb, 256), false);
+    if (e != hipSuccess) {
+      scratch.resize(k);
+      pool_release(t->pool, scratch, st);
+      return fail(IGN_ERR_OOM, "training CSR scratch: device alloc: %s", hipGetErrorString(e));
+    }
+  }
+  uint32_t* keys_in = static_cast<uint32_t*>(scratch[0]);
+  uint32_t* keys_out = static_cast<uint32_t*>(scratch[1]);
+  int32_t* vals_in = static_cast<int32_t*>(scratch[2]);
+  uint32_t max_key = 0;
+  hipError_t e;
+  if (seq) {
+    e = launch_tcsr_keys_seq(mb.d_step_code, n, (uint32_t)mb.zero_row, keys_in, vals_in, st);
+    max_key = (uint32_t)mb.zero_row;
+  } else {
+    e = launch_tcsr_keys_sum(mb.d_msg_ptr, mb.d_order, mb.n_dst, mb.d_msg_src, keys_in, vals_in, st);
+    max_key = ((uint32_t)(S - 1) << IGN_SLOT_SHIFT) | IGN_ROW_MASK;
+  }
+  if (e == hipSuccess) e = launch_tcsr_sort(scratch[3], tb, keys_in, keys_out, vals_in, idx, n, max_key, st);
+  for (int s = 0; s < S && e == hipSuccess; ++s) {
+    const uint32_t key0 = seq ? (uint32_t)mb.src_off[s] : (uint32_t)s << IGN_SLOT_SHIFT;
+    e = launch_tcsr_ptr(keys_out, n, key0, tkeys[s], ptr[s], st);
+  }
+  pool_release(t->pool, scratch, st);
+  if (e != hipSuccess) return fail(IGN_ERR_DEVICE, "training CSR sort: %s", hipGetErrorString(e));
+  return IGN_OK;
+}
+
 template <typename T, typename A>
 int tupload(TrainState* t, T** out, const std::vector<T, A>& h) {
   void* p = nullptr;
@@ -289,6 +338,8 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
   int rc = ensure_device(p);
   if (rc) return rc;
   UploadScope scope("ign_batch_enable_training");
+  const char* tcsr_env = getenv("IGN_TRAIN_CSR_GPU");
+  const bool tcsr_on = !tcsr_env || atoi(tcsr_env) != 0;   // the transposed CSRs on the GPU (train_csr.hip)
   const char* fine = getenv("IGN_BUILD_PROF_FINE");
   BuildMarks bm(fine && atoi(fine) != 0);   // IGN_BUILD_PROF_FINE=1: host sections of this build
   const int E = (int)p->ents.size();
@@ -334,8 +385,10 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
     const CellP& cp = p->cells[mp.cell];
     const int H = cp.H, DIN = mp.din, S = (int)mp.src.size();
     MPTrain mt;
-    // transposed CSRs (source row -> steps / destinations reading it), built below
+    // transposed CSRs (source row -> steps / destinations reading it), built below: on the GPU
+    // (mt.tptr, gidx) or on the host (tptr, tidx, uploaded with the slots below)
     std::vector<hvec<int32_t>> tptr, tidx;
+    int32_t* gidx = nullptr;
     int64_t tkeys[IGN_MAX_SLOTS] = {0, 0, 0, 0};
     for (int s = 0; s < S; ++s)
       tkeys[s] = mp.nn[s].layers.empty() ? b->rows[mp.src[s].entity] + b->halo[mp.src[s].entity] : mb.n_edges[s];
@@ -358,7 +411,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         HIP_TRY(launch_seq_bwd_hdr(mb.d_seq_hdr, mb.d_step_code, n_pos, mt.hdrb, upload_stream()));
       }
       // source row -> steps whose input contains it (directly or through a pre-summed row)
-      build_csrs(S, tkeys, [&](auto&& emit) {
+      if (tcsr_on && mb.n_multi == 0) {
+        if ((rc = tcsr_gpu(t.get(), mb, S, tkeys, true, mt.tptr, gidx))) return rc;
+      } else build_csrs(S, tkeys, [&](auto&& emit) {
         auto add_row = [&](uint32_t trow, int32_t step) {
           for (int s = S - 1; s >= 0; --s)
             if ((int64_t)trow >= mb.src_off[s]) {
@@ -428,7 +483,9 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
         dtab_n = std::max(dtab_n, 2 * mb.n_dst * DIN);   // du and d(sum) of the convolution
         need_part(mb.n_dst, DIN, DIN);
       }
-      build_csrs(S, tkeys, [&](auto&& emit) {
+      if (tcsr_on) {
+        if ((rc = tcsr_gpu(t.get(), mb, S, tkeys, false, mt.tptr, gidx))) return rc;
+      } else build_csrs(S, tkeys, [&](auto&& emit) {
         for (int64_t pos = 0; pos < mb.n_dst; ++pos)
           for (int32_t m = mb.h_msg_ptr[pos]; m < mb.h_msg_ptr[pos + 1]; ++m) {
             const uint32_t code = mb.h_msg_src[m];
@@ -445,10 +502,14 @@ int ign_batch_enable_training(ign_plan* p, ign_batch* b) {
       const int se = mp.src[s].entity;
       const MsgNN& nn = mp.nn[s];
       const int64_t rows_s = tkeys[s];
-      int32_t *dp = nullptr, *di = nullptr;
-      if ((rc = tupload(t.get(), &dp, tptr[s])) || (rc = tupload(t.get(), &di, tidx[s]))) return rc;
-      mt.tptr.push_back(dp);
-      mt.tidx.push_back(di);
+      if (gidx) {
+        mt.tidx.push_back(gidx);   // (mt.tptr[s] set by tcsr_gpu)
+      } else {
+        int32_t *dp = nullptr, *di = nullptr;
+        if ((rc = tupload(t.get(), &dp, tptr[s])) || (rc = tupload(t.get(), &di, tidx[s]))) return rc;
+        mt.tptr.push_back(dp);
+        mt.tidx.push_back(di);
+      }
       mt.trows.push_back(rows_s);
       if (nn.layers.empty()) continue;
       // message network (GM:440-475): buffers for its backward, and the state row -> edge CSRs

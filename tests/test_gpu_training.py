@@ -516,3 +516,18 @@ def test_pooled_buffers_reused_and_poisoned(monkeypatch, kind):
     np.testing.assert_array_equal(g.cpu().numpy(), g0)
     b.close()
     eng.trim_cache()
+
+
+@pytest.mark.parametrize("kind,topo,n", [("routenet", "synth50", 4), ("qsize", "geant2", 3), ("routenet", "nsfnet", 5)])
+def test_gpu_transposed_csrs_equal_host(monkeypatch, kind, topo, n):
+    """The training tables' transposed CSRs built on the GPU (train_csr.hip, a stable radix sort;
+    the default) and on the host (IGN_TRAIN_CSR_GPU=0): the same gradients, bitwise -- the sort
+    keeps every row's steps / destinations in the host's emission order.  Q-size: two source slots
+    of its sum MP and an interleaved ordered MP."""
+    desc, dims, mi, graphs, labels = workloads.make_batch_inputs(kind, topo, n)
+    prm = MPPlan.from_model_info(mi).init_params(17, bias_scale=0.1)
+    g_gpu = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    monkeypatch.setenv("IGN_TRAIN_CSR_GPU", "0")
+    g_host = _engine_grads(desc, dims, graphs, labels, prm)[5].cpu().numpy()
+    assert np.abs(g_host).sum() > 0
+    np.testing.assert_array_equal(g_gpu, g_host)

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 python -m ignnition_amd.build > /dev/null
 mkdir -p ignnition_amd/ab/obj_$NAME
 pids=""
-for SRC in kernels.hip kernels_bf.hip train_kernels.hip readout_kernels.hip resident.hip readout_h32.hip; do
+for SRC in kernels.hip kernels_bf.hip train_kernels.hip readout_kernels.hip resident.hip readout_h32.hip train_csr.hip; do
   EXTRA=""
   { [ "$SRC" = kernels_bf.hip ] || [ "$SRC" = resident.hip ] || [ "$SRC" = readout_h32.hip ]; } && EXTRA="-mllvm -amdgpu-mfma-vgpr-form"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Wno-unused-value $EXTRA $DEFS \
