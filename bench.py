@@ -511,7 +511,7 @@ def main():
             batches = trainer.prefetch(source.ids(), depth=args.input_workers + 1, workers=args.input_workers,
                                        load=source.load)
 
-        pipe_t = {"wait_s": 0.0, "step_s": 0.0, "steps": 0}
+        pipe_t = {"wait_s": 0.0, "step_s": 0.0, "steps": 0, "waits": []}
 
         def step():   # train_and_evaluate's loop (FO:108-166): next batch from the pipeline, one step
             t0 = time.perf_counter()
@@ -520,6 +520,7 @@ def main():
             # as framework_operations.train_and_evaluate: the loss reaches the host on logged steps only
             trainer.train_prepared(*nb, want_loss=pipe_t["steps"] % 10 == 0)
             pipe_t["wait_s"] += t1 - t0
+            pipe_t["waits"].append(t1 - t0)
             pipe_t["step_s"] += time.perf_counter() - t1
             pipe_t["steps"] += 1
         pipe_t["trainer"] = trainer
@@ -718,8 +719,10 @@ def main():
         line[edge_cut_key(args.edge_cut_nodes)] = edge_cut
     if fresh_stats and fresh_stats["steps"]:
         n = fresh_stats["steps"]   # warm-up included
+        timed = fresh_stats["waits"][-args.steps:]   # the timed steps only (the warm-up fills the pipeline)
         line["input_pipeline"] = {"workers": 0 if args.no_prefetch else args.input_workers,
-                                  "ms_waiting_for_batch": round(1e3 * fresh_stats["wait_s"] / n, 2),
+                                  "ms_waiting_for_batch": round(1e3 * sum(timed) / max(len(timed), 1), 2),
+                                  "ms_waiting_for_batch_incl_warmup": round(1e3 * fresh_stats["wait_s"] / n, 2),
                                   "ms_in_step": round(1e3 * fresh_stats["step_s"] / n, 2), "steps": n,
                                   "host_cpus_granted": int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None}
         sp = getattr(fresh_stats.get("trainer"), "step_prof", None)
