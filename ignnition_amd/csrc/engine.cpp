@@ -571,7 +571,8 @@ int ign_plan_create(const ign_plan_desc* d, int32_t device, ign_plan** out) {
       pk = align(pk + 3LL * dp.in * dp.out / 2);
       if (l == 1) {
         dp.pk_h = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64);
-        dp.pk_h32 = pk; pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64);
+        if (p->readout_variant == 5)   // (otherwise neither packed after each optimizer step nor allocated)
+          dp.pk_h32 = pk, pk = align(pk + (int64_t)dp.in * dp.out + 64 + (int64_t)p->dense[0].in * dp.in + 64);
       }
     }
     if (dense_bf_supported(dp.in, dp.out)) {
