@@ -169,7 +169,8 @@ int tcsr_gpu(TrainState* t, const MPB& mb, int S, const int64_t* tkeys, bool seq
     max_key = (uint32_t)mb.zero_row;
   } else {
     e = launch_tcsr_keys_sum(mb.d_msg_ptr, mb.d_order, mb.n_dst, mb.d_msg_src, keys_in, vals_in, st);
-    max_key = ((uint32_t)(S - 1) << IGN_SLOT_SHIFT) | IGN_ROW_MASK;
+    // one slot: the codes are the rows (radix passes over the row bits only); else slot bits above
+    max_key = S == 1 ? (uint32_t)std::max<int64_t>(tkeys[0], 1) : ((uint32_t)(S - 1) << IGN_SLOT_SHIFT) | IGN_ROW_MASK;
   }
   if (e == hipSuccess) e = launch_tcsr_sort(scratch[3], tb, keys_in, keys_out, vals_in, idx, n, max_key, st);
   for (int s = 0; s < S && e == hipSuccess; ++s) {
