@@ -649,7 +649,10 @@ __global__ __launch_bounds__(256) void sum_gru_bwd_kernel(SumBwdArgs a) {
 // batched tail: a RouteNet path (~3 links) was a 4-batch and single rows, each a dependent
 // idx -> row round trip; the link-update backward's gather 114 -> 98 us, 16.60 -> 16.43 ms per
 // training step (same box, tools/gpu_calls/r05_c54.sh)
-template <int V, bool NT = false>
+#ifndef IGN_GATHER_BATCH   // rows per batch in flight; 16 measured slower: 16.06-16.16 against
+#define IGN_GATHER_BATCH 8   // 15.65-15.72 ms per training step, same box (r06_c29.sh), the same bits
+#endif
+template <int V, bool NT = false, int GB = IGN_GATHER_BATCH>
 __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, const int32_t* __restrict__ ptr,
                                       const int32_t* __restrict__ idx, const float* __restrict__ in, int cols,
                                       int accumulate) {
@@ -662,20 +665,20 @@ __global__ void csr_gather_add_kernel(float* __restrict__ out, int64_t n_rows, c
 #pragma unroll
     for (int w = 0; w < V; ++w) acc[w] = accumulate ? ld4(out + r * cols + c + 4 * w) : f4{0, 0, 0, 0};
     const int k1 = ptr[r + 1];
-    for (int k = ptr[r]; k < k1; k += 8) {
-      int i8[8];
+    for (int k = ptr[r]; k < k1; k += GB) {
+      int i8[GB];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) i8[u] = idx[min(k + u, k1 - 1)];
-      f4 v8[8][V];
+      for (int u = 0; u < GB; ++u) i8[u] = idx[min(k + u, k1 - 1)];
+      f4 v8[GB][V];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < GB; ++u)
 #pragma unroll
         for (int w = 0; w < V; ++w) {
           const float* pv = in + (int64_t)i8[u] * cols + c + 4 * w;
           v8[u][w] = NT ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(pv)) : ld4(pv);
         }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < GB; ++u)
         if (k + u < k1) {
 #pragma unroll
           for (int w = 0; w < V; ++w) acc[w] += v8[u][w];
